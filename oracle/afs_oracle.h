@@ -1,0 +1,104 @@
+/*
+ * afs_oracle.h -- CPU restatement of the reference hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (areafunctionsynthesis_amd/,
+ * include/) links, loads or calls this code.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may use it, and only as the checker.
+ *
+ * What it restates (reference = /root/reference, file:line):
+ *   Synthesizer::synthesizeSignalTds          src/Backend/Synthesizer.cpp:515-639
+ *   Tube (static geometry, interpolate, ...)  src/Backend/Tube.cpp:46-654
+ *   TriangularGlottis (calcGeometry/incTime)  src/Backend/TriangularGlottis.cpp:154-576
+ *   TdsModel (proceedTimeStep and stages)     src/Backend/TdsModel.cpp:67-2385
+ *   IirFilter (run, one-pole, Chebyshev)      src/Backend/IirFilter.cpp:47-432
+ *   glibc random_r TYPE_3 (rand()/srand())    glibc 2.35 stdlib/random_r.c (the
+ *                                             reference calls rand() at
+ *                                             src/Backend/TdsModel.cpp:1690-1692)
+ *   OneDimAreaFunction (area fn -> tube)      src/Backend/OneDimAreaFunction.cpp:23-138
+ *
+ * Parity pin: the restatement is checked bit-for-bit against oracle/_ref, a build of
+ * the reference's own TdsModel/Tube/TriangularGlottis/IirFilter sources driven by
+ * oracle/ref_harness.cpp (tests/test_oracle_vs_ref.py), and against the committed
+ * golden vectors in tests/golden/ that the same reference build produced.
+ * OneDimAreaFunction is not buildable from the reference (it needs wxWidgets'
+ * generated setup.h); that row is pinned by the restatement and its tests only.
+ */
+#ifndef AFS_ORACLE_H
+#define AFS_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AO_NUM_PM 40          /* Tube::NUM_PHARYNX_MOUTH_SECTIONS, Tube.h:56 */
+#define AO_NUM_GLOTTIS_PARAMS 6 /* TriangularGlottis::NUM_CONTROL_PARAMS */
+
+/* One synthesis frame = the arguments of one synthesizeSignalTds() call:
+ * the dynamic part of the Tube plus the six glottis control parameters.
+ * Byte layout is identical to afs_frame in include/afs.h (1072 bytes). */
+typedef struct ao_frame {
+  double area_cm2[AO_NUM_PM];
+  double length_cm[AO_NUM_PM];
+  double laterality[AO_NUM_PM];
+  double teeth_position_cm;
+  double velum_opening_cm2;
+  double glottis[AO_NUM_GLOTTIS_PARAMS];
+  uint8_t articulator[AO_NUM_PM];
+  uint8_t pad_[8];
+} ao_frame;
+
+/* TdsModel::Options (TdsModel.h:83-95); defaults of TdsModel.cpp:35-44. */
+typedef struct ao_options {
+  int turbulence_losses;        /* 1 */
+  int soft_walls;               /* 1 */
+  int generate_noise_sources;   /* 1 */
+  int radiation_from_skin;      /* 1 */
+  int piriform_fossa;           /* 0 */
+  int inner_length_corrections; /* 1 */
+} ao_options;
+
+void ao_default_options(ao_options *o);
+
+/* Opaque single-utterance synthesizer (one Synthesizer + TdsModel + glottis). */
+typedef struct ao_synth ao_synth;
+
+ao_synth *ao_create(double fs_hz, uint32_t seed, const ao_options *opt);
+void ao_destroy(ao_synth *s);
+/* synthesizeSignalTds(newTube, glottis, n, out): the first call only latches the
+ * frame (Synthesizer.cpp:522-532) and returns 0; later calls produce max(n,1)
+ * samples into out and return that count. */
+int ao_synthesize_call(ao_synth *s, const ao_frame *frame, int n, double *out);
+
+/* Introspection after the latest sample (for per-step fixtures). */
+int ao_position(const ao_synth *s);
+void ao_get_pressures(const ao_synth *s, double *p93);
+void ao_get_currents(const ao_synth *s, double *u97);
+void ao_get_state(const ao_synth *s, double *buf, int *len); /* flat dump */
+long ao_rng_calls(const ao_synth *s);
+
+/* Whole utterance: latch frames[0], then (F-1) calls of hop samples.
+ * out must hold (F-1)*hop doubles.  Returns the number of samples. */
+long ao_synthesize_utterance(const ao_frame *frames, int num_frames, int hop,
+                             uint32_t seed, double fs_hz, const ao_options *opt,
+                             double *out);
+
+/* glibc TYPE_3 generator restatement (srand/rand semantics). */
+typedef struct ao_rng { int32_t r[31]; int f; } ao_rng;
+void ao_rng_seed(ao_rng *g, uint32_t seed);
+int32_t ao_rng_next(ao_rng *g);
+
+/* OneDimAreaFunction: 16 parameters (OneDimAreaFunction.h:34-43) -> the pharynx/
+ * mouth part of a frame (area, length, articulator, laterality, teeth).
+ * Velum and glottis fields are left untouched. */
+void ao_af_to_frame(const double params16[16], ao_frame *f);
+double ao_af_area(const double params16[16], double x_cm);
+
+/* IirFilter::createChebyshev (IirFilter.cpp:286-432): a[0..order], b[0..order]. */
+int ao_chebyshev(double cutoff_ratio, int highpass, int poles, double *a, double *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

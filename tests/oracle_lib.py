@@ -1,0 +1,204 @@
+"""ctypes access to the two CHECKERS built by oracle/Makefile.
+
+* ``Oracle``  -> oracle/_build/liboracle.so : our C restatement of the reference path.
+* ``RefLib``  -> oracle/_ref/libafsref.so   : the reference's own sources + harness.
+
+Test infrastructure only (see oracle/afs_oracle.h).  Neither library is used by the
+product; tests call them to produce expected values.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from areafunctionsynthesis_amd.frames import FRAME_DTYPE
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libafsref.so")
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_vp = ctypes.c_void_p
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def build_oracle() -> None:
+    """Build the restatement (and the reference build when /root/reference exists)."""
+    targets = ["oracle"]
+    if os.path.isdir("/root/reference/src/Backend"):
+        targets.append("ref")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")] + targets)
+
+
+class Oracle:
+    """Restatement: one utterance at a time (batch 1), fp64."""
+
+    def __init__(self, path: str = ORACLE_SO):
+        if not os.path.exists(path):
+            build_oracle()
+        lib = ctypes.CDLL(path)
+        lib.ao_create.restype = _vp
+        lib.ao_create.argtypes = [ctypes.c_double, ctypes.c_uint32, _vp]
+        lib.ao_destroy.argtypes = [_vp]
+        lib.ao_synthesize_call.restype = ctypes.c_int
+        lib.ao_synthesize_call.argtypes = [_vp, _vp, ctypes.c_int, _vp]
+        lib.ao_synthesize_utterance.restype = ctypes.c_long
+        lib.ao_synthesize_utterance.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
+                                                ctypes.c_double, _vp, _vp]
+        lib.ao_get_pressures.argtypes = [_vp, _vp]
+        lib.ao_get_currents.argtypes = [_vp, _vp]
+        lib.ao_get_state.argtypes = [_vp, _vp, ctypes.POINTER(ctypes.c_int)]
+        lib.ao_position.argtypes = [_vp]
+        lib.ao_position.restype = ctypes.c_int
+        lib.ao_rng_calls.argtypes = [_vp]
+        lib.ao_rng_calls.restype = ctypes.c_long
+        lib.ao_rng_seed.argtypes = [_vp, ctypes.c_uint32]
+        lib.ao_rng_next.argtypes = [_vp]
+        lib.ao_rng_next.restype = ctypes.c_int32
+        lib.ao_af_to_frame.argtypes = [_vp, _vp]
+        lib.ao_af_area.argtypes = [_vp, ctypes.c_double]
+        lib.ao_af_area.restype = ctypes.c_double
+        lib.ao_chebyshev.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int, _vp, _vp]
+        lib.ao_chebyshev.restype = ctypes.c_int
+        self.lib = lib
+
+    def utterance(self, frames: np.ndarray, hop: int, seed: int, fs: float) -> np.ndarray:
+        frames = np.ascontiguousarray(frames, dtype=FRAME_DTYPE)
+        F = frames.shape[0]
+        out = np.zeros((F - 1) * hop, dtype=np.float64)
+        n = self.lib.ao_synthesize_utterance(_ptr(frames), F, hop, seed, fs, None, _ptr(out))
+        assert n == out.size
+        return out
+
+    def batch(self, frames: np.ndarray, hop: int, seeds, fs: float) -> np.ndarray:
+        B, F = frames.shape
+        out = np.zeros((B, (F - 1) * hop), dtype=np.float64)
+        for u in range(B):
+            out[u] = self.utterance(frames[u], hop, int(seeds[u]), fs)
+        return out
+
+    def rand_stream(self, seed: int, n: int) -> np.ndarray:
+        buf = ctypes.create_string_buffer(31 * 4 + 8)
+        self.lib.ao_rng_seed(buf, seed)
+        return np.array([self.lib.ao_rng_next(buf) for _ in range(n)], dtype=np.int64)
+
+    def af_to_frame(self, params16) -> np.ndarray:
+        p = np.ascontiguousarray(params16, dtype=np.float64)
+        f = np.zeros((), dtype=FRAME_DTYPE)
+        self.lib.ao_af_to_frame(_ptr(p), f.ctypes.data_as(ctypes.c_void_p))
+        return f
+
+    def chebyshev(self, ratio: float, poles: int, highpass: bool = False):
+        a = np.zeros(33)
+        b = np.zeros(33)
+        n = self.lib.ao_chebyshev(ratio, int(highpass), poles, _ptr(a), _ptr(b))
+        return a[: n + 1], b[: n + 1]
+
+    # step-level access -------------------------------------------------------
+    def create(self, fs: float, seed: int):
+        return self.lib.ao_create(fs, seed, None)
+
+    def call(self, h, frame: np.ndarray, n: int) -> np.ndarray:
+        fr = np.ascontiguousarray(frame, dtype=FRAME_DTYPE)
+        out = np.zeros(max(n, 1), dtype=np.float64)
+        m = self.lib.ao_synthesize_call(h, _ptr(fr), n, _ptr(out))
+        return out[:m]
+
+    def pressures(self, h) -> np.ndarray:
+        p = np.zeros(93)
+        self.lib.ao_get_pressures(h, _ptr(p))
+        return p
+
+    def currents(self, h) -> np.ndarray:
+        u = np.zeros(97)
+        self.lib.ao_get_currents(h, _ptr(u))
+        return u
+
+    def destroy(self, h) -> None:
+        self.lib.ao_destroy(h)
+
+
+class RefLib:
+    """The reference's own classes (TdsModel, TriangularGlottis, Tube, IirFilter)."""
+
+    def __init__(self, path: str = REF_SO):
+        if not os.path.exists(path):
+            build_oracle()
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        lib = ctypes.CDLL(path)
+        lib.afsref_create.restype = _vp
+        lib.afsref_create.argtypes = [ctypes.c_double, ctypes.c_uint]
+        lib.afsref_destroy.argtypes = [_vp]
+        lib.afsref_call.restype = ctypes.c_int
+        lib.afsref_call.argtypes = [_vp, _vp, ctypes.c_int, _vp]
+        lib.afsref_pressures.argtypes = [_vp, _vp]
+        lib.afsref_currents.argtypes = [_vp, _vp]
+        lib.afsref_position.argtypes = [_vp]
+        lib.afsref_position.restype = ctypes.c_int
+        lib.afsref_rand_calls.restype = ctypes.c_long
+        lib.afsref_utterance.restype = ctypes.c_long
+        lib.afsref_utterance.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint,
+                                         ctypes.c_double, _vp]
+        lib.afsref_chebyshev.restype = ctypes.c_int
+        lib.afsref_chebyshev.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int, _vp, _vp]
+        lib.afsref_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, _vp]
+        self.lib = lib
+
+    def utterance(self, frames: np.ndarray, hop: int, seed: int, fs: float) -> np.ndarray:
+        frames = np.ascontiguousarray(frames, dtype=FRAME_DTYPE)
+        F = frames.shape[0]
+        out = np.zeros((F - 1) * hop, dtype=np.float64)
+        n = self.lib.afsref_utterance(_ptr(frames), F, hop, seed, fs, _ptr(out))
+        assert n == out.size
+        return out
+
+    def batch(self, frames: np.ndarray, hop: int, seeds, fs: float) -> np.ndarray:
+        B, F = frames.shape
+        out = np.zeros((B, (F - 1) * hop), dtype=np.float64)
+        for u in range(B):
+            out[u] = self.utterance(frames[u], hop, int(seeds[u]), fs)
+        return out
+
+    def glibc_rand(self, seed: int, n: int) -> np.ndarray:
+        out = np.zeros(n, dtype=np.int32)
+        self.lib.afsref_glibc_rand(seed, n, _ptr(out))
+        return out.astype(np.int64)
+
+    def chebyshev(self, ratio: float, poles: int, highpass: bool = False):
+        a = np.zeros(33)
+        b = np.zeros(33)
+        n = self.lib.afsref_chebyshev(ratio, int(highpass), poles, _ptr(a), _ptr(b))
+        return a[: n + 1], b[: n + 1]
+
+    def create(self, fs: float, seed: int):
+        return self.lib.afsref_create(fs, seed)
+
+    def call(self, h, frame: np.ndarray, n: int) -> np.ndarray:
+        fr = np.ascontiguousarray(frame, dtype=FRAME_DTYPE)
+        out = np.zeros(max(n, 1), dtype=np.float64)
+        m = self.lib.afsref_call(h, _ptr(fr), n, _ptr(out))
+        return out[:m]
+
+    def pressures(self, h) -> np.ndarray:
+        p = np.zeros(93)
+        self.lib.afsref_pressures(h, _ptr(p))
+        return p
+
+    def currents(self, h) -> np.ndarray:
+        u = np.zeros(97)
+        self.lib.afsref_currents(h, _ptr(u))
+        return u
+
+    def destroy(self, h) -> None:
+        self.lib.afsref_destroy(h)
+
+
+def ref_available() -> bool:
+    return os.path.exists(REF_SO) or os.path.isdir("/root/reference/src/Backend")
