@@ -1,0 +1,99 @@
+"""ctypes binding of libafs.so (include/afs.h).
+
+The library is built in-tree by ``areafunctionsynthesis_amd.build``.  There is no
+fallback: if the library or a HIP device is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libafs.so")
+
+AFS_OK = 0
+STATUS = {0: "ok", 1: "invalid argument", 2: "no HIP device", 3: "HIP runtime error",
+          4: "out of device memory", 5: "unsupported configuration"}
+AFS_SOLVER_CHOLESKY = 0
+AFS_SOLVER_TREE = 1
+AFS_FP64 = 0
+AFS_ASYNC = 0x1
+
+# Every symbol include/afs.h declares.
+EXPORTED = (
+    "afs_abi_version", "afs_config_default", "afs_status_string", "afs_create", "afs_destroy",
+    "afs_last_error", "afs_set_stream", "afs_synchronize", "afs_synthesize",
+    "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_session_destroy",
+    "afs_af_to_frames",
+)
+
+
+class AfsOptions(ctypes.Structure):
+    _fields_ = [("turbulence_losses", ctypes.c_int32), ("soft_walls", ctypes.c_int32),
+                ("generate_noise_sources", ctypes.c_int32), ("radiation_from_skin", ctypes.c_int32),
+                ("piriform_fossa", ctypes.c_int32), ("inner_length_corrections", ctypes.c_int32)]
+
+
+class AfsConfig(ctypes.Structure):
+    _fields_ = [("sampling_rate_hz", ctypes.c_double), ("precision", ctypes.c_int32),
+                ("solver", ctypes.c_int32), ("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("options", AfsOptions)]
+
+
+class AfsReport(ctypes.Structure):
+    _fields_ = [("device_ms", ctypes.c_double), ("samples", ctypes.c_int64),
+                ("nonfinite_utterances", ctypes.c_int32), ("kernel", ctypes.c_int32)]
+
+
+class AfsError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libafs.so, building it first when it is absent (never a CPU substitute)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        from . import build as _build
+        _build.build()
+    if not os.path.exists(path):
+        raise AfsError(f"libafs.so not found at {path}; run python -m areafunctionsynthesis_amd.build")
+    lib = ctypes.CDLL(path)
+    vp = ctypes.c_void_p
+    lib.afs_abi_version.restype = ctypes.c_int32
+    lib.afs_config_default.argtypes = [ctypes.POINTER(AfsConfig)]
+    lib.afs_status_string.restype = ctypes.c_char_p
+    lib.afs_status_string.argtypes = [ctypes.c_int]
+    lib.afs_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(AfsConfig)]
+    lib.afs_destroy.argtypes = [vp]
+    lib.afs_last_error.restype = ctypes.c_char_p
+    lib.afs_last_error.argtypes = [vp]
+    lib.afs_set_stream.argtypes = [vp, vp]
+    lib.afs_synchronize.argtypes = [vp]
+    lib.afs_synthesize.argtypes = [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp,
+                                   ctypes.POINTER(AfsReport)]
+    lib.afs_session_create.argtypes = [vp, ctypes.c_int32, vp, ctypes.POINTER(vp)]
+    lib.afs_session_synthesize.argtypes = [vp, vp, ctypes.c_int32, vp, ctypes.POINTER(ctypes.c_int32),
+                                           ctypes.POINTER(AfsReport)]
+    lib.afs_session_reset.argtypes = [vp, vp]
+    lib.afs_session_destroy.argtypes = [vp]
+    lib.afs_af_to_frames.argtypes = [vp, vp, ctypes.c_int64, vp]
+    for name in ("afs_create", "afs_set_stream", "afs_synchronize", "afs_synthesize",
+                 "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_af_to_frames"):
+        getattr(lib, name).restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def check(status: int, ctx=None, what: str = "") -> None:
+    if status != AFS_OK:
+        msg = STATUS.get(status, str(status))
+        detail = ""
+        if ctx is not None:
+            raw = load().afs_last_error(ctx)
+            detail = raw.decode() if raw else ""
+        raise AfsError(f"{what}: {msg}" + (f" ({detail})" if detail else ""))

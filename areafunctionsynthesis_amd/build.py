@@ -1,0 +1,65 @@
+"""Build libafs.so (HIP, gfx950) in-tree with hipcc.
+
+Usage: python -m areafunctionsynthesis_amd.build [--force]
+The shared library lands next to this file so it travels with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libafs.so")
+ARCH = os.environ.get("AFS_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["afs_capi.cpp", "afs_tables.cpp", "tds_lane.hip", "af_kernels.hip"]
+HEADERS = ["afs_model.h", "afs_lane.h", os.path.join("..", "..", "include", "afs.h")]
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+          # keep the reference's rounding: no contraction of a*b+c into fma
+          "-ffp-contract=off"]
+
+
+def _hipcc() -> str:
+    for p in ("/opt/rocm/bin/hipcc", "hipcc"):
+        if os.path.sep not in p or os.path.exists(p):
+            return p
+    return "hipcc"
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    for f in SOURCES + HEADERS:
+        if os.path.getmtime(os.path.join(CSRC, f)) > t:
+            return True
+    return False
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and not _stale():
+        return LIB
+    objdir = os.path.join(HERE, "_obj")
+    os.makedirs(objdir, exist_ok=True)
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        lang = ["-x", "hip"] if src.endswith(".cpp") else []
+        cmd = [_hipcc(), "-c"] + lang + [os.path.join(CSRC, src), "-o", obj, f"--offload-arch={ARCH}"] + COMMON
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        objs.append(obj)
+    cmd = [_hipcc(), "-shared", "-o", LIB + ".tmp", f"--offload-arch={ARCH}", "-fPIC"] + objs
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

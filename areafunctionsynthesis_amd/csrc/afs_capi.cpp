@@ -1,0 +1,396 @@
+// afs_capi.cpp -- the C ABI of include/afs.h: contexts, sessions, staging, launches.
+//
+// Host-side orchestration only; all synthesis arithmetic runs in the HIP kernels.
+// There is no CPU fallback: without a usable HIP device afs_create fails with
+// AFS_ERR_NO_DEVICE.
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include <hip/hip_runtime.h>
+
+#include "afs_lane.h"
+#include "afs_model.h"
+
+static_assert(sizeof(afs_frame) == 1072, "afs_frame layout");
+
+struct afs_ctx {
+  afs_config cfg{};
+  hipStream_t stream = nullptr;
+  afs::Tables host_tab{};
+  afs::Tables *dev_tab = nullptr;
+  std::string err;
+  // reusable device buffers for whole-trajectory calls
+  void *ws = nullptr;
+  size_t ws_bytes = 0;
+  int32_t *rng = nullptr;
+  size_t rng_bytes = 0;
+  void *stage_in = nullptr;
+  size_t stage_in_bytes = 0;
+  void *stage_out = nullptr;
+  size_t stage_out_bytes = 0;
+  void *stage_seeds = nullptr;
+  size_t stage_seeds_bytes = 0;
+  int32_t *dcount = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+struct afs_session {
+  afs_ctx *ctx = nullptr;
+  int B = 0;
+  int64_t bp = 0;
+  void *ws = nullptr;
+  int32_t *rng = nullptr;
+  afs_frame *pair = nullptr;   // [B][2]: previous frame, new frame
+  uint32_t *seeds = nullptr;   // device copy
+  bool latched = false;
+};
+
+namespace {
+
+afs_status fail(afs_ctx *c, afs_status s, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return s;
+}
+
+#define HIP_TRY(ctx, call)                                                                   \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return fail((ctx), e_ == hipErrorOutOfMemory ? AFS_ERR_OUT_OF_MEMORY : AFS_ERR_HIP,    \
+                  "%s failed: %s", #call, hipGetErrorString(e_));                            \
+  } while (0)
+
+bool is_device_ptr(const void *p) {
+  if (!p) return false;
+  hipPointerAttribute_t at;
+  hipError_t e = hipPointerGetAttributes(&at, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+afs_status ensure(afs_ctx *c, void **buf, size_t *cap, size_t bytes) {
+  if (bytes <= *cap) return AFS_OK;
+  if (*buf) (void)hipFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
+  HIP_TRY(c, hipMalloc(buf, bytes));
+  *cap = bytes;
+  return AFS_OK;
+}
+
+int64_t pad64(int64_t b) { return (b + 63) / 64 * 64; }
+
+bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY; }
+
+// Launch the synthesis for frame transitions [k0, k1) in chunks that keep each kernel short.
+afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int k0, int k1, int hop,
+                      double *out, int64_t ostride, void *ws, int32_t *rng, int64_t bp, int B) {
+  const int64_t max_samples = 8192;
+  int per = (int)std::max<int64_t>(1, max_samples / std::max(1, hop));
+  for (int k = k0; k < k1; k += per) {
+    int ke = std::min(k1, k + per);
+    afs::LaneArgs a{c->dev_tab, frames, fstride, k, ke, hop, out + (int64_t)(k - k0) * hop, ostride,
+                    (double *)ws, rng, bp, B};
+    HIP_TRY(c, afs::launch_lane_synth(a, c->stream));
+  }
+  return AFS_OK;
+}
+
+int64_t ws_rows(const afs_ctx *c) {
+  return afs::lane_ws_rows(c->host_tab);
+}
+
+afs_status reset_state(afs_ctx *c, void *ws, int32_t *rng, int64_t bp, int B, const uint32_t *seeds_dev) {
+  HIP_TRY(c, afs::launch_lane_reset((double *)ws, rng, bp, B, seeds_dev, c->stream));
+  return AFS_OK;
+}
+
+afs_status count_nonfinite(afs_ctx *c, void *ws, int64_t bp, int B, int32_t *out) {
+  HIP_TRY(c, hipMemsetAsync(c->dcount, 0, sizeof(int32_t), c->stream));
+  HIP_TRY(c, afs::launch_lane_nonfinite((const double *)ws, bp, B, c->dcount, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(out, c->dcount, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  return AFS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t afs_abi_version(void) { return AFS_ABI_VERSION; }
+
+void afs_config_default(afs_config *cfg) {
+  if (!cfg) return;
+  std::memset(cfg, 0, sizeof *cfg);
+  cfg->sampling_rate_hz = 22050.0;
+  cfg->precision = AFS_FP64;
+  cfg->solver = AFS_SOLVER_CHOLESKY;
+  cfg->device = 0;
+  cfg->flags = 0;
+  cfg->options.turbulence_losses = 1;
+  cfg->options.soft_walls = 1;
+  cfg->options.generate_noise_sources = 1;
+  cfg->options.radiation_from_skin = 1;
+  cfg->options.piriform_fossa = 0;
+  cfg->options.inner_length_corrections = 1;
+}
+
+const char *afs_status_string(afs_status s) {
+  switch (s) {
+    case AFS_OK: return "ok";
+    case AFS_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case AFS_ERR_NO_DEVICE: return "no HIP device";
+    case AFS_ERR_HIP: return "HIP runtime error";
+    case AFS_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case AFS_ERR_UNSUPPORTED: return "unsupported configuration";
+  }
+  return "unknown status";
+}
+
+afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
+  if (!out) return AFS_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  afs_config c;
+  if (cfg) c = *cfg; else afs_config_default(&c);
+  if (!(c.sampling_rate_hz > 0.0) || c.precision != AFS_FP64 || !solver_ok(c.solver))
+    return AFS_ERR_INVALID_ARGUMENT;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return AFS_ERR_NO_DEVICE;
+  }
+  if (c.device < 0 || c.device >= n) return AFS_ERR_NO_DEVICE;
+  if (hipSetDevice(c.device) != hipSuccess) return AFS_ERR_NO_DEVICE;
+  afs_ctx *ctx = new afs_ctx();
+  ctx->cfg = c;
+  afs::build_tables(&ctx->host_tab, c.sampling_rate_hz, c.options);
+  afs_status st = AFS_OK;
+  auto bail = [&](afs_status s) { afs_destroy(ctx); return s; };
+  if (hipMalloc((void **)&ctx->dev_tab, sizeof(afs::Tables)) != hipSuccess) return bail(AFS_ERR_OUT_OF_MEMORY);
+  if (hipMemcpy(ctx->dev_tab, &ctx->host_tab, sizeof(afs::Tables), hipMemcpyHostToDevice) != hipSuccess)
+    return bail(AFS_ERR_HIP);
+  if (hipMalloc((void **)&ctx->dcount, sizeof(int32_t)) != hipSuccess) return bail(AFS_ERR_OUT_OF_MEMORY);
+  if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return bail(AFS_ERR_HIP);
+  (void)st;
+  *out = ctx;
+  return AFS_OK;
+}
+
+void afs_destroy(afs_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->cfg.device);
+  if (c->dev_tab) (void)hipFree(c->dev_tab);
+  if (c->ws) (void)hipFree(c->ws);
+  if (c->rng) (void)hipFree(c->rng);
+  if (c->stage_in) (void)hipFree(c->stage_in);
+  if (c->stage_out) (void)hipFree(c->stage_out);
+  if (c->stage_seeds) (void)hipFree(c->stage_seeds);
+  if (c->dcount) (void)hipFree(c->dcount);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  delete c;
+}
+
+const char *afs_last_error(const afs_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+afs_status afs_set_stream(afs_ctx *c, void *s) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  c->stream = (hipStream_t)s;
+  return AFS_OK;
+}
+
+afs_status afs_synchronize(afs_ctx *c) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return AFS_OK;
+}
+
+afs_status afs_synthesize(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B,
+                          int32_t F, int32_t hop, double *out, afs_report *rep) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (!frames || !out || B <= 0 || F < 2 || hop < 1)
+    return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_synthesize: need frames, out, batch>0, num_frames>=2, hop>=1");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  const int64_t T = (int64_t)(F - 1) * hop;
+  const int64_t bp = pad64(B);
+  afs_status s;
+  // inputs
+  const afs_frame *dframes = frames;
+  if (!is_device_ptr(frames)) {
+    size_t bytes = (size_t)B * F * sizeof(afs_frame);
+    if ((s = ensure(c, &c->stage_in, &c->stage_in_bytes, bytes)) != AFS_OK) return s;
+    HIP_TRY(c, hipMemcpyAsync(c->stage_in, frames, bytes, hipMemcpyHostToDevice, c->stream));
+    dframes = (const afs_frame *)c->stage_in;
+  }
+  const uint32_t *dseeds = seeds;
+  if (seeds && !is_device_ptr(seeds)) {
+    if ((s = ensure(c, &c->stage_seeds, &c->stage_seeds_bytes, (size_t)B * 4)) != AFS_OK) return s;
+    HIP_TRY(c, hipMemcpyAsync(c->stage_seeds, seeds, (size_t)B * 4, hipMemcpyHostToDevice, c->stream));
+    dseeds = (const uint32_t *)c->stage_seeds;
+  }
+  double *dout = out;
+  const bool host_out = !is_device_ptr(out);
+  if (host_out) {
+    if ((s = ensure(c, &c->stage_out, &c->stage_out_bytes, (size_t)B * T * sizeof(double))) != AFS_OK) return s;
+    dout = (double *)c->stage_out;
+  }
+  // state
+  if ((s = ensure(c, &c->ws, &c->ws_bytes, (size_t)(ws_rows(c) * bp) * sizeof(double))) != AFS_OK) return s;
+  if ((s = ensure(c, (void **)&c->rng, &c->rng_bytes, (size_t)(32 * bp) * sizeof(int32_t))) != AFS_OK) return s;
+  if ((s = reset_state(c, c->ws, c->rng, bp, B, dseeds)) != AFS_OK) return s;
+  HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
+  if ((s = run_chunks(c, dframes, F, 1, F, hop, dout, T, c->ws, c->rng, bp, B)) != AFS_OK) return s;
+  HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
+  int32_t nonfinite = 0;
+  if ((s = count_nonfinite(c, c->ws, bp, B, &nonfinite)) != AFS_OK) return s;
+  if (host_out) HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)B * T * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  const bool sync = !(c->cfg.flags & AFS_ASYNC) || host_out || rep;
+  if (sync) HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (rep) {
+    float ms = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    rep->device_ms = ms;
+    rep->samples = (int64_t)B * T;
+    rep->nonfinite_utterances = nonfinite;
+    rep->kernel = c->cfg.solver;
+  }
+  return AFS_OK;
+}
+
+afs_status afs_session_create(afs_ctx *c, int32_t B, const uint32_t *seeds, afs_session **out) {
+  if (!c || !out || B <= 0) return c ? fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_session_create: bad args") : AFS_ERR_INVALID_ARGUMENT;
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  afs_session *s = new afs_session();
+  s->ctx = c;
+  s->B = B;
+  s->bp = pad64(B);
+  auto bail = [&](hipError_t e) {
+    afs_session_destroy(s);
+    return fail(c, e == hipErrorOutOfMemory ? AFS_ERR_OUT_OF_MEMORY : AFS_ERR_HIP, "session alloc: %s", hipGetErrorString(e));
+  };
+  hipError_t e;
+  if ((e = hipMalloc(&s->ws, (size_t)(ws_rows(c) * s->bp) * sizeof(double))) != hipSuccess) return bail(e);
+  if ((e = hipMalloc((void **)&s->rng, (size_t)(32 * s->bp) * sizeof(int32_t))) != hipSuccess) return bail(e);
+  if ((e = hipMalloc((void **)&s->pair, (size_t)B * 2 * sizeof(afs_frame))) != hipSuccess) return bail(e);
+  if ((e = hipMalloc((void **)&s->seeds, (size_t)B * sizeof(uint32_t))) != hipSuccess) return bail(e);
+  *out = s;
+  afs_status st = afs_session_reset(s, seeds);
+  if (st != AFS_OK) {
+    afs_session_destroy(s);
+    *out = nullptr;
+  }
+  return st;
+}
+
+afs_status afs_session_reset(afs_session *s, const uint32_t *seeds) {
+  if (!s) return AFS_ERR_INVALID_ARGUMENT;
+  afs_ctx *c = s->ctx;
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  if (seeds) {
+    hipMemcpyKind k = is_device_ptr(seeds) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    HIP_TRY(c, hipMemcpyAsync(s->seeds, seeds, (size_t)s->B * 4, k, c->stream));
+  } else {
+    HIP_TRY(c, hipMemsetAsync(s->seeds, 0, (size_t)s->B * 4, c->stream));
+  }
+  afs_status st = reset_state(c, s->ws, s->rng, s->bp, s->B, s->seeds);
+  if (st != AFS_OK) return st;
+  s->latched = false;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return AFS_OK;
+}
+
+void afs_session_destroy(afs_session *s) {
+  if (!s) return;
+  if (s->ws) (void)hipFree(s->ws);
+  if (s->rng) (void)hipFree(s->rng);
+  if (s->pair) (void)hipFree(s->pair);
+  if (s->seeds) (void)hipFree(s->seeds);
+  delete s;
+}
+
+afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32_t n, double *out,
+                                  int32_t *produced, afs_report *rep) {
+  if (!s || !frames) return AFS_ERR_INVALID_ARGUMENT;
+  afs_ctx *c = s->ctx;
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  const int B = s->B;
+  hipMemcpyKind k = is_device_ptr(frames) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  // frames[u] -> pair[u][slot]
+  const int slot = s->latched ? 1 : 0;
+  HIP_TRY(c, hipMemcpy2DAsync(s->pair + slot, 2 * sizeof(afs_frame), frames, sizeof(afs_frame),
+                              sizeof(afs_frame), B, k, c->stream));
+  if (!s->latched) {  // Synthesizer.cpp:522-532
+    s->latched = true;
+    if (produced) *produced = 0;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (rep) { std::memset(rep, 0, sizeof *rep); rep->kernel = c->cfg.solver; }
+    return AFS_OK;
+  }
+  if (!out) return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_session_synthesize: out is NULL");
+  if (n < 1) n = 1;  // Synthesizer.cpp:543-546
+  double *dout = out;
+  const bool host_out = !is_device_ptr(out);
+  afs_status st;
+  if (host_out) {
+    if ((st = ensure(c, &c->stage_out, &c->stage_out_bytes, (size_t)B * n * sizeof(double))) != AFS_OK) return st;
+    dout = (double *)c->stage_out;
+  }
+  HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
+  if ((st = run_chunks(c, s->pair, 2, 1, 2, n, dout, n, s->ws, s->rng, s->bp, B)) != AFS_OK) return st;
+  HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
+  // prevTube = *newTube (Synthesizer.cpp:633-637)
+  HIP_TRY(c, hipMemcpy2DAsync(s->pair, 2 * sizeof(afs_frame), s->pair + 1, 2 * sizeof(afs_frame),
+                              sizeof(afs_frame), B, hipMemcpyDeviceToDevice, c->stream));
+  int32_t nonfinite = 0;
+  if ((st = count_nonfinite(c, s->ws, s->bp, B, &nonfinite)) != AFS_OK) return st;
+  if (host_out) HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)B * n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (produced) *produced = n;
+  if (rep) {
+    float ms = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    rep->device_ms = ms;
+    rep->samples = (int64_t)B * n;
+    rep->nonfinite_utterances = nonfinite;
+    rep->kernel = c->cfg.solver;
+  }
+  return AFS_OK;
+}
+
+afs_status afs_af_to_frames(afs_ctx *c, const double *params, int64_t n, afs_frame *frames) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (!params || !frames || n <= 0) return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_af_to_frames: bad args");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  const double *dp = params;
+  void *tmp_p = nullptr, *tmp_f = nullptr;
+  const bool host_p = !is_device_ptr(params), host_f = !is_device_ptr(frames);
+  afs_frame *df = frames;
+  if (host_p) {
+    HIP_TRY(c, hipMalloc(&tmp_p, (size_t)n * 16 * sizeof(double)));
+    HIP_TRY(c, hipMemcpyAsync(tmp_p, params, (size_t)n * 16 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    dp = (const double *)tmp_p;
+  }
+  if (host_f) {
+    HIP_TRY(c, hipMalloc(&tmp_f, (size_t)n * sizeof(afs_frame)));
+    HIP_TRY(c, hipMemcpyAsync(tmp_f, frames, (size_t)n * sizeof(afs_frame), hipMemcpyHostToDevice, c->stream));
+    df = (afs_frame *)tmp_f;
+  }
+  HIP_TRY(c, afs::launch_af_to_frames(dp, n, df, c->stream));
+  if (host_f) HIP_TRY(c, hipMemcpyAsync(frames, df, (size_t)n * sizeof(afs_frame), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (tmp_p) (void)hipFree(tmp_p);
+  if (tmp_f) (void)hipFree(tmp_f);
+  return AFS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+// afs_model.h -- the branched-tube network shared by host and device code.
+//
+// Section/current numbering follows the reference exactly so that indices in tests
+// and fixtures mean the same thing:
+//   sections (Tube.h:53-82): 0-22 trachea, 23/24 glottis, 25-40 pharynx, 41-64 mouth,
+//                            65-83 nose, 84-88 piriform fossa, 89-92 paranasal sinuses
+//   currents (TdsModel.h:37, TdsModel.cpp:93-131): current c flows into section c
+//                            (c < 93); 93/94 mouth radiation (R, L), 95/96 nostril radiation.
+// Everything that does not change during synthesis -- static tube sections, their
+// L/C/R/wall constants, filter coefficients, topology -- is evaluated once on the host
+// (afs_tables.cpp) with the reference's own formulas and operand order, and handed to
+// the kernels in one read-only `Tables` block.
+#pragma once
+
+#include <cstdint>
+
+#include "../../include/afs.h"
+
+#if defined(__HIPCC__)
+#define AFS_HD __host__ __device__
+#else
+#define AFS_HD
+#endif
+
+namespace afs {
+
+constexpr int NS = 93;   // Tube::NUM_SECTIONS
+constexpr int NC = 97;   // TdsModel::NUM_BRANCH_CURRENTS
+constexpr int NPM = 40;  // pharynx + mouth sections
+constexpr int S_LAST_TRACHEA = 22, S_GLOT_LO = 23, S_GLOT_UP = 24;
+constexpr int S_PHARYNX0 = 25, S_LAST_PHARYNX = 40, S_LAST_MOUTH = 64;
+constexpr int S_NOSE0 = 65, S_LAST_NOSE = 83, S_FOSSA0 = 84, S_LAST_FOSSA = 88;
+constexpr int S_SINUS0 = 89, S_LAST_SINUS = 92;
+constexpr int NDIP = 41;  // dipole sources of sections 25..64, then the lips source
+constexpr int DIP_LIPS = 40;
+constexpr int ENV_COLS = 10;
+
+enum Articulator : int { VOCAL_FOLDS = 0, TONGUE = 1, LOWER_INCISORS = 2, LOWER_LIP = 3, OTHER = 4 };
+
+// Physical constants (Constants.h:8-16) and discretisation (TdsModel.cpp:15-22).
+constexpr double RHO = 1.14e-3;
+constexpr double CSND = 3.5e4;
+constexpr double MU = 1.86e-4;
+constexpr double TH = 0.515;
+constexpr double TH1 = 1.0 - 0.515;
+constexpr double AMIN = 0.1e-2;
+constexpr double PI = 3.14159265358979323846;
+
+// Glottis static parameters (TriangularGlottis.cpp:38-56).
+constexpr double G_REST_LEN = 1.3, G_REST_THICK0 = 0.24, G_REST_THICK1 = 0.06;
+constexpr double G_MASS0 = 0.12, G_MASS1 = 0.03, G_DAMP0 = 0.1, G_DAMP1 = 0.6;
+constexpr double G_K0 = 80000.0, G_K1 = 8000.0, G_KC0 = 240000.0, G_KC1 = 24000.0;
+constexpr double G_KCOUPLE = 25000.0, G_INLET = 0.05, G_OUTLET = 0.01;
+constexpr double G_NAT_F0 = 129.0, G_F0_DIV_Q = 125.51;
+
+// A section is "static" when nothing about its geometry changes during synthesis:
+// trachea, nose beyond the velum taper (nose[4..18]), fossa, sinuses.
+AFS_HD constexpr bool is_static_section(int s) {
+  return s <= S_LAST_TRACHEA || (s >= S_NOSE0 + 4);
+}
+
+struct Tables {
+  // time step and derived scalars
+  double fs, dt, dtTH, dtTH1, th1_th, inv_dtTH;
+  double noise_amp_F;      // 1 - exp(-2 pi 40 dt)           (TdsModel.cpp:1637-1638)
+  double noise_lp_c;       // exp(-2 pi 500 dt)               (TdsModel.cpp:2061)
+  double noise_x_2000;     // exp(-2 pi (2000 dt)): one-pole coefficient at the clamped cutoff
+  double sqrt12;           // sqrt(12.0)
+  double nose4_area;       // Tube noseSection[4].area, target of the velum taper (Tube.cpp:407)
+  double fossa_R0;         // decoupled fossa entrance resistance (TdsModel.cpp:888)
+  double rrad_num, lrad_num; // 128 rho c, 8 rho                     (TdsModel.cpp:1874, 1889)
+  double tone_a[5], tone_b[5];  // glottalToneFilter (TdsModel.cpp:494-510)
+  double out_a[9], out_b[9];    // Chebyshev(7000/fs, 8 poles)     (Synthesizer.cpp:52)
+
+  // per-section geometry and walls (static sections: final values; dynamic: walls only)
+  double area[NS], len[NS], vol[NS], Mw[NS], Bw[NS], Kw[NS];
+  // static-section network constants, evaluated as prepareTimeStep would (TdsModel.cpp:732-834)
+  double L[NS], C[NS], R[NS], alpha[NS], wc1[NS], wc2[NS], Lw[NS], E[NS];
+
+  // topology (TdsModel::initModel, TdsModel.cpp:93-292)
+  int16_t src[NC], tgt[NC], cin[NS], cout0[NS], cout1[NS];
+  // symmetric-envelope Cholesky structure: row i spans columns env_start[i] .. i-1
+  int16_t env_start[NC], env_n[NC], env_off[NC];
+  int16_t col_n[NC], col[NC][ENV_COLS];
+  int32_t env_total;
+
+  afs_options opt;
+};
+
+// Host: build the tables for a sampling rate and option set (afs_tables.cpp).
+void build_tables(Tables *t, double fs_hz, const afs_options &opt);
+// Host: IirFilter::createChebyshev restatement used for the output filter.
+int chebyshev(double ratio, bool highpass, int poles, double *a, double *b);
+
+}  // namespace afs

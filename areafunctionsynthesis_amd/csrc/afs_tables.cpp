@@ -1,0 +1,223 @@
+// afs_tables.cpp -- host-side evaluation of everything static in the tube network.
+//
+// All values are computed with the reference's formulas and operand order in plain
+// IEEE double (no FMA contraction: this file is built with -ffp-contract=off), so the
+// constants the kernels read are bit-identical to what the reference recomputes each
+// sample for the same sections.
+#include <cmath>
+#include <cstring>
+
+#include "afs_model.h"
+
+namespace afs {
+
+namespace {
+
+const double NOSE_AREA[19] = {1.63, 2.07, 2.72, 3.59, 4.24, 3.26, 3.04, 3.04, 2.72, 2.5,
+                              2.39, 2.39, 1.85, 0.76, 1.41, 1.74, 1.30, 1.74, 0.76};  // Tube.cpp:155-157
+const double SINUS_VOLUME[4] = {11.3, 6.8, 33.0, 6.2};                                 // Tube.cpp:159
+const double NECK_LENGTH[4] = {0.3, 0.3, 0.45, 1.0};                                   // Tube.cpp:160
+const double NECK_AREA[4] = {0.185, 0.185, 0.145, 0.11};                               // Tube.cpp:161
+const int SINUS_COUPLING[4] = {8, 9, 11, 12};                                          // Tube.cpp:35-38
+
+// Static geometry and wall data (Tube.cpp:79-314).
+void static_geometry(Tables *t) {
+  for (int i = 0; i < NS; ++i) {
+    t->Mw[i] = 2.1; t->Bw[i] = 800.0; t->Kw[i] = 84500.0;
+    t->area[i] = 0.0; t->len[i] = 0.0; t->vol[i] = 0.0;
+  }
+  for (int i = 0; i <= S_LAST_TRACHEA; ++i) {
+    t->area[i] = (i == 0) ? 4.0 : (i == 1) ? 3.0 : 2.5;
+    t->len[i] = 23.0 / (double)23;
+    t->vol[i] = t->area[i] * t->len[i];
+    t->Mw[i] = 0.25; t->Bw[i] = 1000.0;
+  }
+  const double lf = 11.4 / 11.4;
+  for (int i = 0; i < 19; ++i) {
+    int k = S_NOSE0 + i;
+    t->area[k] = NOSE_AREA[i];
+    t->len[k] = lf * 0.6;
+    t->vol[k] = t->area[k] * t->len[k];
+  }
+  for (int i = 0; i < 4; ++i) {
+    int k = S_SINUS0 + i;
+    t->area[k] = NECK_AREA[i]; t->len[k] = NECK_LENGTH[i]; t->vol[k] = SINUS_VOLUME[i];
+    t->Mw[k] = 0.0; t->Bw[k] = 6500.0;
+  }
+  const double amax = 2.0 * 2.0 / 3.0, sl = 3.0 / (double)5;
+  for (int i = 0; i < 5; ++i) {
+    int k = S_FOSSA0 + i;
+    t->area[k] = amax * (1.0 - (i + 0.5) / (double)5);
+    t->len[k] = sl;
+    t->vol[k] = t->area[k] * t->len[k];
+  }
+  t->nose4_area = t->area[S_NOSE0 + 4];
+}
+
+// prepareTimeStep's per-section terms for sections whose geometry never changes
+// (TdsModel.cpp:741-832 and :988-1008 for E).
+void static_network(Tables *t) {
+  const double dt = t->dt;
+  for (int i = 0; i < NS; ++i) {
+    t->L[i] = t->C[i] = t->R[i] = t->alpha[i] = t->wc1[i] = t->wc2[i] = t->Lw[i] = t->E[i] = 0.0;
+    if (!is_static_section(i)) continue;
+    double area = t->area[i], len = t->len[i], vol = t->vol[i];
+    double circ = 2.0 * std::sqrt(area * PI);
+    if (i >= S_SINUS0 && i <= S_LAST_SINUS) {
+      t->L[i] = RHO * (len / area);
+      t->C[i] = vol / (RHO * CSND * CSND);
+      t->R[i] = (8.0 * MU * PI * len) / (area * area);
+    } else {
+      double a = std::sqrt(area / PI), b = a;
+      const double rmin = 1.6;
+      if (a < rmin) { a = rmin; b = area / (PI * a); }
+      t->L[i] = (RHO * 0.5 * len) / area;
+      t->C[i] = vol / (RHO * CSND * CSND);
+      t->R[i] = ((2.0 * MU * len) * (a * a + b * b)) / (PI * a * a * a * b * b * b);
+    }
+    if (t->opt.soft_walls) {
+      double surf;
+      if (i >= S_SINUS0 && i <= S_LAST_SINUS)
+        surf = 4.0 * PI * std::pow((3.0 * vol) / (4.0 * PI), 2.0 / 3.0);
+      else
+        surf = circ * len;
+      if (surf < AMIN) surf = AMIN;
+      double Rw = t->Bw[i] / surf, Lw = t->Mw[i] / surf, Cw = surf / t->Kw[i];
+      t->alpha[i] = 1.0 / (Lw / (dt * dt * TH * TH) + Rw / (dt * TH) + 1.0 / Cw);
+      t->wc1[i] = Lw / (dt * dt * TH * TH) + Rw / (dt * TH);
+      t->wc2[i] = Lw * (TH1 / TH + 1.0) / (dt * TH) + Rw * (TH1 / TH);
+      t->Lw[i] = Lw;
+    }
+    t->E[i] = dt * TH / (t->C[i] + t->alpha[i]);
+  }
+}
+
+void topology(Tables *t) {
+  for (int i = 0; i < NS; ++i) { t->src[i] = (int16_t)(i - 1); t->tgt[i] = (int16_t)i; }
+  t->src[0] = -1;
+  t->src[S_NOSE0] = S_LAST_PHARYNX;
+  t->src[S_FOSSA0] = S_PHARYNX0 + 3;
+  for (int i = 0; i < 4; ++i) t->src[S_SINUS0 + i] = (int16_t)(S_NOSE0 + SINUS_COUPLING[i]);
+  t->src[93] = t->src[94] = S_LAST_MOUTH;
+  t->src[95] = t->src[96] = S_LAST_NOSE;
+  t->tgt[93] = t->tgt[94] = t->tgt[95] = t->tgt[96] = -1;
+  for (int s = 0; s < NS; ++s) t->cin[s] = t->cout0[s] = t->cout1[s] = -1;
+  for (int c = 0; c < NC; ++c) {
+    if (t->src[c] != -1) {
+      int s = t->src[c];
+      if (t->cout0[s] == -1) t->cout0[s] = (int16_t)c; else t->cout1[s] = (int16_t)c;
+    }
+    if (t->tgt[c] != -1) t->cin[t->tgt[c]] = (int16_t)c;
+  }
+  // Matrix pattern and the envelope (TdsModel.cpp:218-292).
+  static unsigned char nz[NC][NC];
+  std::memset(nz, 0, sizeof nz);
+  int off = 0;
+  for (int c = 0; c < NC; ++c) {
+    const int sides[2] = {t->src[c], t->tgt[c]};
+    for (int s : sides) {
+      if (s == -1) continue;
+      if (t->cin[s] != -1) nz[c][t->cin[s]] = 1;
+      if (t->cout0[s] != -1) nz[c][t->cout0[s]] = 1;
+      if (t->cout1[s] != -1) nz[c][t->cout1[s]] = 1;
+    }
+    int first = c;
+    for (int j = 0; j < c; ++j)
+      if (nz[c][j]) { first = j; break; }
+    for (int j = first; j < c; ++j) nz[c][j] = 1;
+    t->env_start[c] = (int16_t)first;
+    t->env_n[c] = (int16_t)(c - first);
+    t->env_off[c] = (int16_t)off;
+    off += c - first;
+  }
+  t->env_total = off;
+  for (int j = 0; j < NC; ++j) {
+    int n = 0;
+    for (int i = j + 1; i < NC; ++i)
+      if (nz[i][j]) t->col[j][n++] = (int16_t)i;
+    t->col_n[j] = (int16_t)n;
+  }
+}
+
+}  // namespace
+
+// IirFilter::createChebyshev, IirFilter.cpp:286-432 (0.5 % ripple).
+int chebyshev(double ratio, bool hp, int poles, double *aout, double *bout) {
+  double a[33], b[33], ta[33], tb[33];
+  if (poles & 1) poles++;
+  if (poles > 32) poles = 32;
+  for (int i = 0; i <= 32; ++i) a[i] = b[i] = 0.0;
+  a[2] = 1.0;
+  b[2] = 1.0;
+  for (int p = 1; p <= poles / 2; ++p) {
+    double re = -std::cos(PI / (2.0 * poles) + (PI * (p - 1)) / (double)poles);
+    double im = std::sin(PI / (2.0 * poles) + (PI * (p - 1)) / (double)poles);
+    const double tmp = 100.0 / (100.0 - 0.5);
+    const double es = std::sqrt(tmp * tmp - 1.0);
+    const double vx = (1.0 / (double)poles) * std::log((1.0 / es) + std::sqrt((1.0 / (es * es)) + 1));
+    double kx = (1.0 / (double)poles) * std::log((1.0 / es) + std::sqrt((1.0 / (es * es)) - 1));
+    kx = 0.5 * (std::exp(kx) + std::exp(-kx));
+    re = re * (0.5 * (std::exp(vx) - std::exp(-vx))) / kx;
+    im = im * (0.5 * (std::exp(vx) + std::exp(-vx))) / kx;
+    const double t = 2.0 * std::tan(0.5);
+    const double w = 2.0 * PI * ratio;
+    const double m = re * re + im * im;
+    double d = 4.0 - 4.0 * re * t + m * t * t;
+    const double x0 = (t * t) / d, x1 = (2.0 * t * t) / d, x2 = (t * t) / d;
+    const double y1 = (8.0 - 2.0 * m * t * t) / d;
+    const double y2 = (-4.0 - 4.0 * re * t - m * t * t) / d;
+    const double k = hp ? -std::cos(0.5 * w + 0.5) / std::cos(0.5 * w - 0.5)
+                        : std::sin(0.5 - 0.5 * w) / std::sin(0.5 + 0.5 * w);
+    d = 1.0 + y1 * k - y2 * k * k;
+    const double a0 = (x0 - x1 * k + x2 * k * k) / d;
+    double a1 = (-2.0 * x0 * k + x1 + x1 * k * k - 2.0 * x2 * k) / d;
+    const double a2 = (x0 * k * k - x1 * k + x2) / d;
+    double b1 = (2.0 * k + y1 + y1 * k * k - 2.0 * y2 * k) / d;
+    const double b2 = (-(k * k) - y1 * k + y2) / d;
+    if (hp) { a1 = -a1; b1 = -b1; }
+    std::memcpy(ta, a, sizeof ta);
+    std::memcpy(tb, b, sizeof tb);
+    for (int i = 2; i <= 32; ++i) {
+      a[i] = a0 * ta[i] + a1 * ta[i - 1] + a2 * ta[i - 2];
+      b[i] = tb[i] - b1 * tb[i - 1] - b2 * tb[i - 2];
+    }
+  }
+  b[2] = 0.0;
+  for (int i = 0; i <= 30; ++i) { a[i] = a[i + 2]; b[i] = -b[i + 2]; }
+  double sa = 0.0, sb = 0.0;
+  for (int i = 0; i <= 30; ++i) {
+    if (!hp || (i & 1) == 0) { sa += a[i]; sb += b[i]; }
+    else { sa -= a[i]; sb -= b[i]; }
+  }
+  const double gain = sa / (1.0 - sb);
+  for (int i = 0; i <= 30; ++i) a[i] /= gain;
+  for (int i = 0; i <= poles; ++i) { aout[i] = a[i]; bout[i] = b[i]; }
+  return poles;
+}
+
+void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
+  std::memset(t, 0, sizeof *t);
+  t->opt = opt;
+  t->fs = fs_hz;
+  t->dt = 1.0 / fs_hz;
+  t->dtTH = t->dt * TH;
+  t->dtTH1 = t->dt * TH1;
+  t->th1_th = TH1 / TH;
+  t->inv_dtTH = 1.0 / (t->dt * TH);
+  t->noise_amp_F = 1.0 - std::exp(-2.0 * PI * 40.0 * t->dt);
+  t->noise_lp_c = std::exp(-2.0 * PI * 500.0 * t->dt);
+  t->noise_x_2000 = std::exp(-2.0 * PI * (2000.0 * t->dt));
+  t->sqrt12 = std::sqrt(12.0);
+  t->rrad_num = 128 * RHO * CSND;
+  t->lrad_num = 8.0 * RHO;
+  static const double TA[5] = {5.027640021717718e-007, -7.995535578908732e-007, 2.967895557191014e-007, 0.0, 0.0};
+  static const double TB[5] = {0.0, 3.986308869708467, -5.959669638387298, 3.960408461107104, -0.987047716233603};
+  for (int i = 0; i < 5; ++i) { t->tone_a[i] = TA[i]; t->tone_b[i] = TB[i]; }
+  chebyshev(7000.0 / fs_hz, false, 8, t->out_a, t->out_b);
+  static_geometry(t);
+  static_network(t);
+  t->fossa_R0 = 8.0 * MU * t->len[S_FOSSA0] * PI / (AMIN * AMIN);
+  topology(t);
+}
+
+}  // namespace afs

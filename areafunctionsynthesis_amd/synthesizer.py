@@ -1,0 +1,180 @@
+"""Host-side mirror of the reference's synthesis API on top of libafs.so.
+
+* :class:`Context` -- one ``afs_ctx`` (device, sampling rate, solver, TdsModel options).
+* :class:`Synthesizer` -- the stateful ``Synthesizer::synthesizeSignalTds`` equivalent
+  (``src/Backend/Synthesizer.cpp:515-639``) for a batch of independent voices, backed by
+  an ``afs_session`` whose state stays on the GPU.
+* :meth:`Context.synthesize` -- whole trajectories (latch frame 0, then ``F-1`` calls of
+  ``hop`` samples) for ``B`` utterances in one go.
+
+Arrays may be numpy arrays (host) or torch tensors on the GPU (device pointers are
+passed straight to the library).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _native
+from .frames import FRAME_DTYPE
+
+_vp = ctypes.c_void_p
+
+SOLVERS = {"cholesky": _native.AFS_SOLVER_CHOLESKY, "tree": _native.AFS_SOLVER_TREE}
+
+
+def _addr(x) -> int:
+    if x is None:
+        return 0
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    if isinstance(x, np.ndarray):
+        if not x.flags["C_CONTIGUOUS"]:
+            raise ValueError("array must be C-contiguous")
+        return int(x.ctypes.data)
+    raise TypeError(f"unsupported buffer type {type(x)}")
+
+
+def _nbytes(x) -> int:
+    if hasattr(x, "element_size"):
+        return int(x.numel() * x.element_size())
+    return int(x.nbytes)
+
+
+class Context:
+    """An afs_ctx: device + sampling rate + solver + options (TdsModel::Options)."""
+
+    def __init__(self, sampling_rate_hz: float = 22050.0, solver: str = "cholesky", device: int = 0,
+                 async_calls: bool = False, **options):
+        lib = _native.load()
+        cfg = _native.AfsConfig()
+        lib.afs_config_default(ctypes.byref(cfg))
+        cfg.sampling_rate_hz = float(sampling_rate_hz)
+        cfg.solver = SOLVERS[solver]
+        cfg.device = int(device)
+        cfg.flags = _native.AFS_ASYNC if async_calls else 0
+        for k, v in options.items():
+            if not hasattr(cfg.options, k):
+                raise TypeError(f"unknown option {k}")
+            setattr(cfg.options, k, int(bool(v)))
+        h = _vp()
+        _native.check(lib.afs_create(ctypes.byref(h), ctypes.byref(cfg)), None, "afs_create")
+        self._lib = lib
+        self._h = h
+        self.sampling_rate_hz = float(sampling_rate_hz)
+        self.solver = solver
+        self.device = int(device)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.afs_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int) -> None:
+        """Issue all work on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""
+        _native.check(self._lib.afs_set_stream(self._h, _vp(stream_handle)), self._h, "afs_set_stream")
+
+    def synchronize(self) -> None:
+        _native.check(self._lib.afs_synchronize(self._h), self._h, "afs_synchronize")
+
+    def synthesize(self, frames, hop: int, seeds=None, out=None, report: bool = False):
+        """frames[B, F] (FRAME_DTYPE array, or a uint8 torch tensor [B, F, 1072] on the GPU)
+        -> audio[B, (F-1)*hop] float64."""
+        if isinstance(frames, np.ndarray):
+            if frames.dtype != FRAME_DTYPE or frames.ndim != 2:
+                raise ValueError("frames must be a 2-D FRAME_DTYPE array [B, F]")
+            B, F = frames.shape
+            frames = np.ascontiguousarray(frames)
+        else:
+            B, F = int(frames.shape[0]), int(frames.shape[1])
+            if _nbytes(frames) != B * F * FRAME_DTYPE.itemsize:
+                raise ValueError("device frames must hold B*F*1072 bytes")
+        T = (F - 1) * hop
+        if seeds is None:
+            seeds = np.arange(1, B + 1, dtype=np.uint32)
+        if isinstance(seeds, np.ndarray):
+            seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        if out is None:
+            out = np.zeros((B, T), dtype=np.float64)
+        if _nbytes(out) != B * T * 8:
+            raise ValueError("out must hold B*(F-1)*hop doubles")
+        rep = _native.AfsReport()
+        st = self._lib.afs_synthesize(self._h, _vp(_addr(frames)), _vp(_addr(seeds)), B, F, hop,
+                                      _vp(_addr(out)), ctypes.byref(rep))
+        _native.check(st, self._h, "afs_synthesize")
+        if report:
+            return out, {"device_ms": rep.device_ms, "samples": rep.samples,
+                         "nonfinite_utterances": rep.nonfinite_utterances, "kernel": rep.kernel}
+        return out
+
+    def af_to_frames(self, params, frames=None):
+        """OneDimAreaFunction::calculateOneDimTubeFunction on the GPU.
+        params[..., 16] -> frames[...] (tube fields filled; velum/glottis left as given)."""
+        p = np.ascontiguousarray(params, dtype=np.float64)
+        shape = p.shape[:-1]
+        n = int(np.prod(shape)) if shape else 1
+        if frames is None:
+            frames = np.zeros(shape, dtype=FRAME_DTYPE)
+        st = self._lib.afs_af_to_frames(self._h, _vp(_addr(p)), n, _vp(_addr(frames)))
+        _native.check(st, self._h, "afs_af_to_frames")
+        return frames
+
+
+class Synthesizer:
+    """Batch of ``B`` voices with the reference's incremental synthesis semantics.
+
+    ``synthesize_signal_tds(frames, n)`` is ``Synthesizer::synthesizeSignalTds(newTube,
+    newGlottisParams, n, newSignal)`` applied to every voice: the first call after
+    construction / :meth:`reset` only latches the frames and returns an empty array.
+    """
+
+    def __init__(self, context: Context, batch: int = 1, seeds: Optional[Sequence[int]] = None):
+        self.ctx = context
+        self.batch = int(batch)
+        lib = context._lib
+        s = np.arange(1, self.batch + 1, dtype=np.uint32) if seeds is None else np.asarray(seeds, dtype=np.uint32)
+        h = _vp()
+        _native.check(lib.afs_session_create(context.handle, self.batch, _vp(_addr(s)), ctypes.byref(h)),
+                      context.handle, "afs_session_create")
+        self._h = h
+        self._lib = lib
+
+    def reset(self, seeds: Optional[Sequence[int]] = None) -> None:
+        s = np.arange(1, self.batch + 1, dtype=np.uint32) if seeds is None else np.asarray(seeds, dtype=np.uint32)
+        _native.check(self._lib.afs_session_reset(self._h, _vp(_addr(s))), self.ctx.handle, "afs_session_reset")
+
+    def synthesize_signal_tds(self, frames: np.ndarray, num_samples: int) -> np.ndarray:
+        fr = np.ascontiguousarray(np.broadcast_to(frames, (self.batch,)), dtype=FRAME_DTYPE)
+        n = max(int(num_samples), 1)
+        out = np.zeros((self.batch, n), dtype=np.float64)
+        produced = ctypes.c_int32(0)
+        st = self._lib.afs_session_synthesize(self._h, _vp(_addr(fr)), int(num_samples), _vp(_addr(out)),
+                                              ctypes.byref(produced), None)
+        _native.check(st, self.ctx.handle, "afs_session_synthesize")
+        return out[:, : produced.value]
+
+    # reference spelling
+    synthesizeSignalTds = synthesize_signal_tds
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.afs_session_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

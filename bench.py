@@ -1,0 +1,215 @@
+"""Benchmark: batched time-domain tube synthesis on MI355X.
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--seconds S] [--fs HZ]
+For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).
+
+One *step* = one pass of the hot path over this rank's shard of the BASELINE config-4
+batch: B static-vowel utterances (default 8192 per GPU; 65536 at 8 GPUs) of S seconds at
+fs Hz, from frames already resident in HBM to fp64 audio in HBM, plus (N > 1) the RCCL
+gather of the shard's audio to rank 0.  Scaling is weak: per-GPU work is fixed.
+
+Printed (rank 0): one JSON line with the BASELINE metric (whole-node samples/s), the
+roofline object of the dominant kernel and the CPU baseline (the reference's own
+sources, oracle/_ref, timed on this host's cores over a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters (spec)
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (spec)
+FLOPS_PER_SAMPLE = 1.8e4       # reference algorithm, analytic estimate
+
+
+def frame_bytes_per_sample(hop: int) -> float:
+    # one 1072-B frame per hop samples + one 8-B fp64 output sample
+    return 1072.0 / hop + 8.0
+
+
+def cpu_baseline(frames: np.ndarray, seeds: np.ndarray, hop: int, fs: float, n_utt: int, gpu_out: np.ndarray):
+    """Time the reference build (oracle/_ref) on a bounded sample, one process per core."""
+    import multiprocessing as mp
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import REF_SO, ORACLE_SO  # noqa: F401
+
+    kind = "reference" if os.path.exists(REF_SO) else "port"
+    cores = max(1, min(16, os.cpu_count() or 1, n_utt))
+    jobs = [(kind, frames[u], int(seeds[u]), hop, fs) for u in range(n_utt)]
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(cores) as pool:
+        outs = pool.map(_cpu_job, jobs)
+    wall = time.perf_counter() - t0
+    samples = sum(o.size for o in outs)
+    errs = [float(np.abs(gpu_out[u] - outs[u]).max()) for u in range(n_utt)]
+    rmss = [float(np.sqrt(np.mean((gpu_out[u] - outs[u]) ** 2))) for u in range(n_utt)]
+    return {
+        "value": samples / wall,
+        "unit": "samples/s",
+        "cores": cores,
+        "kind": kind,
+        "sample": f"{n_utt} utterances x {frames.shape[1] - 1} frames x {hop} samples @ {fs:g} Hz "
+                  f"(first utterances of this shard), {cores} processes",
+        "wall_s": wall,
+    }, max(errs), max(rmss)
+
+
+def _cpu_job(job):
+    kind, fr, seed, hop, fs = job
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle, RefLib
+    lib = RefLib() if kind == "reference" else Oracle()
+    return lib.utterance(fr, hop, seed, fs)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=8192, help="utterances per GPU")
+    ap.add_argument("--seconds", type=float, default=1.0)
+    ap.add_argument("--fs", type=float, default=44100.0)
+    ap.add_argument("--solver", default=os.environ.get("AFS_SOLVER", "cholesky"))
+    ap.add_argument("--cpu-utterances", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from areafunctionsynthesis_amd.frames import FRAME_DTYPE
+    from areafunctionsynthesis_amd.synthesizer import Context
+    from areafunctionsynthesis_amd.workloads import build_frames, static_vowels
+
+    B = args.batch
+    ctx = Context(args.fs, solver=args.solver, device=local, async_calls=True)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+
+    w = static_vowels(B, seconds=args.seconds, fs=args.fs, first_utterance=rank * B)
+    frames = build_frames(w, ctx.af_to_frames)
+    F, hop, T = w.num_frames, w.hop, w.samples_per_utterance
+    frames_dev = torch.from_numpy(frames.view(np.uint8).reshape(B, F, FRAME_DTYPE.itemsize)).to(dev)
+    seeds_dev = torch.from_numpy(w.seeds.astype(np.int32)).to(dev)
+    out_dev = torch.empty((B, T), dtype=torch.float64, device=dev)
+    gather_list = None
+    if world > 1 and rank == 0:
+        gather_list = [torch.empty_like(out_dev) for _ in range(world)]
+
+    launches_per_step = -(-(F - 1) // max(1, 8192 // hop))
+
+    def step():
+        ctx.synthesize(frames_dev, hop, seeds=seeds_dev, out=out_dev)
+        if world > 1:
+            dist.gather(out_dev, gather_list=gather_list, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        ctx.synthesize(frames_dev, hop, seeds=seeds_dev, out=out_dev)
+        ev[k][1].record(stream)
+        if world > 1:
+            dist.gather(out_dev, gather_list=gather_list, dst=0)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    synth_ms = [a.elapsed_time(b) for a, b in ev]
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    if rank == 0:
+        total_samples = float(world) * B * T * args.steps
+        value = total_samples / elapsed
+        ms_step = elapsed / args.steps * 1e3
+        avg_launch_s = (np.mean(synth_ms) / 1e3) / launches_per_step
+        samples_per_launch = B * T / launches_per_step
+        alg_bytes = samples_per_launch * frame_bytes_per_sample(hop)
+        achieved_gbs = alg_bytes / avg_launch_s / 1e9
+        flops = samples_per_launch * FLOPS_PER_SAMPLE
+        result = {
+            "metric": "audio samples/s (whole node) on 64k-utterance batch; max-abs err vs CPU ref",
+            "value": value,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"BASELINE config 4 shard: {B} static-vowel utterances/GPU x {args.seconds:g} s "
+                            f"@ {args.fs:g} Hz ({B * 8} at 8 GPUs), frames resident in HBM",
+                "batch_per_gpu": B,
+                "global_batch": B * world,
+                "samples_per_utterance": T,
+                "fs_hz": args.fs,
+                "hop": hop,
+                "solver": args.solver,
+                "parallelism": f"dp{world} (utterance shards, RCCL gather of audio to rank 0)" if world > 1
+                               else "dp1",
+            },
+            "x_realtime": value / args.fs,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved_gbs,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved_gbs / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "lane_synth_kernel" if args.solver == "cholesky" else "tree_synth_kernel",
+                "avg_launch_ms": avg_launch_s * 1e3,
+                "launches_per_step": launches_per_step,
+                "bytes_per_sample": frame_bytes_per_sample(hop),
+                "fp64_achieved_tflops": flops / avg_launch_s / 1e12,
+                "fp64_peak_tflops": FP64_PEAK_TFLOPS,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            n = min(args.cpu_utterances, B)
+            gpu_out = out_dev[:n].cpu().numpy()
+            cb, max_abs, max_rms = cpu_baseline(frames[:n], w.seeds[:n], hop, args.fs, n, gpu_out)
+            cb.pop("wall_s")
+            result["cpu_baseline"] = cb
+            result["max_abs_err_vs_cpu_ref"] = max_abs
+            result["max_rms_err_vs_cpu_ref"] = max_rms
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,144 @@
+/*
+ * afs.h -- C ABI of the MI355X batched area-function synthesizer (libafs.so).
+ *
+ * This is the drop-in boundary for the reference's synthesis hot path.  The reference
+ * has no FFI layer; its callers use the C++ class API, and every entry point below
+ * names the reference interface it replaces:
+ *
+ *   afs_session_synthesize  <- Synthesizer::synthesizeSignalTds(Tube*, double*, int, double*)
+ *                              src/Backend/Synthesizer.h:161-162, Synthesizer.cpp:515-639
+ *                              (together with TdsModel::setTube / setFlowSource /
+ *                              setPressureSource / proceedTimeStep, TdsModel.h:267-271, and
+ *                              Glottis::calcGeometry / getTubeData / incTime, Glottis.h:77-82)
+ *   afs_session_reset       <- Synthesizer::reset (Synthesizer.cpp:231-250: TdsModel::resetMotion,
+ *                              TriangularGlottis::resetMotion, output filter reset) + srand(seed)
+ *   afs_synthesize          <- the same driver run over whole trajectories: one latch call on
+ *                              frame 0 then F-1 calls of `hop` samples each, as
+ *                              Synthesizer::synthesizeSegment (Synthesizer.cpp:928-986) and
+ *                              playTargetSequence (:1299-1422) drive it, for B utterances at once
+ *   afs_af_to_frames        <- OneDimAreaFunction::calculateOneDimTubeFunction
+ *                              (src/Backend/OneDimAreaFunction.cpp:75-138)
+ *   afs_options             <- TdsModel::Options (src/Backend/TdsModel.h:83-95)
+ *
+ * Errors: the reference prints and continues (TdsModel.cpp:1832,1849,1898,2267); here every
+ * call returns an afs_status and afs_last_error() holds a message.  Inputs are clamped exactly
+ * as the reference clamps them (areas >= 0.001 cm^2, Tube.cpp:337/371/413).  Non-finite audio
+ * (the reference's "matrix is not positive definite" path) is reported per call in
+ * afs_report.nonfinite_utterances.
+ *
+ * Memory: frames / seeds / out may be host or device (hipMalloc) pointers; the library
+ * detects which.  Device state lives in the session.  One context per host thread.
+ * All work is issued on the context's HIP stream (afs_set_stream) and the calls are
+ * synchronous unless AFS_ASYNC is set in afs_config.flags.
+ */
+#ifndef AFS_H
+#define AFS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AFS_ABI_VERSION 1
+#define AFS_NUM_TUBE_SECTIONS 40   /* Tube::NUM_PHARYNX_MOUTH_SECTIONS (Tube.h:56-58) */
+#define AFS_NUM_GLOTTIS_PARAMS 6   /* TriangularGlottis::NUM_CONTROL_PARAMS (TriangularGlottis.h:26-35) */
+#define AFS_NUM_AF_PARAMS 16       /* OneDimAreaFunction::NUM_AF_PARAMS (OneDimAreaFunction.h:34-43) */
+
+typedef enum afs_status {
+  AFS_OK = 0,
+  AFS_ERR_INVALID_ARGUMENT = 1,
+  AFS_ERR_NO_DEVICE = 2,
+  AFS_ERR_HIP = 3,
+  AFS_ERR_OUT_OF_MEMORY = 4,
+  AFS_ERR_UNSUPPORTED = 5
+} afs_status;
+
+/* Linear solver for the per-sample 97x97 SPD system. */
+typedef enum afs_solver {
+  AFS_SOLVER_CHOLESKY = 0, /* TdsModel::CHOLESKY_FACTORIZATION, same operation order (TdsModel.cpp:2231-2314) */
+  AFS_SOLVER_TREE = 1      /* fill-free leaf-first LDL^T on the tube tree (same system, fewer flops) */
+} afs_solver;
+
+typedef enum afs_precision { AFS_FP64 = 0 } afs_precision;
+
+/* Options of TdsModel (TdsModel.h:83-95), defaults of TdsModel.cpp:35-44. */
+typedef struct afs_options {
+  int32_t turbulence_losses;        /* 1 */
+  int32_t soft_walls;               /* 1 */
+  int32_t generate_noise_sources;   /* 1 */
+  int32_t radiation_from_skin;      /* 1 */
+  int32_t piriform_fossa;           /* 0 */
+  int32_t inner_length_corrections; /* 1 */
+} afs_options;
+
+#define AFS_ASYNC 0x1u
+
+typedef struct afs_config {
+  double sampling_rate_hz; /* reference: 22050 (Constants.h:22-26); any rate is accepted */
+  int32_t precision;       /* afs_precision */
+  int32_t solver;          /* afs_solver */
+  int32_t device;          /* HIP device ordinal */
+  uint32_t flags;          /* AFS_ASYNC */
+  afs_options options;
+} afs_config;
+
+/* One frame = the arguments of one synthesizeSignalTds() call: the dynamic part of the
+ * caller's Tube and the six glottis control parameters.  1072 bytes. */
+typedef struct afs_frame {
+  double area_cm2[AFS_NUM_TUBE_SECTIONS];   /* Tube::pharynxMouthSection[i].area_cm2 */
+  double length_cm[AFS_NUM_TUBE_SECTIONS];  /* .length_cm */
+  double laterality[AFS_NUM_TUBE_SECTIONS]; /* .laterality */
+  double teeth_position_cm;                 /* Tube::teethPosition_cm */
+  double velum_opening_cm2;                 /* argument of Tube::setVelumOpening */
+  double glottis[AFS_NUM_GLOTTIS_PARAMS];   /* f0 Hz, lung pressure dPa, rest disp 1/2 cm, ary area cm^2, aspiration dB */
+  uint8_t articulator[AFS_NUM_TUBE_SECTIONS]; /* Tube::Articulator (Tube.h:24-32) */
+  uint8_t reserved[8];
+} afs_frame;
+
+typedef struct afs_report {
+  double device_ms;              /* time of the synthesis kernels (HIP events) */
+  int64_t samples;               /* audio samples produced (all utterances) */
+  int32_t nonfinite_utterances;  /* utterances whose output contains NaN/Inf */
+  int32_t kernel;                /* which kernel ran (implementation detail, for profiles) */
+} afs_report;
+
+typedef struct afs_ctx afs_ctx;
+typedef struct afs_session afs_session;
+
+void afs_config_default(afs_config *cfg);
+const char *afs_status_string(afs_status s);
+int32_t afs_abi_version(void);
+
+afs_status afs_create(afs_ctx **ctx, const afs_config *cfg);
+void afs_destroy(afs_ctx *ctx);
+const char *afs_last_error(const afs_ctx *ctx);
+/* Use this hipStream_t (passed as void*) for all work of the context; NULL = default stream. */
+afs_status afs_set_stream(afs_ctx *ctx, void *hip_stream);
+afs_status afs_synchronize(afs_ctx *ctx);
+
+/* Whole trajectories.  frames[batch][num_frames], seeds[batch] (srand() seed per utterance,
+ * 0 behaves as 1 like glibc), out[batch][(num_frames-1)*hop] doubles in [-1,1]. */
+afs_status afs_synthesize(afs_ctx *ctx, const afs_frame *frames, const uint32_t *seeds,
+                          int32_t batch, int32_t num_frames, int32_t hop, double *out,
+                          afs_report *report);
+
+/* Stateful sessions: B independent Synthesizer instances living on the device. */
+afs_status afs_session_create(afs_ctx *ctx, int32_t batch, const uint32_t *seeds, afs_session **s);
+/* One synthesizeSignalTds(newTube, glottisParams, num_samples, newSignal) call for every
+ * utterance: frames[batch], out[batch][max(num_samples,1)].  The first call after create/reset
+ * only latches the frames and produces no samples (*produced = 0). */
+afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32_t num_samples,
+                                  double *out, int32_t *produced, afs_report *report);
+afs_status afs_session_reset(afs_session *s, const uint32_t *seeds);
+void afs_session_destroy(afs_session *s);
+
+/* Area-function model -> tube frames (pharynx/mouth part, teeth).  params[n][16] in
+ * OneDimAreaFunction::ParamIndex order; velum and glottis fields of frames are left unchanged. */
+afs_status afs_af_to_frames(afs_ctx *ctx, const double *params, int64_t n, afs_frame *frames);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AFS_H */

@@ -1,0 +1,125 @@
+"""Generate the golden vectors in tests/golden/ from the REFERENCE build.
+
+Run in the build container (needs /root/reference for oracle/_ref):
+    python tests/golden/make_golden.py
+
+Every expected value comes from oracle/_ref/libafsref.so -- the reference's own
+TdsModel / Tube / TriangularGlottis / IirFilter sources compiled unmodified and driven
+through their public API -- or from glibc itself (rand).  Inputs (frames) are stored
+next to the outputs so the GPU box needs neither the reference nor the generator.
+
+The one exception is af_frames.npz: OneDimAreaFunction is not buildable from the
+reference here (wxWidgets), so those expected frames come from the C restatement and
+are marked "restatement" (parity against the reference unpinned for that row).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from oracle_lib import Oracle, RefLib  # noqa: E402
+
+from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS, FRAME_DTYPE  # noqa: E402
+from areafunctionsynthesis_amd.params import default_shapes  # noqa: E402
+
+
+def static(o: Oracle, shape, F, velum=0.0, glottis=DEFAULT_GLOTTIS):
+    f = o.af_to_frame(shape)
+    f["velum_opening_cm2"] = velum
+    f["glottis"] = glottis
+    return np.repeat(f[None], F)
+
+
+def trajectory(o: Oracle, shapes, names, F, rng, lateral=False):
+    fr = np.zeros(F, FRAME_DTYPE)
+    for k in range(F):
+        f = o.af_to_frame(shapes[names[k * len(names) // F]] * (1 + 0.01 * rng.standard_normal(16)))
+        f["velum_opening_cm2"] = 0.3 if k % 3 == 0 else 0.0
+        if lateral:
+            f["laterality"] = np.clip(rng.uniform(-0.2, 0.3, 40), 0, 1)
+        f["glottis"] = [110 + 20 * np.sin(k), 8000 - 200 * k, 0.01, 0.012, 0.01 * (k % 2), -40 + 3 * k]
+        fr[k] = f
+    return fr
+
+
+def main() -> None:
+    o = Oracle()
+    r = RefLib()
+    sh = default_shapes()
+
+    # glibc rand() streams (srand(seed) then rand()), seeds 1..4 and two large ones
+    seeds = np.array([1, 2, 3, 4, 12345, 4294967295], dtype=np.uint64)
+    np.savez_compressed(os.path.join(HERE, "rand_glibc.npz"), seeds=seeds,
+                        values=np.stack([r.glibc_rand(int(s), 4096) for s in seeds]))
+
+    # IirFilter::createChebyshev for the output filter at both rates, plus other orders
+    cases = [(7000 / 22050, 8), (7000 / 44100, 8), (25 / 44100, 4), (50 / 22050, 4), (0.1, 6)]
+    a_all, b_all = [], []
+    for ratio, poles in cases:
+        a, b = r.chebyshev(ratio, poles)
+        a_all.append(np.pad(a, (0, 9 - a.size)))
+        b_all.append(np.pad(b, (0, 9 - b.size)))
+    np.savez_compressed(os.path.join(HERE, "chebyshev.npz"), ratio=np.array([c[0] for c in cases]),
+                        poles=np.array([c[1] for c in cases]), a=np.stack(a_all), b=np.stack(b_all))
+
+    # per-step state of static /a:/ at 22050 Hz: pressures and currents after every sample
+    fr = static(o, sh["a:"], 2)
+    h = r.create(22050.0, 1)
+    r.call(h, fr[0], 64)
+    P, U, Y = [], [], []
+    for _ in range(64):
+        Y.append(r.call(h, fr[1], 1)[0])
+        P.append(r.pressures(h))
+        U.append(r.currents(h))
+    r.destroy(h)
+    np.savez_compressed(os.path.join(HERE, "steps_a.npz"), frames=fr, fs=22050.0, seed=1,
+                        pressures=np.stack(P), currents=np.stack(U), out=np.array(Y))
+
+    # whole utterances: inputs + reference outputs
+    rng = np.random.default_rng(2024)
+    cases = [
+        ("a:", static(o, sh["a:"], 11), 220, 1, 22050.0),
+        ("i:", static(o, sh["i:"], 11), 220, 2, 22050.0),
+        ("u:@44k", static(o, sh["u:"], 11), 441, 3, 44100.0),
+        ("s+velum", static(o, sh["s"], 11, velum=1.0), 220, 4, 22050.0),
+        ("f", static(o, sh["f"], 11), 220, 5, 22050.0),
+        ("(a)b(a):", static(o, sh["(a)b(a):"], 11), 220, 6, 22050.0),
+        ("vcv-aba@44k", trajectory(o, sh, ["a:", "(a)b(a):", "a:"], 12, rng), 200, 7, 44100.0),
+        ("x-lateral", trajectory(o, sh, ["x", "S", "C"], 12, rng, lateral=True), 200, 0, 22050.0),
+    ]
+    names, frames, hops, useeds, fss, outs = [], [], [], [], [], []
+    for name, fr, hop, seed, fs in cases:
+        y = r.utterance(fr, hop, seed, fs)[:2048]
+        names.append(name)
+        frames.append(fr)
+        hops.append(hop)
+        useeds.append(seed)
+        fss.append(fs)
+        outs.append(y)
+    Fmax = max(f.size for f in frames)
+    fpad = np.zeros((len(frames), Fmax), FRAME_DTYPE)
+    nfr = np.array([f.size for f in frames])
+    for i, f in enumerate(frames):
+        fpad[i, : f.size] = f
+    np.savez_compressed(os.path.join(HERE, "utterances.npz"), names=np.array(names), frames=fpad.view(np.uint8),
+                        num_frames=nfr, hop=np.array(hops), seed=np.array(useeds), fs=np.array(fss),
+                        out=np.stack(outs))
+
+    # area function -> tube (restatement; reference unbuildable for this row)
+    names = sorted(sh)
+    P = np.stack([sh[n] for n in names])
+    F = np.stack([o.af_to_frame(p) for p in P])
+    np.savez_compressed(os.path.join(HERE, "af_frames.npz"), names=np.array(names), params=P,
+                        area=F["area_cm2"], length=F["length_cm"], articulator=F["articulator"],
+                        teeth=F["teeth_position_cm"], source=np.array("restatement"))
+    print("golden vectors written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,202 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the oracle and the golden
+vectors of the reference build.
+
+Tolerances (fp64 path): the kernels keep the reference's operand order, so the only
+differences come from device libm (exp for noise cutoffs below the 2 kHz clamp, pow for
+the aspiration gain); those ulp-level differences are amplified by the chaotic
+glottis/tube dynamics (trap 3).  Bounds used below:
+  * golden / oracle, first 2048 samples:   max |err| <= 1e-9
+  * oracle, 1 s @ 44.1 kHz (north star):   per-utterance RMS <= 1e-4, reported max-abs
+Integer/bookkeeping behaviour (batch independence, session == trajectory, seeds,
+latching) is checked bit for bit.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS, FRAME_DTYPE
+from areafunctionsynthesis_amd.params import default_shapes
+
+pytestmark = pytest.mark.gpu
+
+GOLD_TOL = 1e-9
+RMS_TOL = 1e-4
+SOLVERS = ("cholesky",)
+
+
+@pytest.fixture(scope="module")
+def contexts():
+    from areafunctionsynthesis_amd.synthesizer import Context
+    cache = {}
+
+    def get(fs, solver="cholesky", **opt):
+        key = (fs, solver, tuple(sorted(opt.items())))
+        if key not in cache:
+            cache[key] = Context(fs, solver=solver, **opt)
+        return cache[key]
+
+    yield get
+    for c in cache.values():
+        c.close()
+
+
+def golden(golden_dir):
+    g = np.load(os.path.join(golden_dir, "utterances.npz"), allow_pickle=False)
+    return g, g["frames"].view(FRAME_DTYPE)
+
+
+def static_frames(oracle, name, F, velum=0.0, glottis=DEFAULT_GLOTTIS):
+    f = oracle.af_to_frame(default_shapes()[name])
+    f["velum_opening_cm2"] = velum
+    f["glottis"] = glottis
+    return np.repeat(f[None], F)
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_golden_utterances(contexts, golden_dir, solver):
+    g, frames = golden(golden_dir)
+    n = g["out"].shape[1]
+    for i, name in enumerate(g["names"]):
+        fr = frames[i, : g["num_frames"][i]][None]
+        ctx = contexts(float(g["fs"][i]), solver)
+        y = ctx.synthesize(np.ascontiguousarray(fr), int(g["hop"][i]), seeds=np.array([g["seed"][i]], np.uint32))
+        err = np.abs(y[0, :n] - g["out"][i]).max()
+        assert err <= GOLD_TOL, (name, err)
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_golden_per_step_outputs(contexts, golden_dir, solver):
+    g = np.load(os.path.join(golden_dir, "steps_a.npz"), allow_pickle=False)
+    fr = g["frames"]
+    ctx = contexts(float(g["fs"]), solver)
+    y = ctx.synthesize(np.ascontiguousarray(fr[None]), 64, seeds=np.array([g["seed"]], np.uint32))
+    assert np.abs(y[0] - g["out"]).max() <= GOLD_TOL
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_batch_vs_oracle_mixed(contexts, oracle, solver):
+    """70 utterances (ragged: not a multiple of 64) of mixed vowels, fricatives with an
+    open velum and laterality, random glottis settings, vs the oracle."""
+    sh = default_shapes()
+    names = ["a:", "i:", "u:", "e:", "o:", "s", "f", "x", "S", "(a)b(a):", "l", "C"]
+    rng = np.random.default_rng(7)
+    B, F, hop, fs = 70, 9, 256, 22050.0
+    frames = np.zeros((B, F), FRAME_DTYPE)
+    for u in range(B):
+        for k in range(F):
+            f = oracle.af_to_frame(sh[names[(u + k // 4) % len(names)]] * (1 + 0.01 * rng.standard_normal(16)))
+            f["velum_opening_cm2"] = (0.0, 1.0)[u % 2]
+            f["laterality"] = np.clip(rng.uniform(-0.5, 0.3, 40), 0, 1) if u % 5 == 0 else 0.0
+            f["glottis"] = [rng.uniform(90, 180), rng.uniform(6000, 10000), 0.01, 0.01, 0.0, -40.0 + 20 * (u % 3)]
+            frames[u, k] = f
+    seeds = np.arange(1, B + 1, dtype=np.uint32)
+    y = contexts(fs, solver).synthesize(frames, hop, seeds=seeds)
+    for u in range(B):
+        x = oracle.utterance(frames[u], hop, int(seeds[u]), fs)
+        err = np.abs(y[u] - x).max()
+        assert err <= GOLD_TOL, (u, err)
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_batch_independence_bitwise(contexts, oracle, solver):
+    """An utterance's audio does not depend on its batch-mates or its slot."""
+    ctx = contexts(22050.0, solver)
+    a = static_frames(oracle, "a:", 4)
+    s = static_frames(oracle, "s", 4, velum=1.0)
+    alone = ctx.synthesize(np.ascontiguousarray(s[None]), 128, seeds=np.array([9], np.uint32))
+    batch = np.stack([a] * 40 + [s] + [a] * 30)
+    seeds = np.arange(1, 72, dtype=np.uint32)
+    seeds[40] = 9
+    y = ctx.synthesize(batch, 128, seeds=seeds)
+    assert np.array_equal(y[40], alone[0])
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_session_equals_trajectory(contexts, oracle, solver):
+    """afs_session_synthesize called frame by frame == afs_synthesize on the whole
+    trajectory (Synthesizer::synthesizeSignalTds incremental semantics)."""
+    from areafunctionsynthesis_amd.synthesizer import Synthesizer
+    ctx = contexts(22050.0, solver)
+    sh = default_shapes()
+    B, F, hop = 3, 6, 150
+    frames = np.zeros((B, F), FRAME_DTYPE)
+    for u in range(B):
+        for k in range(F):
+            f = oracle.af_to_frame(sh[["a:", "(a)d(a):", "i:", "s"][(u + k) % 4]])
+            f["glottis"] = [100 + 10 * k, 8000, 0.01, 0.01, 0, -40]
+            frames[u, k] = f
+    seeds = np.array([3, 4, 5], np.uint32)
+    y = ctx.synthesize(frames, hop, seeds=seeds)
+    syn = Synthesizer(ctx, B, seeds)
+    assert syn.synthesize_signal_tds(frames[:, 0], hop).shape == (B, 0)   # latch only
+    parts = [syn.synthesize_signal_tds(frames[:, k], hop) for k in range(1, F)]
+    assert np.array_equal(np.concatenate(parts, axis=1), y)
+    syn.reset(seeds)
+    syn.synthesize_signal_tds(frames[:, 0], hop)
+    assert np.array_equal(syn.synthesize_signal_tds(frames[:, 1], hop), y[:, :hop])
+    # numNewSamples < 1 produces one sample (Synthesizer.cpp:543-546)
+    assert syn.synthesize_signal_tds(frames[:, 2], 0).shape == (B, 1)
+    syn.close()
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_edge_cases(contexts, oracle, solver):
+    ctx = contexts(44100.0, solver)
+    fr = static_frames(oracle, "u:", 2)
+    # hop = 1, two frames, single utterance
+    y = ctx.synthesize(np.ascontiguousarray(fr[None]), 1, seeds=np.array([1], np.uint32))
+    assert y.shape == (1, 1)
+    assert np.abs(y[0] - oracle.utterance(fr, 1, 1, 44100.0)).max() <= GOLD_TOL
+    # seed 0 behaves as glibc's srand(0) == srand(1)
+    s = static_frames(oracle, "s", 3, velum=1.0)
+    y0 = ctx.synthesize(np.ascontiguousarray(s[None]), 300, seeds=np.array([0], np.uint32))
+    y1 = ctx.synthesize(np.ascontiguousarray(s[None]), 300, seeds=np.array([1], np.uint32))
+    assert np.array_equal(y0, y1)
+    # invalid arguments are rejected with a status, not a crash
+    from areafunctionsynthesis_amd._native import AfsError
+    with pytest.raises(AfsError):
+        ctx.synthesize(np.ascontiguousarray(fr[None][:, :1]), 10)
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_nonfinite_is_reported(contexts, oracle, solver):
+    """The reference keeps going after a non-positive-definite pivot and yields NaN;
+    the library reproduces that and reports it per call."""
+    ctx = contexts(22050.0, solver)
+    f = oracle.af_to_frame(default_shapes()["a:"])
+    f["glottis"] = [40.0, 20000.0, -0.05, 0.3, 0.5, 0.0]
+    f["area_cm2"][:] = 1e-9
+    fr = np.repeat(f[None], 3)
+    x = oracle.utterance(fr, 200, 1, 22050.0)
+    y, rep = ctx.synthesize(np.ascontiguousarray(fr[None]), 200, report=True)
+    assert np.isfinite(y).all() == np.isfinite(x).all()
+    assert rep["nonfinite_utterances"] == (0 if np.isfinite(x).all() else 1)
+
+
+def test_af_to_frames_vs_restatement(contexts, golden_dir):
+    g = np.load(os.path.join(golden_dir, "af_frames.npz"), allow_pickle=False)
+    fr = contexts(22050.0).af_to_frames(g["params"])
+    assert np.array_equal(fr["articulator"], g["articulator"])
+    assert np.array_equal(fr["length_cm"], g["length"])
+    assert np.array_equal(fr["teeth_position_cm"], g["teeth"])
+    assert np.allclose(fr["area_cm2"], g["area"], rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_full_second_static_vowels_rms(contexts, oracle, solver):
+    """Config 2 at full length: 1024 utterances x 1 s @ 44.1 kHz on the GPU; every 128th
+    utterance re-synthesised by the oracle.  North-star bound: RMS < 1e-4 per utterance."""
+    from areafunctionsynthesis_amd.workloads import build_frames, static_vowels
+    ctx = contexts(44100.0, solver)
+    w = static_vowels(1024, seconds=1.0, fs=44100.0)
+    frames = build_frames(w, ctx.af_to_frames)
+    y, rep = ctx.synthesize(frames, w.hop, seeds=w.seeds, report=True)
+    assert rep["nonfinite_utterances"] == 0
+    for u in range(0, 1024, 128):
+        x = oracle.utterance(frames[u], w.hop, int(w.seeds[u]), w.fs)
+        rms = float(np.sqrt(np.mean((y[u] - x) ** 2)))
+        assert rms < RMS_TOL, (u, rms, float(np.abs(y[u] - x).max()))
+    # deterministic: a second run is bitwise identical
+    y2 = ctx.synthesize(frames, w.hop, seeds=w.seeds)
+    assert np.array_equal(y, y2)

@@ -1,0 +1,91 @@
+"""CPU-only checks of the product boundary: libafs.so builds, loads and exports every
+symbol include/afs.h declares; host-side logic (formats, workloads) behaves.
+No compute calls are made here (there is no GPU in the build container)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from areafunctionsynthesis_amd import _native
+from areafunctionsynthesis_amd.frames import FRAME_DTYPE
+from areafunctionsynthesis_amd.params import Shape, default_shapes, read_params, write_params
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    txt = open(os.path.join(ROOT, "include", "afs.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(afs_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_header_and_binding_agree():
+    assert sorted(_native.EXPORTED) == declared_functions()
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.afs_abi_version() == 1
+
+
+def test_config_defaults_mirror_tdsmodel_options():
+    lib = _native.load()
+    cfg = _native.AfsConfig()
+    lib.afs_config_default(ctypes.byref(cfg))
+    assert cfg.sampling_rate_hz == 22050.0
+    o = cfg.options
+    assert (o.turbulence_losses, o.soft_walls, o.generate_noise_sources, o.radiation_from_skin,
+            o.piriform_fossa, o.inner_length_corrections) == (1, 1, 1, 1, 0, 1)
+
+
+def test_create_fails_loudly_without_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(_native.AfsError):
+        from areafunctionsynthesis_amd.synthesizer import Context
+        Context()
+
+
+def test_status_strings():
+    lib = _native.load()
+    assert lib.afs_status_string(0) == b"ok"
+    assert lib.afs_status_string(2) == b"no HIP device"
+
+
+def test_frame_record_layout():
+    assert FRAME_DTYPE.itemsize == 1072
+    assert FRAME_DTYPE.fields["glottis"][1] == 40 * 8 * 3 + 16
+    assert FRAME_DTYPE.fields["articulator"][1] == 1024
+
+
+def test_params_roundtrip(tmp_path):
+    shapes = [Shape(k, v) for k, v in default_shapes().items()]
+    path = tmp_path / "x.params"
+    write_params(str(path), shapes)
+    back = read_params(str(path))
+    assert [s.name for s in back] == [s.name for s in shapes]
+    for a, b in zip(shapes, back):
+        assert np.allclose(a.params, b.params, atol=5e-7)
+
+
+def test_workload_sharding_is_consistent():
+    from areafunctionsynthesis_amd.workloads import static_vowels
+    full = static_vowels(16, seconds=0.05)
+    part = static_vowels(6, seconds=0.05, first_utterance=10)
+    assert np.array_equal(full.params[10:], part.params)
+    assert np.array_equal(full.glottis[10:], part.glottis)
+    assert np.array_equal(full.seeds[10:], part.seeds)
+    assert full.samples_per_utterance == 2205
+
+
+def test_vcv_workload_shapes():
+    from areafunctionsynthesis_amd.workloads import vcv
+    w = vcv(3)
+    assert w.params.shape[0] == 3 and w.hop == 441
+    assert (w.glottis[:, 0, 1] == 0.0).all()   # 50 ms of silence at the start
+    assert w.glottis[:, :, 1].max() == 8000.0
