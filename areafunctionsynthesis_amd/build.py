@@ -14,12 +14,12 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libafs.so")
 ARCH = os.environ.get("AFS_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["afs_capi.cpp", "afs_tables.cpp", "tds_lane.hip", "af_kernels.hip"]
-HEADERS = ["afs_model.h", "afs_lane.h", os.path.join("..", "..", "include", "afs.h")]
+SOURCES = ["afs_capi.cpp", "afs_tables.cpp", "tds_lane.hip", "tds_tree.hip", "af_kernels.hip"]
+HEADERS = ["afs_model.h", "afs_lane.h", "afs_tree.h", "tree_core.h", os.path.join("..", "..", "include", "afs.h")]
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
           # keep the reference's rounding: no contraction of a*b+c into fma
-          "-ffp-contract=off"]
+          "-ffp-contract=off", "-fno-strict-aliasing", "-Wno-unknown-pragmas"]
 
 
 def _hipcc() -> str:

@@ -13,6 +13,7 @@
 
 #include "afs_lane.h"
 #include "afs_model.h"
+#include "afs_tree.h"
 
 static_assert(sizeof(afs_frame) == 1072, "afs_frame layout");
 
@@ -27,6 +28,8 @@ struct afs_ctx {
   size_t ws_bytes = 0;
   int32_t *rng = nullptr;
   size_t rng_bytes = 0;
+  void *tree_lanes = nullptr;
+  size_t tree_lanes_bytes = 0;
   void *stage_in = nullptr;
   size_t stage_in_bytes = 0;
   void *stage_out = nullptr;
@@ -41,8 +44,9 @@ struct afs_session {
   afs_ctx *ctx = nullptr;
   int B = 0;
   int64_t bp = 0;
-  void *ws = nullptr;
-  int32_t *rng = nullptr;
+  void *ws = nullptr;          // lane solver: SoA workspace; tree solver: per-utterance LDS blocks
+  int32_t *rng = nullptr;      // lane solver: generator state; tree solver: unused
+  void *tree_lanes = nullptr;  // tree solver: per-lane register state
   afs_frame *pair = nullptr;   // [B][2]: previous frame, new frame
   uint32_t *seeds = nullptr;   // device copy
   bool latched = false;
@@ -91,34 +95,53 @@ afs_status ensure(afs_ctx *c, void **buf, size_t *cap, size_t bytes) {
 
 int64_t pad64(int64_t b) { return (b + 63) / 64 * 64; }
 
-bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY; }
+bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_TREE; }
 
-// Launch the synthesis for frame transitions [k0, k1) in chunks that keep each kernel short.
+bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE; }
+
+// Launch the synthesis for frame transitions [k0, k1) in chunks that keep each kernel
+// well below a second (state is carried between launches).
 afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int k0, int k1, int hop,
-                      double *out, int64_t ostride, void *ws, int32_t *rng, int64_t bp, int B) {
-  const int64_t max_samples = 8192;
+                      double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B) {
+  const int64_t max_samples = tree(c) ? 65536 : 8192;
   int per = (int)std::max<int64_t>(1, max_samples / std::max(1, hop));
   for (int k = k0; k < k1; k += per) {
     int ke = std::min(k1, k + per);
-    afs::LaneArgs a{c->dev_tab, frames, fstride, k, ke, hop, out + (int64_t)(k - k0) * hop, ostride,
-                    (double *)ws, rng, bp, B};
-    HIP_TRY(c, afs::launch_lane_synth(a, c->stream));
+    double *o = out + (int64_t)(k - k0) * hop;
+    if (tree(c)) {
+      afs::TreeArgs a{c->dev_tab, frames, fstride, k, ke, hop, o, ostride, lanes, (double *)ws, B};
+      HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
+    } else {
+      afs::LaneArgs a{c->dev_tab, frames, fstride, k, ke, hop, o, ostride, (double *)ws, rng, bp, B};
+      HIP_TRY(c, afs::launch_lane_synth(a, c->stream));
+    }
   }
   return AFS_OK;
 }
 
-int64_t ws_rows(const afs_ctx *c) {
-  return afs::lane_ws_rows(c->host_tab);
+// bytes of the state buffers for B utterances
+size_t ws_bytes_for(const afs_ctx *c, int64_t bp) {
+  if (tree(c)) return (size_t)bp * afs::tree_lds_doubles() * sizeof(double);
+  return (size_t)(afs::lane_ws_rows(c->host_tab) * bp) * sizeof(double);
+}
+size_t lanes_bytes_for(const afs_ctx *c, int64_t bp) {
+  return tree(c) ? (size_t)bp * afs::TREE_W * afs::tree_lane_bytes() : 0;
 }
 
-afs_status reset_state(afs_ctx *c, void *ws, int32_t *rng, int64_t bp, int B, const uint32_t *seeds_dev) {
-  HIP_TRY(c, afs::launch_lane_reset((double *)ws, rng, bp, B, seeds_dev, c->stream));
+afs_status reset_state(afs_ctx *c, void *ws, int32_t *rng, void *lanes, int64_t bp, int B, const uint32_t *seeds_dev) {
+  if (tree(c))
+    HIP_TRY(c, afs::launch_tree_reset(lanes, (double *)ws, B, seeds_dev, c->stream));
+  else
+    HIP_TRY(c, afs::launch_lane_reset((double *)ws, rng, bp, B, seeds_dev, c->stream));
   return AFS_OK;
 }
 
 afs_status count_nonfinite(afs_ctx *c, void *ws, int64_t bp, int B, int32_t *out) {
   HIP_TRY(c, hipMemsetAsync(c->dcount, 0, sizeof(int32_t), c->stream));
-  HIP_TRY(c, afs::launch_lane_nonfinite((const double *)ws, bp, B, c->dcount, c->stream));
+  if (tree(c))
+    HIP_TRY(c, afs::launch_tree_nonfinite((const double *)ws, B, c->dcount, c->stream));
+  else
+    HIP_TRY(c, afs::launch_lane_nonfinite((const double *)ws, bp, B, c->dcount, c->stream));
   HIP_TRY(c, hipMemcpyAsync(out, c->dcount, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   return AFS_OK;
 }
@@ -134,7 +157,7 @@ void afs_config_default(afs_config *cfg) {
   std::memset(cfg, 0, sizeof *cfg);
   cfg->sampling_rate_hz = 22050.0;
   cfg->precision = AFS_FP64;
-  cfg->solver = AFS_SOLVER_CHOLESKY;
+  cfg->solver = AFS_SOLVER_TREE;
   cfg->device = 0;
   cfg->flags = 0;
   cfg->options.turbulence_losses = 1;
@@ -174,6 +197,7 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   afs_ctx *ctx = new afs_ctx();
   ctx->cfg = c;
   afs::build_tables(&ctx->host_tab, c.sampling_rate_hz, c.options);
+  if (ctx->host_tab.n_rounds <= 0) { afs_destroy(ctx); return AFS_ERR_UNSUPPORTED; }
   afs_status st = AFS_OK;
   auto bail = [&](afs_status s) { afs_destroy(ctx); return s; };
   if (hipMalloc((void **)&ctx->dev_tab, sizeof(afs::Tables)) != hipSuccess) return bail(AFS_ERR_OUT_OF_MEMORY);
@@ -192,6 +216,7 @@ void afs_destroy(afs_ctx *c) {
   if (c->dev_tab) (void)hipFree(c->dev_tab);
   if (c->ws) (void)hipFree(c->ws);
   if (c->rng) (void)hipFree(c->rng);
+  if (c->tree_lanes) (void)hipFree(c->tree_lanes);
   if (c->stage_in) (void)hipFree(c->stage_in);
   if (c->stage_out) (void)hipFree(c->stage_out);
   if (c->stage_seeds) (void)hipFree(c->stage_seeds);
@@ -245,11 +270,12 @@ afs_status afs_synthesize(afs_ctx *c, const afs_frame *frames, const uint32_t *s
     dout = (double *)c->stage_out;
   }
   // state
-  if ((s = ensure(c, &c->ws, &c->ws_bytes, (size_t)(ws_rows(c) * bp) * sizeof(double))) != AFS_OK) return s;
+  if ((s = ensure(c, &c->ws, &c->ws_bytes, ws_bytes_for(c, bp))) != AFS_OK) return s;
   if ((s = ensure(c, (void **)&c->rng, &c->rng_bytes, (size_t)(32 * bp) * sizeof(int32_t))) != AFS_OK) return s;
-  if ((s = reset_state(c, c->ws, c->rng, bp, B, dseeds)) != AFS_OK) return s;
+  if (tree(c) && (s = ensure(c, &c->tree_lanes, &c->tree_lanes_bytes, lanes_bytes_for(c, bp))) != AFS_OK) return s;
+  if ((s = reset_state(c, c->ws, c->rng, c->tree_lanes, bp, B, dseeds)) != AFS_OK) return s;
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-  if ((s = run_chunks(c, dframes, F, 1, F, hop, dout, T, c->ws, c->rng, bp, B)) != AFS_OK) return s;
+  if ((s = run_chunks(c, dframes, F, 1, F, hop, dout, T, c->ws, c->rng, c->tree_lanes, bp, B)) != AFS_OK) return s;
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   int32_t nonfinite = 0;
   if ((s = count_nonfinite(c, c->ws, bp, B, &nonfinite)) != AFS_OK) return s;
@@ -279,8 +305,9 @@ afs_status afs_session_create(afs_ctx *c, int32_t B, const uint32_t *seeds, afs_
     return fail(c, e == hipErrorOutOfMemory ? AFS_ERR_OUT_OF_MEMORY : AFS_ERR_HIP, "session alloc: %s", hipGetErrorString(e));
   };
   hipError_t e;
-  if ((e = hipMalloc(&s->ws, (size_t)(ws_rows(c) * s->bp) * sizeof(double))) != hipSuccess) return bail(e);
+  if ((e = hipMalloc(&s->ws, ws_bytes_for(c, s->bp))) != hipSuccess) return bail(e);
   if ((e = hipMalloc((void **)&s->rng, (size_t)(32 * s->bp) * sizeof(int32_t))) != hipSuccess) return bail(e);
+  if (tree(c) && (e = hipMalloc(&s->tree_lanes, lanes_bytes_for(c, s->bp))) != hipSuccess) return bail(e);
   if ((e = hipMalloc((void **)&s->pair, (size_t)B * 2 * sizeof(afs_frame))) != hipSuccess) return bail(e);
   if ((e = hipMalloc((void **)&s->seeds, (size_t)B * sizeof(uint32_t))) != hipSuccess) return bail(e);
   *out = s;
@@ -302,7 +329,7 @@ afs_status afs_session_reset(afs_session *s, const uint32_t *seeds) {
   } else {
     HIP_TRY(c, hipMemsetAsync(s->seeds, 0, (size_t)s->B * 4, c->stream));
   }
-  afs_status st = reset_state(c, s->ws, s->rng, s->bp, s->B, s->seeds);
+  afs_status st = reset_state(c, s->ws, s->rng, s->tree_lanes, s->bp, s->B, s->seeds);
   if (st != AFS_OK) return st;
   s->latched = false;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -313,6 +340,7 @@ void afs_session_destroy(afs_session *s) {
   if (!s) return;
   if (s->ws) (void)hipFree(s->ws);
   if (s->rng) (void)hipFree(s->rng);
+  if (s->tree_lanes) (void)hipFree(s->tree_lanes);
   if (s->pair) (void)hipFree(s->pair);
   if (s->seeds) (void)hipFree(s->seeds);
   delete s;
@@ -346,7 +374,7 @@ afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32
     dout = (double *)c->stage_out;
   }
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-  if ((st = run_chunks(c, s->pair, 2, 1, 2, n, dout, n, s->ws, s->rng, s->bp, B)) != AFS_OK) return st;
+  if ((st = run_chunks(c, s->pair, 2, 1, 2, n, dout, n, s->ws, s->rng, s->tree_lanes, s->bp, B)) != AFS_OK) return st;
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   // prevTube = *newTube (Synthesizer.cpp:633-637)
   HIP_TRY(c, hipMemcpy2DAsync(s->pair, 2 * sizeof(afs_frame), s->pair + 1, 2 * sizeof(afs_frame),

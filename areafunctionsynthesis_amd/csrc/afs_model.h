@@ -59,6 +59,18 @@ AFS_HD constexpr bool is_static_section(int s) {
   return s <= S_LAST_TRACHEA || (s >= S_NOSE0 + 4);
 }
 
+// Fill-free leaf-first LDL^T schedule for the per-sample system (tree solver).
+// Edges of the current graph: for section s with in-current a and out-currents b (c),
+// edge[s][0] = (a,b), edge[s][1] = (a,c), edge[s][2] = (b,c).  In round r, chain lane k
+// eliminates step[r][k].c, whose remaining neighbours are n0 (and n1) through edges e0
+// (e1); e01 is the edge n0-n1 that receives the fill-free update.  c = -1: idle.
+constexpr int TREE_CHAINS = 4;
+constexpr int TREE_MAX_ROUNDS = 40;
+constexpr int TREE_NE = 104;
+struct SolveStep {
+  int16_t c, n0, n1, e0, e1, e01;
+};
+
 struct Tables {
   // time step and derived scalars
   double fs, dt, dtTH, dtTH1, th1_th, inv_dtTH;
@@ -83,6 +95,11 @@ struct Tables {
   int16_t env_start[NC], env_n[NC], env_off[NC];
   int16_t col_n[NC], col[NC][ENV_COLS];
   int32_t env_total;
+
+  // tree solver
+  int16_t edge[NS][3];
+  int32_t n_edges, n_rounds;
+  SolveStep step[TREE_MAX_ROUNDS][TREE_CHAINS];
 
   afs_options opt;
 };

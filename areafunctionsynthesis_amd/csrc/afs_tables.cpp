@@ -4,8 +4,10 @@
 // IEEE double (no FMA contraction: this file is built with -ffp-contract=off), so the
 // constants the kernels read are bit-identical to what the reference recomputes each
 // sample for the same sections.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 #include "afs_model.h"
 
@@ -139,6 +141,115 @@ void topology(Tables *t) {
   }
 }
 
+// Edges of the current graph and the elimination schedule of the tree solver.
+// Chains (eliminated concurrently by 4 lanes, one step per round):
+//   lane 0: trachea + glottis + lower pharynx, from the lungs up:  0, 1, ..., 31
+//   lane 1: lips inward: 94, 93 (mouth radiation), 64, 63, ..., 34
+//   lane 2: nostrils inward: 96, 95, 83, 82, ..., 65 (the sinus leaves are gone by then)
+//   lane 3: paranasal sinuses 89..92, then the piriform fossa 88, ..., 84
+// then 32 and finally the root 33.  build_schedule() checks that every elimination is
+// fill-free and that no two lanes touch the same unknown in one round.
+bool tree_schedule(Tables *t) {
+  int e = 0;
+  for (int s = 0; s < NS; ++s) {
+    t->edge[s][0] = t->edge[s][1] = t->edge[s][2] = -1;
+    if (t->cout0[s] != -1) t->edge[s][0] = (int16_t)e++;
+    if (t->cout1[s] != -1) {
+      t->edge[s][1] = (int16_t)e++;
+      t->edge[s][2] = (int16_t)e++;
+    }
+  }
+  t->n_edges = e;
+  if (e != TREE_NE) return false;
+  // edge lookup between two currents (shared section)
+  auto sec_of_pair = [&](int a, int b, int *eid) -> bool {
+    for (int s = 0; s < NS; ++s) {
+      int in = t->cin[s], o0 = t->cout0[s], o1 = t->cout1[s];
+      int m[3] = {in, o0, o1};
+      int pa = -1, pb = -1;
+      for (int k = 0; k < 3; ++k) {
+        if (m[k] == a) pa = k;
+        if (m[k] == b) pb = k;
+      }
+      if (pa < 0 || pb < 0 || m[pa] == -1 || m[pb] == -1) continue;
+      int lo = pa < pb ? pa : pb, hi = pa < pb ? pb : pa;
+      int k = (lo == 0 && hi == 1) ? 0 : (lo == 0 && hi == 2) ? 1 : 2;
+      *eid = t->edge[s][k];
+      return *eid >= 0;
+    }
+    return false;
+  };
+  std::vector<int> chain[TREE_CHAINS];
+  for (int c = 0; c <= 31; ++c) chain[0].push_back(c);
+  chain[1].push_back(94);
+  chain[1].push_back(93);
+  for (int c = 64; c >= 34; --c) chain[1].push_back(c);
+  chain[2].push_back(96);
+  chain[2].push_back(95);
+  for (int c = 83; c >= 65; --c) chain[2].push_back(c);
+  for (int c = 89; c <= 92; ++c) chain[3].push_back(c);
+  for (int c = 88; c >= 84; --c) chain[3].push_back(c);
+  size_t longest = 0;
+  for (auto &ch : chain) longest = std::max(longest, ch.size());
+  const int rounds = (int)longest + 2;  // + eliminate 32, + root 33
+  if (rounds > TREE_MAX_ROUNDS) return false;
+  t->n_rounds = rounds;
+  for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
+    for (int k = 0; k < TREE_CHAINS; ++k) t->step[r][k] = SolveStep{-1, -1, -1, -1, -1, -1};
+  // symbolic elimination: adjacency of remaining currents
+  static bool adj[NC][NC];
+  std::memset(adj, 0, sizeof adj);
+  for (int s = 0; s < NS; ++s) {
+    int m[3] = {t->cin[s], t->cout0[s], t->cout1[s]};
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b)
+        if (a != b && m[a] != -1 && m[b] != -1) adj[m[a]][m[b]] = true;
+  }
+  bool gone[NC] = {false};
+  auto plan = [&](int r, int k, int c) -> bool {
+    int nb[NC], n = 0;
+    for (int j = 0; j < NC; ++j)
+      if (!gone[j] && adj[c][j]) nb[n++] = j;
+    if (n > 2) return false;                                   // would create fill
+    if (n == 2 && !adj[nb[0]][nb[1]]) return false;            // neighbours must be a clique
+    SolveStep st{(int16_t)c, -1, -1, -1, -1, -1};
+    int id;
+    if (n >= 1) { st.n0 = (int16_t)nb[0]; if (!sec_of_pair(c, nb[0], &id)) return false; st.e0 = (int16_t)id; }
+    if (n == 2) {
+      st.n1 = (int16_t)nb[1];
+      if (!sec_of_pair(c, nb[1], &id)) return false;
+      st.e1 = (int16_t)id;
+      if (!sec_of_pair(nb[0], nb[1], &id)) return false;
+      st.e01 = (int16_t)id;
+    }
+    t->step[r][k] = st;
+    return true;
+  };
+  for (int r = 0; r < (int)longest; ++r) {
+    // all lanes of one round must touch disjoint unknowns
+    bool touched[NC] = {false};
+    for (int k = 0; k < TREE_CHAINS; ++k) {
+      if (r >= (int)chain[k].size()) continue;
+      if (!plan(r, k, chain[k][r])) return false;
+      const SolveStep &st = t->step[r][k];
+      for (int q : {(int)st.c, (int)st.n0, (int)st.n1}) {
+        if (q < 0) continue;
+        if (touched[q]) return false;
+        touched[q] = true;
+      }
+    }
+    for (int k = 0; k < TREE_CHAINS; ++k)
+      if (r < (int)chain[k].size()) gone[chain[k][r]] = true;
+  }
+  if (!plan(rounds - 2, 0, 32)) return false;
+  gone[32] = true;
+  if (!plan(rounds - 1, 0, 33)) return false;
+  gone[33] = true;
+  for (int c = 0; c < NC; ++c)
+    if (!gone[c]) return false;
+  return t->step[rounds - 1][0].n0 == -1;
+}
+
 }  // namespace
 
 // IirFilter::createChebyshev, IirFilter.cpp:286-432 (0.5 % ripple).
@@ -218,6 +329,7 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   static_network(t);
   t->fossa_R0 = 8.0 * MU * t->len[S_FOSSA0] * PI / (AMIN * AMIN);
   topology(t);
+  t->n_rounds = tree_schedule(t) ? t->n_rounds : -1;
 }
 
 }  // namespace afs

@@ -46,7 +46,7 @@ def _nbytes(x) -> int:
 class Context:
     """An afs_ctx: device + sampling rate + solver + options (TdsModel::Options)."""
 
-    def __init__(self, sampling_rate_hz: float = 22050.0, solver: str = "cholesky", device: int = 0,
+    def __init__(self, sampling_rate_hz: float = 22050.0, solver: str = "tree", device: int = 0,
                  async_calls: bool = False, **options):
         lib = _native.load()
         cfg = _native.AfsConfig()

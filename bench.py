@@ -80,7 +80,7 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=8192, help="utterances per GPU")
     ap.add_argument("--seconds", type=float, default=1.0)
     ap.add_argument("--fs", type=float, default=44100.0)
-    ap.add_argument("--solver", default=os.environ.get("AFS_SOLVER", "cholesky"))
+    ap.add_argument("--solver", default=os.environ.get("AFS_SOLVER", "tree"))
     ap.add_argument("--cpu-utterances", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -116,7 +116,8 @@ def main() -> None:
     if world > 1 and rank == 0:
         gather_list = [torch.empty_like(out_dev) for _ in range(world)]
 
-    launches_per_step = -(-(F - 1) // max(1, 8192 // hop))
+    max_launch_samples = 65536 if args.solver == "tree" else 8192
+    launches_per_step = -(-(F - 1) // max(1, max_launch_samples // hop))
 
     def step():
         ctx.synthesize(frames_dev, hop, seeds=seeds_dev, out=out_dev)

@@ -1,0 +1,78 @@
+// tree_emu.cpp -- TEST-ONLY host execution of the cooperative tree kernel's phase code.
+//
+// Runs csrc/tree_core.h's sample_step with the W lanes of each phase executed one after
+// another (phases only read LDS data written by earlier phases, so this is the same
+// computation the GPU does in lock step).  Used by tests/test_tree_emu.py to check the
+// decomposition (slot ownership, LDS exchange, the tree LDL^T schedule) against the
+// oracle on the CPU.  Never part of the product; libafs.so does not contain it.
+#include <cstring>
+#include <vector>
+
+#include "tree_core.h"
+
+using namespace afs;
+using namespace afs::tree;
+
+namespace {
+
+template <int W>
+struct CpuExec {
+  Lane<W> *R;
+  template <class F> void par(F f) { for (int gl = 0; gl < W; ++gl) f(gl, R[gl]); }
+  template <class F> void one(F f) { f(R[0]); }
+  template <class F> void lanes(int n, F f) { for (int k = 0; k < n; ++k) f(k, R[k]); }
+  void sync() {}
+};
+
+template <int W>
+long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, const afs_options &opt,
+         double *out, double *dump_p, double *dump_u, int ndump) {
+  static Tables T;
+  build_tables(&T, fs, opt);
+  if (T.n_rounds < 0) return -1;
+  std::vector<Lane<W>> R(W);
+  std::vector<double> X(X_TOTAL);
+  for (int gl = 0; gl < W; ++gl) reset_lane<W>(gl, R[gl]);
+  reset_lds(X.data(), seed);
+  CpuExec<W> ex{R.data()};
+  long t = 0;
+  for (int k = 1; k < F; ++k) {
+    for (int gl = 0; gl < W; ++gl) frame_load<W>(gl, R[gl], X.data(), frames + k - 1, frames + k);
+    for (int i = 0; i < hop; ++i) {
+      double ratio = (double)i / (double)hop;
+      sample_step<W>(ex, X.data(), T, ratio);
+      out[t] = R[0].sample;
+      if (t < ndump) {
+        for (int gl = 0; gl < W; ++gl)
+          for (int j = 0; j < Shape<W>::NSL; ++j) {
+            int s = slot_section<W>(j, gl);
+            if (s >= 0) dump_p[t * NS + s] = R[gl].p[j];
+          }
+        for (int c = 0; c < NC; ++c) dump_u[t * NC + c] = X[X_U + c];
+      }
+      ++t;
+    }
+  }
+  return t;
+}
+
+}  // namespace
+
+extern "C" long emu_tree_utterance(const afs_frame *frames, int F, int hop, unsigned seed, double fs, int W,
+                                   double *out, double *dump_p, double *dump_u, int ndump) {
+  afs_options opt{1, 1, 1, 1, 0, 1};
+  switch (W) {
+    case 16: return run<16>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
+    case 8: return run<8>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
+    case 32: return run<32>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
+    case 64: return run<64>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
+  }
+  return -2;
+}
+
+extern "C" int emu_tree_rounds(double fs) {
+  static Tables T;
+  afs_options opt{1, 1, 1, 1, 0, 1};
+  build_tables(&T, fs, opt);
+  return T.n_rounds;
+}

@@ -1,10 +1,11 @@
 """GPU parity: the HIP kernels (through the C ABI) against the oracle and the golden
 vectors of the reference build.
 
-Tolerances (fp64 path): the kernels keep the reference's operand order, so the only
-differences come from device libm (exp for noise cutoffs below the 2 kHz clamp, pow for
-the aspiration gain); those ulp-level differences are amplified by the chaotic
-glottis/tube dynamics (trap 3).  Bounds used below:
+Two kernels are checked: "cholesky" keeps the reference's operation order (differences only
+from device libm: exp for noise cutoffs below the 2 kHz clamp, pow for the aspiration
+gain); "tree" solves the same system with a fill-free LDL^T (rounding-level differences,
+~1e-12 on the CPU emulator).  Such differences are amplified by the chaotic glottis/tube
+dynamics (trap 3).  Bounds used below:
   * golden / oracle, first 2048 samples:   max |err| <= 1e-9
   * oracle, 1 s @ 44.1 kHz (north star):   per-utterance RMS <= 1e-4, reported max-abs
 Integer/bookkeeping behaviour (batch independence, session == trajectory, seeds,
@@ -22,7 +23,7 @@ pytestmark = pytest.mark.gpu
 
 GOLD_TOL = 1e-9
 RMS_TOL = 1e-4
-SOLVERS = ("cholesky",)
+SOLVERS = ("cholesky", "tree")
 
 
 @pytest.fixture(scope="module")
@@ -172,6 +173,20 @@ def test_nonfinite_is_reported(contexts, oracle, solver):
     y, rep = ctx.synthesize(np.ascontiguousarray(fr[None]), 200, report=True)
     assert np.isfinite(y).all() == np.isfinite(x).all()
     assert rep["nonfinite_utterances"] == (0 if np.isfinite(x).all() else 1)
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_long_utterance_chunked_launches(contexts, oracle, solver):
+    """An utterance longer than one kernel launch (state carried across launches)."""
+    ctx = contexts(22050.0, solver)
+    f = oracle.af_to_frame(default_shapes()["i:"])
+    f["glottis"] = DEFAULT_GLOTTIS
+    fr = np.repeat(f[None], 160)
+    fr["glottis"][:, 0] = np.linspace(100, 140, 160)
+    y = ctx.synthesize(np.ascontiguousarray(fr[None]), 441, seeds=np.array([5], np.uint32))
+    x = oracle.utterance(fr, 441, 5, 22050.0)
+    assert y.shape[1] == 159 * 441 > 65536
+    assert float(np.sqrt(np.mean((y[0] - x) ** 2))) < RMS_TOL
 
 
 def test_af_to_frames_vs_restatement(contexts, golden_dir):
