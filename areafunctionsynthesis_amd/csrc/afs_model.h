@@ -65,10 +65,21 @@ AFS_HD constexpr bool is_static_section(int s) {
 // eliminates step[r][k].c, whose remaining neighbours are n0 (and n1) through edges e0
 // (e1); e01 is the edge n0-n1 that receives the fill-free update.  c = -1: idle.
 constexpr int TREE_CHAINS = 4;
-constexpr int TREE_MAX_ROUNDS = 40;
+constexpr int TREE_MAX_ROUNDS = 36;
 constexpr int TREE_NE = 104;
 struct SolveStep {
-  int16_t c, n0, n1, e0, e1, e01;
+  int8_t c, n0, n1, e0, e1, e01;
+};
+
+// The tables the cooperative kernel reads inside its time loop, packed so that one copy
+// per wave fits in LDS next to the four utterance blocks (tds_tree.hip).
+constexpr int NSTATIC = 47;  // static sections 0..22, 69..92 -> index s < 23 ? s : s - 46
+enum : int { ST_E, ST_ALPHA, ST_WC1, ST_WC2, ST_LW, ST_L, ST_R, ST_N };
+enum : int { TP_SRC, TP_OUT0, TP_OUT1, TP_E0, TP_E1, TP_E2, TP_N };
+struct Consts {
+  SolveStep step[TREE_MAX_ROUNDS][TREE_CHAINS];
+  int8_t topo[NS][TP_N];
+  double stat[NSTATIC][ST_N];
 };
 
 struct Tables {
@@ -100,6 +111,7 @@ struct Tables {
   int16_t edge[NS][3];
   int32_t n_edges, n_rounds;
   SolveStep step[TREE_MAX_ROUNDS][TREE_CHAINS];
+  Consts consts;
 
   afs_options opt;
 };

@@ -212,15 +212,15 @@ bool tree_schedule(Tables *t) {
       if (!gone[j] && adj[c][j]) nb[n++] = j;
     if (n > 2) return false;                                   // would create fill
     if (n == 2 && !adj[nb[0]][nb[1]]) return false;            // neighbours must be a clique
-    SolveStep st{(int16_t)c, -1, -1, -1, -1, -1};
+    SolveStep st{(int8_t)c, -1, -1, -1, -1, -1};
     int id;
-    if (n >= 1) { st.n0 = (int16_t)nb[0]; if (!sec_of_pair(c, nb[0], &id)) return false; st.e0 = (int16_t)id; }
+    if (n >= 1) { st.n0 = (int8_t)nb[0]; if (!sec_of_pair(c, nb[0], &id)) return false; st.e0 = (int8_t)id; }
     if (n == 2) {
-      st.n1 = (int16_t)nb[1];
+      st.n1 = (int8_t)nb[1];
       if (!sec_of_pair(c, nb[1], &id)) return false;
-      st.e1 = (int16_t)id;
+      st.e1 = (int8_t)id;
       if (!sec_of_pair(nb[0], nb[1], &id)) return false;
-      st.e01 = (int16_t)id;
+      st.e01 = (int8_t)id;
     }
     t->step[r][k] = st;
     return true;
@@ -330,6 +330,27 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   t->fossa_R0 = 8.0 * MU * t->len[S_FOSSA0] * PI / (AMIN * AMIN);
   topology(t);
   t->n_rounds = tree_schedule(t) ? t->n_rounds : -1;
+  // packed copy for the cooperative kernel
+  Consts &c = t->consts;
+  std::memcpy(c.step, t->step, sizeof c.step);
+  for (int s = 0; s < NS; ++s) {
+    c.topo[s][TP_SRC] = (int8_t)t->src[s];
+    c.topo[s][TP_OUT0] = (int8_t)t->cout0[s];
+    c.topo[s][TP_OUT1] = (int8_t)t->cout1[s];
+    c.topo[s][TP_E0] = (int8_t)t->edge[s][0];
+    c.topo[s][TP_E1] = (int8_t)t->edge[s][1];
+    c.topo[s][TP_E2] = (int8_t)t->edge[s][2];
+  }
+  for (int k = 0; k < NSTATIC; ++k) {
+    int s = k < 23 ? k : k + 46;
+    c.stat[k][ST_E] = t->E[s];
+    c.stat[k][ST_ALPHA] = t->alpha[s];
+    c.stat[k][ST_WC1] = t->wc1[s];
+    c.stat[k][ST_WC2] = t->wc2[s];
+    c.stat[k][ST_LW] = t->Lw[s];
+    c.stat[k][ST_L] = t->L[s];
+    c.stat[k][ST_R] = t->R[s];
+  }
 }
 
 }  // namespace afs

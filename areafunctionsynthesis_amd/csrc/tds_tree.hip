@@ -35,20 +35,33 @@ struct GpuExec {
   }
 };
 
+// One block of LDS per wave: the packed hot tables (shared by the four utterances) and the
+// four utterance blocks.
+struct WaveLds {
+  Consts C;
+  double X[UPW][X_TOTAL];
+};
+
 __global__ void __launch_bounds__(64) tree_synth_kernel(TreeArgs a) {
-  __shared__ double smem[UPW * X_TOTAL];
+  __shared__ WaveLds lds;
   const int lane = threadIdx.x;
   const int g = lane / TW, gl = lane % TW;
   const int u = blockIdx.x * UPW + g;
   const bool valid = u < a.B;
   const int ue = valid ? u : 0;
-  double *X = smem + g * X_TOTAL;
+  double *X = lds.X[g];
   const Tables &T = *a.tab;
+  {  // stage the hot tables (8-byte words; Consts is a multiple of 8 bytes)
+    const uint64_t *src = (const uint64_t *)&T.consts;
+    uint64_t *dst = (uint64_t *)&lds.C;
+    for (int k = lane; k < (int)(sizeof(Consts) / 8); k += 64) dst[k] = src[k];
+  }
   Lane<TW> R = ((const Lane<TW> *)a.lane_state)[(int64_t)ue * TW + gl];
   const double *ls = a.lds_state + (int64_t)ue * X_TOTAL;
   for (int k = gl; k < X_TOTAL; k += TW) X[k] = ls[k];
+  __syncthreads();
+  const Consts &C = lds.C;
   GpuExec ex{gl, &R};
-  ex.sync();
   const afs_frame *fu = a.frames + (int64_t)ue * a.frame_stride;
   double *o = a.out + (int64_t)ue * a.out_stride;
   int64_t t = 0;
@@ -57,18 +70,12 @@ __global__ void __launch_bounds__(64) tree_synth_kernel(TreeArgs a) {
     ex.sync();
     for (int i = 0; i < a.hop; ++i) {
       const double ratio = (double)i / (double)a.hop;
-      sample_step<TW>(ex, X, T, ratio);
-      if (gl == 0) X[X_RING + (int)(t % RING)] = R.sample;
+      sample_step<TW>(ex, X, T, C, ratio);
+      if (valid && gl == 0) o[t] = R.sample;
       ++t;
-      if (t % RING == 0) {
-        ex.sync();
-        if (valid) o[t - RING + gl] = X[X_RING + gl];
-      }
     }
   }
-  const int rem = (int)(t % RING);
   ex.sync();
-  if (valid && gl < rem) o[t - rem + gl] = X[X_RING + gl];
   if (valid) {
     ((Lane<TW> *)a.lane_state)[(int64_t)u * TW + gl] = R;
     double *ws = a.lds_state + (int64_t)u * X_TOTAL;

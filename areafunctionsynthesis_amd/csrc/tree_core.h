@@ -70,13 +70,11 @@ enum : int {
   X_OUTF = X_TONE + 8,         // output Chebyshev: x1..x8, y1..y8
   X_PREVFLOW = X_OUTF + 16,
   X_NONFIN = X_PREVFLOW + 1,
-  X_RING = X_NONFIN + 1,       // output staging (RING samples)
-  X_ART = X_RING + 16,         // 40 articulator bytes
+  X_ART = X_NONFIN + 1,        // 40 articulator bytes
   X_RNG = X_ART + 5,           // 31 int32 words + ring index (16 doubles)
   X_GP = X_RNG + 16,           // interpolated glottis controls (6) and teeth position (lane 0)
   X_TOTAL = X_GP + 8
 };
-constexpr int RING = 16;
 
 template <int W>
 struct Shape {
@@ -342,14 +340,17 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Tables &T
 // Phase N: per-section network elements L, C, R, wall terms, D, E (TdsModel.cpp:732-1008).
 // Static sections take L, C, R, alpha, E from the tables; only beta and D depend on state.
 // ---------------------------------------------------------------------------
+AFS_HD inline int static_index(int s) { return s < 23 ? s : s - 46; }
+
 template <int W>
-AFS_HD inline double static_beta(const Lane<W> &R, int j, const Tables &T, int s) {
-  return T.opt.soft_walls ? T.alpha[s] * (R.w[j] * T.wc1[s] + R.wr[j] * T.wc2[s] + R.wr2[j] * T.Lw[s] * (TH1 / TH))
+AFS_HD inline double static_beta(const Lane<W> &R, int j, const Tables &T, const Consts &C, int s) {
+  const double *k = C.stat[static_index(s)];
+  return T.opt.soft_walls ? k[ST_ALPHA] * (R.w[j] * k[ST_WC1] + R.wr[j] * k[ST_WC2] + R.wr2[j] * k[ST_LW] * (TH1 / TH))
                           : 0.0;
 }
 
 template <int W>
-AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T) {
+AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T, const Consts &C) {
   using S = Shape<W>;
   const afs_options &opt = T.opt;
   const double dt = T.dt;
@@ -358,8 +359,8 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T)
     const int jj = S::ND + j;
     const int s = static_section(W, j, gl);
     if (s < 0) continue;
-    const double E = T.E[s];
-    const double beta = static_beta<W>(R, jj, T, s);
+    const double E = C.stat[static_index(s)][ST_E];
+    const double beta = static_beta<W>(R, jj, T, C, s);
     X[X_E + s] = E;
     X[X_D + s] = R.p[jj] + T.dtTH1 * R.pr[jj] - E * (beta - 0.0);
   }
@@ -369,7 +370,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T)
     if (s < 0) continue;
     const bool glot = (s == S_GLOT_LO || s == S_GLOT_UP);
     const double area = X[X_AREA + s - DYN0];
-    const double len = glot ? X[X_GLEN + s - DYN0] : (s <= S_LAST_MOUTH ? X[X_LEN + s - S_PHARYNX0] : T.len[s]);
+    const double len = glot ? X[X_GLEN + s - DYN0] : (s <= S_LAST_MOUTH ? X[X_LEN + s - S_PHARYNX0] : T.len[S_NOSE0]);
     const double vol = area * len;
     double alpha = 0.0, beta = 0.0;
     double circ = 2.0 * sqrt(area * PI);
@@ -382,7 +383,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T)
     if (opt.soft_walls && !glot) {
       double surf = circ * len;
       if (surf < AMIN) surf = AMIN;
-      double Rw = T.Bw[s] / surf, Lw = T.Mw[s] / surf, Cw = surf / T.Kw[s];
+      double Rw = T.Bw[S_PHARYNX0] / surf, Lw = T.Mw[S_PHARYNX0] / surf, Cw = surf / T.Kw[S_PHARYNX0];
       alpha = 1.0 / (Lw / (dt * dt * TH * TH) + Rw / (dt * TH) + 1.0 / Cw);
       beta = alpha * (R.w[j] * (Lw / (dt * dt * TH * TH) + Rw / (dt * TH)) +
                       R.wr[j] * (Lw * (TH1 / TH + 1.0) / (dt * TH) + Rw * (TH1 / TH)) +
@@ -462,8 +463,46 @@ AFS_HD inline void tongue_obstacle(const double *X, double teeth, Cons &c, doubl
   }
 }
 
+// Dipole targets of one constriction (TdsModel.cpp:1456-1602).
+AFS_HD inline void dipole_targets(double *X, const Tables &T, const Consts &C, double teeth, const Cons &c) {
+  int ob = -1;
+  for (int i = S_PHARYNX0; i <= S_LAST_MOUTH && ob == -1; ++i) {
+    double pos = X[X_POS + i - S_PHARYNX0];
+    if (pos <= c.obst && pos + X[X_LEN + i - S_PHARYNX0] >= c.obst) ob = i;
+  }
+  if (ob == -1) return;
+  int up = ob - S_PHARYNX0;
+  int dn = (ob < S_LAST_MOUTH) ? up + 1 : DIP_LIPS;
+  double fdn = (c.obst - X[X_POS + up]) / X[X_LEN + up];
+  double fup = 1.0 - fdn;
+  double A = X[X_AREA + c.narrow - DYN0];
+  if (A < 0.1) A = 0.1;
+  double flow = 0.0;
+  int o0 = C.topo[c.narrow][TP_OUT0], o1 = C.topo[c.narrow][TP_OUT1];
+  if (o0 != -1) flow += X[X_UN + o0];
+  if (o1 != -1) flow += X[X_UN + o1];
+  if (flow < 0.0) flow = 0.0;
+  double v = flow / A;
+  double fc = 6000.0, gain = 0.0;
+  if (c.art == LOWER_LIP) {
+    gain = 2.0e-7;
+  } else if (c.art == VOCAL_FOLDS) {
+    gain = 0.5e-7 * pow(10.0, X[X_GP + 5] / 20.0);
+  } else {
+    double d = sqrt(4.0 * A / PI);
+    fc = 0.15 * v / d;
+    gain = (fabs(c.obst - teeth) < 0.0001) ? 10.0e-7 : 5.0e-7;
+  }
+  double full = gain * fabs(v) * v * v * sqrt(A);
+  if (c.lat > 0.1) full = 0.0;
+  if (fc < 50.0) fc = 50.0;
+  if (fc > 2000.0) fc = 2000.0;
+  X[X_TGT + up] = fup * full; X[X_CUTN + up] = fc;
+  X[X_TGT + dn] = fdn * full; X[X_CUTN + dn] = fc;
+}
+
 template <int W>
-AFS_HD inline void phase_constrictions(Lane<W> &R, double *X, const Tables &T) {
+AFS_HD inline void phase_constrictions(Lane<W> &R, double *X, const Tables &T, const Consts &C) {
   const unsigned char *art = (const unsigned char *)(X + X_ART);
   const double teeth = X[X_GP + 6];
   {  // section positions (Tube::calcPositions, Tube.cpp:611-622)
@@ -473,9 +512,10 @@ AFS_HD inline void phase_constrictions(Lane<W> &R, double *X, const Tables &T) {
       x += X[X_LEN + m];
     }
   }
-  Cons cs[4];
-  int nc = 1;
-  cs[0] = Cons{S_GLOT_LO, S_GLOT_UP, S_GLOT_UP, VOCAL_FOLDS, 1.5, 0.0};
+  // Up to four constrictions in the reference's order: glottis, tongue, second tongue, lip.
+  const Cons cg = Cons{S_GLOT_LO, S_GLOT_UP, S_GLOT_UP, VOCAL_FOLDS, 1.5, 0.0};
+  Cons ct1 = cg, ct2 = cg, cl = cg;
+  bool has_t1 = false, has_t2 = false, has_l = false;
   double min_teeth = 1000000.0, mt = 1000000.0;
   int mts = -1;
   for (int i = S_PHARYNX0; i <= S_LAST_MOUTH; ++i) {
@@ -483,13 +523,13 @@ AFS_HD inline void phase_constrictions(Lane<W> &R, double *X, const Tables &T) {
     if (art[i - S_PHARYNX0] == TONGUE && a < mt) { mt = a; mts = i; }
   }
   if (mt < 1.0) {
-    Cons &c = cs[nc++];
-    c = Cons{mts, mts, mts, TONGUE, 0.0, 0.0};
-    grow(X, art, c, mt, TONGUE);
-    tongue_obstacle(X, teeth, c, min_teeth);
+    has_t1 = true;
+    ct1 = Cons{mts, mts, mts, TONGUE, 0.0, 0.0};
+    grow(X, art, ct1, mt, TONGUE);
+    tongue_obstacle(X, teeth, ct1, min_teeth);
   }
-  if (cs[nc - 1].art == TONGUE) {
-    const Cons pc = cs[nc - 1];
+  if (has_t1) {
+    const Cons pc = ct1;
     mt = 1000000.0;
     mts = -1;
     for (int i = S_PHARYNX0; i <= S_LAST_MOUTH; ++i) {
@@ -497,11 +537,12 @@ AFS_HD inline void phase_constrictions(Lane<W> &R, double *X, const Tables &T) {
       if (art[i - S_PHARYNX0] == TONGUE && a < mt && (i < pc.first || i > pc.last)) { mt = a; mts = i; }
     }
     if (mt < 1.0) {
-      Cons &c = cs[nc++];
-      c = Cons{mts, mts, mts, TONGUE, 0.0, 0.0};
-      grow(X, art, c, mt, TONGUE);
-      if (c.first > pc.last + 1 || c.last < pc.first - 1) tongue_obstacle(X, teeth, c, min_teeth);
-      else nc--;
+      ct2 = Cons{mts, mts, mts, TONGUE, 0.0, 0.0};
+      grow(X, art, ct2, mt, TONGUE);
+      if (ct2.first > pc.last + 1 || ct2.last < pc.first - 1) {
+        has_t2 = true;
+        tongue_obstacle(X, teeth, ct2, min_teeth);
+      }
     }
   }
   double ml = 1000000.0;
@@ -511,48 +552,15 @@ AFS_HD inline void phase_constrictions(Lane<W> &R, double *X, const Tables &T) {
     if (art[i - S_PHARYNX0] == LOWER_LIP && a < ml) { ml = a; mls = i; }
   }
   if (ml < 1.0 && ml < min_teeth) {
-    Cons &c = cs[nc++];
-    c = Cons{mls, mls, mls, LOWER_LIP, 0.0, 0.0};
-    grow(X, art, c, ml, LOWER_LIP);
-    c.obst = X[X_POS + c.last + 1 - S_PHARYNX0];
+    has_l = true;
+    cl = Cons{mls, mls, mls, LOWER_LIP, 0.0, 0.0};
+    grow(X, art, cl, ml, LOWER_LIP);
+    cl.obst = X[X_POS + cl.last + 1 - S_PHARYNX0];
   }
-  for (int k = 0; k < nc; ++k) {
-    const Cons c = cs[k];
-    int ob = -1;
-    for (int i = S_PHARYNX0; i <= S_LAST_MOUTH && ob == -1; ++i) {
-      double pos = X[X_POS + i - S_PHARYNX0];
-      if (pos <= c.obst && pos + X[X_LEN + i - S_PHARYNX0] >= c.obst) ob = i;
-    }
-    if (ob == -1) continue;
-    int up = ob - S_PHARYNX0;
-    int dn = (ob < S_LAST_MOUTH) ? up + 1 : DIP_LIPS;
-    double fdn = (c.obst - X[X_POS + up]) / X[X_LEN + up];
-    double fup = 1.0 - fdn;
-    double A = X[X_AREA + c.narrow - DYN0];
-    if (A < 0.1) A = 0.1;
-    double flow = 0.0;
-    int o0 = T.cout0[c.narrow], o1 = T.cout1[c.narrow];
-    if (o0 != -1) flow += X[X_UN + o0];
-    if (o1 != -1) flow += X[X_UN + o1];
-    if (flow < 0.0) flow = 0.0;
-    double v = flow / A;
-    double fc = 6000.0, gain = 0.0;
-    if (c.art == LOWER_LIP) {
-      gain = 2.0e-7;
-    } else if (c.art == VOCAL_FOLDS) {
-      gain = 0.5e-7 * pow(10.0, X[X_GP + 5] / 20.0);
-    } else {
-      double d = sqrt(4.0 * A / PI);
-      fc = 0.15 * v / d;
-      gain = (fabs(c.obst - teeth) < 0.0001) ? 10.0e-7 : 5.0e-7;
-    }
-    double full = gain * fabs(v) * v * v * sqrt(A);
-    if (c.lat > 0.1) full = 0.0;
-    if (fc < 50.0) fc = 50.0;
-    if (fc > 2000.0) fc = 2000.0;
-    X[X_TGT + up] = fup * full; X[X_CUTN + up] = fc;
-    X[X_TGT + dn] = fdn * full; X[X_CUTN + dn] = fc;
-  }
+  dipole_targets(X, T, C, teeth, cg);
+  if (has_t1) dipole_targets(X, T, C, teeth, ct1);
+  if (has_t2) dipole_targets(X, T, C, teeth, ct2);
+  if (has_l) dipole_targets(X, T, C, teeth, cl);
 }
 
 // Phase A (all lanes): amplitude smoothing of owned dipoles (TdsModel.cpp:1637-1666).
@@ -614,17 +622,15 @@ AFS_HD inline void phase_noise_filter(int gl, Lane<W> &R, double *X, const Table
 // Owner of section s writes row s (its in-current), the edges of section s and, for
 // s = 64 / 83, the two radiation rows.
 // ---------------------------------------------------------------------------
-template <int W>
-AFS_HD inline double sec_L(const double *X, const Tables &T, int s) {
-  return (s >= DYN0 && s < DYN0 + NDYNS) ? X[X_L + s - DYN0] : T.L[s];
+AFS_HD inline double sec_L(const double *X, const Consts &C, int s) {
+  return (s >= DYN0 && s < DYN0 + NDYNS) ? X[X_L + s - DYN0] : C.stat[static_index(s)][ST_L];
 }
-template <int W>
-AFS_HD inline double sec_R1(const double *X, const Tables &T, int s) {
-  return (s >= DYN0 && s < DYN0 + NDYNS) ? X[X_R1 + s - DYN0] : T.R[s];
+AFS_HD inline double sec_R1(const double *X, const Consts &C, int s) {
+  return (s >= DYN0 && s < DYN0 + NDYNS) ? X[X_R1 + s - DYN0] : C.stat[static_index(s)][ST_R];
 }
 
 template <int W>
-AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Tables &T) {
+AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Tables &T, const Consts &C) {
   using S = Shape<W>;
   const double dt = T.dt;
   const afs_options &opt = T.opt;
@@ -634,17 +640,18 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Tables &T) {
     if (s < 0) continue;
     const bool dyn = j < S::ND;
     const int i = s;  // current i flows into section s
-    const double LB = dyn ? X[X_L + s - DYN0] : T.L[s];
-    const double RB = dyn ? X[X_R0 + s - DYN0] : ((s == S_FOSSA0 && !opt.piriform_fossa) ? T.fossa_R0 : T.R[s]);
-    const double R1B = dyn ? X[X_R1 + s - DYN0] : T.R[s];
-    const double AB = dyn ? X[X_AREA + s - DYN0] : T.area[s];
+    const double *ks = C.stat[static_index(s)];
+    const double LB = dyn ? X[X_L + s - DYN0] : ks[ST_L];
+    const double RB = dyn ? X[X_R0 + s - DYN0] : ((s == S_FOSSA0 && !opt.piriform_fossa) ? T.fossa_R0 : ks[ST_R]);
+    const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
+    const double AB = dyn ? X[X_AREA + s - DYN0] : T.area[S_LAST_NOSE];  // static: only used by s = 83
     const double EB = X[X_E + s], DB = X[X_D + s];
-    const int a = T.src[i];
+    const int a = C.topo[i][TP_SRC];
     double LA = 0.0, RA = 0.0, EA = 0.0, DA = 0.0;
-    if (a != -1) { LA = sec_L<W>(X, T, a); RA = sec_R1<W>(X, T, a); EA = X[X_E + a]; DA = X[X_D + a]; }
+    if (a != -1) { LA = sec_L(X, C, a); RA = sec_R1(X, C, a); EA = X[X_E + a]; DA = X[X_D + a]; }
     double LAB = LA + LB, RAB = RA + RB;
     int br = -1;
-    if (a != -1) br = (T.cout0[a] == i) ? T.cout1[a] : T.cout0[a];
+    if (a != -1) br = (C.topo[a][TP_OUT0] == i) ? C.topo[a][TP_OUT1] : C.topo[a][TP_OUT0];
     double Sx = 0.0;
     if (s >= S_PHARYNX0 && s <= S_LAST_MOUTH) Sx -= X[X_SMP + s - S_PHARYNX0];
     if (s == 0) Sx -= X[X_GP + 1];  // lung pressure source at section 0
@@ -669,14 +676,14 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Tables &T) {
     X[X_DIAG + i] = -m;
     X[X_RHS + i] = -rhs;
     // edges of section s: (in, out0) = -E, (in, out1) = -E, (out0, out1) = E + L/(dt th) + R1
-    const int e0 = T.edge[s][0], e1 = T.edge[s][1], e2 = T.edge[s][2];
+    const int e0 = C.topo[s][TP_E0], e1 = C.topo[s][TP_E1], e2 = C.topo[s][TP_E2];
     if (e0 >= 0) X[X_OFF + e0] = -EB;
     if (e1 >= 0) {
       X[X_OFF + e1] = -EB;
       X[X_OFF + e2] = -(-EB - (LB / (dt * TH) + R1B));
     }
     if (s == S_LAST_MOUTH || s == S_LAST_NOSE) {  // radiation rows (TdsModel.cpp:1841-1911)
-      const int rc = T.cout0[s], lc = T.cout1[s];
+      const int rc = C.topo[s][TP_OUT0], lc = C.topo[s][TP_OUT1];
       double uR = X[X_U + rc], uL = X[X_U + lc], uRr = X[X_UR + rc], uLr = X[X_UR + lc];
       R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
       R.rad_un[0] = X[X_UN + rc]; R.rad_un[1] = X[X_UN + lc];
@@ -703,8 +710,8 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Tables &T) {
 // ---------------------------------------------------------------------------
 // Solver rounds (chain lanes 0..3).
 // ---------------------------------------------------------------------------
-AFS_HD inline void solve_forward(int k, int r, double *X, const Tables &T) {
-  const SolveStep st = T.step[r][k];
+AFS_HD inline void solve_forward(int k, int r, double *X, const Consts &C) {
+  const SolveStep st = C.step[r][k];
   if (st.c < 0) return;
   double d = X[X_DIAG + st.c];
   double inv = (d < 0.0) ? NAN : 1.0 / d;  // the reference takes sqrt of a negative pivot
@@ -725,8 +732,8 @@ AFS_HD inline void solve_forward(int k, int r, double *X, const Tables &T) {
   X[X_DIAG + st.c] = inv;
 }
 
-AFS_HD inline void solve_backward(int k, int r, double *X, const Tables &T) {
-  const SolveStep st = T.step[r][k];
+AFS_HD inline void solve_backward(int k, int r, double *X, const Consts &C) {
+  const SolveStep st = C.step[r][k];
   if (st.c < 0) return;
   double y = X[X_RHS + st.c];
   if (st.n0 >= 0) y -= X[X_OFF + st.e0] * X[X_U + st.n0];
@@ -738,7 +745,7 @@ AFS_HD inline void solve_backward(int k, int r, double *X, const Tables &T) {
 // Phase U: updateVariables (TdsModel.cpp:2046-2098).
 // ---------------------------------------------------------------------------
 template <int W>
-AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Tables &T) {
+AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Tables &T, const Consts &C) {
   using S = Shape<W>;
   const double dt = T.dt, c = T.noise_lp_c;
 #pragma unroll
@@ -747,7 +754,7 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Tables &T) 
     if (s < 0) continue;
     double alpha, beta;
     if (j < S::ND) { alpha = R.al[j]; beta = R.be[j]; }
-    else { alpha = T.alpha[s]; beta = static_beta<W>(R, j, T, s); }  // same values as phase_network
+    else { alpha = C.stat[static_index(s)][ST_ALPHA]; beta = static_beta<W>(R, j, T, C, s); }  // same values as phase_network
     const double unew = X[X_U + s];
     const double uold = R.u[j];
     R.u[j] = unew;
@@ -758,8 +765,9 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Tables &T) 
     double cin = 0.0;
     cin += unew;
     double cout = 0.0;
-    if (T.cout0[s] != -1) cout += X[X_U + T.cout0[s]];
-    if (T.cout1[s] != -1) cout += X[X_U + T.cout1[s]];
+    const int o0 = C.topo[s][TP_OUT0], o1 = C.topo[s][TP_OUT1];
+    if (o0 != -1) cout += X[X_U + o0];
+    if (o1 != -1) cout += X[X_U + o1];
     double net = cin - cout;
     double old = R.p[j];
     double p = X[X_D + s] + X[X_E + s] * net;
@@ -775,7 +783,7 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Tables &T) 
     if (s >= S_LAST_TRACHEA && s <= S_PHARYNX0) X[X_P4 + s - S_LAST_TRACHEA] = p;
     if (s == S_LAST_MOUTH || s == S_LAST_NOSE) {  // the two radiation currents of this section
       for (int q = 0; q < 2; ++q) {
-        const int rc = q == 0 ? T.cout0[s] : T.cout1[s];
+        const int rc = q == 0 ? o0 : o1;
         double un = X[X_U + rc];
         double ur = (un - R.rad_u[q]) / (dt * TH) - (TH1 / TH) * R.rad_ur[q];
         X[X_UR + rc] = ur;
@@ -807,13 +815,13 @@ AFS_HD inline double phase_output(double *X, const Tables &T) {
 // One audio sample.  Xc: execution policy (par / one / lanes / sync).
 // ---------------------------------------------------------------------------
 template <int W, class Xc>
-AFS_HD inline void sample_step(Xc &x, double *X, const Tables &T, double ratio) {
+AFS_HD inline void sample_step(Xc &x, double *X, const Tables &T, const Consts &C, double ratio) {
   x.par([&](int gl, Lane<W> &R) { phase_geometry<W>(gl, R, X, T, ratio); });
   x.sync();
-  x.par([&](int gl, Lane<W> &R) { phase_network<W>(gl, R, X, T); });
+  x.par([&](int gl, Lane<W> &R) { phase_network<W>(gl, R, X, T, C); });
   x.sync();
   if (T.opt.generate_noise_sources) {
-    x.one([&](Lane<W> &R) { phase_constrictions<W>(R, X, T); });
+    x.one([&](Lane<W> &R) { phase_constrictions<W>(R, X, T, C); });
     x.sync();
     x.par([&](int gl, Lane<W> &R) { phase_noise_amp<W>(gl, R, X, T); });
     x.sync();
@@ -827,17 +835,17 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Tables &T, double ratio) 
     });
   }
   x.sync();
-  x.par([&](int gl, Lane<W> &R) { phase_rows<W>(gl, R, X, T); });
+  x.par([&](int gl, Lane<W> &R) { phase_rows<W>(gl, R, X, T, C); });
   x.sync();
   for (int r = 0; r < T.n_rounds; ++r) {
-    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { (void)R; solve_forward(k, r, X, T); });
+    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { (void)R; solve_forward(k, r, X, C); });
     x.sync();
   }
   for (int r = T.n_rounds - 1; r >= 0; --r) {
-    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { (void)R; solve_backward(k, r, X, T); });
+    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { (void)R; solve_backward(k, r, X, C); });
     x.sync();
   }
-  x.par([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, T); });
+  x.par([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, T, C); });
   x.sync();
   x.one([&](Lane<W> &R) { R.sample = phase_output(X, T); });
 }

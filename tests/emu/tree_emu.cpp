@@ -40,7 +40,7 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
     for (int gl = 0; gl < W; ++gl) frame_load<W>(gl, R[gl], X.data(), frames + k - 1, frames + k);
     for (int i = 0; i < hop; ++i) {
       double ratio = (double)i / (double)hop;
-      sample_step<W>(ex, X.data(), T, ratio);
+      sample_step<W>(ex, X.data(), T, T.consts, ratio);
       out[t] = R[0].sample;
       if (t < ndump) {
         for (int gl = 0; gl < W; ++gl)
