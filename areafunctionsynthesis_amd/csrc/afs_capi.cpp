@@ -109,7 +109,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     int ke = std::min(k1, k + per);
     double *o = out + (int64_t)(k - k0) * hop;
     if (tree(c)) {
-      afs::TreeArgs a{c->dev_tab, frames, fstride, k, ke, hop, o, ostride, lanes, (double *)ws, B};
+      afs::TreeArgs a{c->dev_tab, frames, fstride, k, ke, hop, o, ostride, lanes, (double *)ws, B, c->host_tab.uni};
       HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
     } else {
       afs::LaneArgs a{c->dev_tab, frames, fstride, k, ke, hop, o, ostride, (double *)ws, rng, bp, B};

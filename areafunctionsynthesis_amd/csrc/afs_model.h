@@ -67,8 +67,8 @@ AFS_HD constexpr bool is_static_section(int s) {
 constexpr int TREE_CHAINS = 4;
 constexpr int TREE_MAX_ROUNDS = 36;
 constexpr int TREE_NE = 104;
-struct SolveStep {
-  int8_t c, n0, n1, e0, e1, e01;
+struct alignas(8) SolveStep {  // 8 bytes: one LDS load, kept packed until it is used
+  int8_t c, n0, n1, e0, e1, e01, pad0, pad1;
 };
 
 // The tables the cooperative kernel reads inside its time loop, packed so that one copy
@@ -76,7 +76,21 @@ struct SolveStep {
 constexpr int NSTATIC = 47;  // static sections 0..22, 69..92 -> index s < 23 ? s : s - 46
 enum : int { ST_E, ST_ALPHA, ST_WC1, ST_WC2, ST_LW, ST_L, ST_R, ST_N };
 enum : int { TP_SRC, TP_OUT0, TP_OUT1, TP_E0, TP_E1, TP_E2, TP_N };
+// Scalars of the time loop (copies of Tables fields; see build_tables).
+struct Hot {
+  double fs, dt, dtTH1, noise_amp_F, noise_lp_c, noise_x_2000, sqrt12, nose4_area, fossa_R0;
+  double rrad_num, lrad_num, tone_a[5], tone_b[5], out_a[9], out_b[9];
+  double len_nose0, Bw_ph0, Mw_ph0, Kw_ph0, area_last_trachea, area_last_nose;
+};
+// Values that steer branches in the time loop: kernel arguments on the device, so the
+// compiler keeps them in scalar registers and branches on them uniformly.
+struct Uni {
+  int32_t n_rounds;
+  uint64_t fwd_carry, bwd_carry;
+  afs_options opt;
+};
 struct Consts {
+  Hot h;
   SolveStep step[TREE_MAX_ROUNDS][TREE_CHAINS];
   int8_t topo[NS][TP_N];
   double stat[NSTATIC][ST_N];
@@ -110,8 +124,12 @@ struct Tables {
   // tree solver
   int16_t edge[NS][3];
   int32_t n_edges, n_rounds;
+  // bit r: in forward (backward) round r every active chain lane finds the pivot (the
+  // solution of n0) in its registers -- uniform per round, see tree_schedule.
+  uint64_t fwd_carry, bwd_carry;
   SolveStep step[TREE_MAX_ROUNDS][TREE_CHAINS];
   Consts consts;
+  Uni uni;
 
   afs_options opt;
 };

@@ -195,7 +195,7 @@ bool tree_schedule(Tables *t) {
   if (rounds > TREE_MAX_ROUNDS) return false;
   t->n_rounds = rounds;
   for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
-    for (int k = 0; k < TREE_CHAINS; ++k) t->step[r][k] = SolveStep{-1, -1, -1, -1, -1, -1};
+    for (int k = 0; k < TREE_CHAINS; ++k) t->step[r][k] = SolveStep{-1, -1, -1, -1, -1, -1, 0, 0};
   // symbolic elimination: adjacency of remaining currents
   static bool adj[NC][NC];
   std::memset(adj, 0, sizeof adj);
@@ -212,7 +212,7 @@ bool tree_schedule(Tables *t) {
       if (!gone[j] && adj[c][j]) nb[n++] = j;
     if (n > 2) return false;                                   // would create fill
     if (n == 2 && !adj[nb[0]][nb[1]]) return false;            // neighbours must be a clique
-    SolveStep st{(int8_t)c, -1, -1, -1, -1, -1};
+    SolveStep st{(int8_t)c, -1, -1, -1, -1, -1, 0, 0};
     int id;
     if (n >= 1) { st.n0 = (int8_t)nb[0]; if (!sec_of_pair(c, nb[0], &id)) return false; st.e0 = (int8_t)id; }
     if (n == 2) {
@@ -247,7 +247,41 @@ bool tree_schedule(Tables *t) {
   gone[33] = true;
   for (int c = 0; c < NC; ++c)
     if (!gone[c]) return false;
-  return t->step[rounds - 1][0].n0 == -1;
+  if (t->step[rounds - 1][0].n0 != -1) return false;
+  // Register carries (tree_core.h solve_forward / solve_backward).  Forward: after a step
+  // the lane holds the new pivot of its n0, valid until another lane touches that unknown.
+  // Backward: the lane holds the solution of the unknown it solved last.
+  t->fwd_carry = 0;
+  int carry[TREE_CHAINS];
+  for (int k = 0; k < TREE_CHAINS; ++k) carry[k] = -1;
+  for (int r = 0; r < rounds; ++r) {
+    bool all = true;
+    for (int k = 0; k < TREE_CHAINS; ++k) {
+      const SolveStep &st = t->step[r][k];
+      if (st.c >= 0 && st.c != carry[k]) all = false;
+    }
+    if (all) t->fwd_carry |= 1ull << r;
+    for (int k = 0; k < TREE_CHAINS; ++k) {
+      const SolveStep &st = t->step[r][k];
+      if (st.c >= 0) carry[k] = st.n0;
+      for (int q : {(int)st.c, (int)st.n0, (int)st.n1})  // touched by lane k: others' carries die
+        for (int j = 0; j < TREE_CHAINS; ++j)
+          if (j != k && q >= 0 && carry[j] == q) carry[j] = -1;
+    }
+  }
+  t->bwd_carry = 0;
+  for (int k = 0; k < TREE_CHAINS; ++k) carry[k] = -1;
+  for (int r = rounds - 1; r >= 0; --r) {
+    bool all = true;
+    for (int k = 0; k < TREE_CHAINS; ++k) {
+      const SolveStep &st = t->step[r][k];
+      if (st.c >= 0 && (st.n1 >= 0 || (st.n0 >= 0 && st.n0 != carry[k]))) all = false;
+    }
+    if (all) t->bwd_carry |= 1ull << r;
+    for (int k = 0; k < TREE_CHAINS; ++k)
+      if (t->step[r][k].c >= 0) carry[k] = t->step[r][k].c;
+  }
+  return true;
 }
 
 }  // namespace
@@ -332,6 +366,18 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   t->n_rounds = tree_schedule(t) ? t->n_rounds : -1;
   // packed copy for the cooperative kernel
   Consts &c = t->consts;
+  Hot &h = c.h;
+  h.fs = t->fs; h.dt = t->dt; h.dtTH1 = t->dtTH1; h.noise_amp_F = t->noise_amp_F; h.noise_lp_c = t->noise_lp_c;
+  h.noise_x_2000 = t->noise_x_2000; h.sqrt12 = t->sqrt12; h.nose4_area = t->nose4_area; h.fossa_R0 = t->fossa_R0;
+  h.rrad_num = t->rrad_num; h.lrad_num = t->lrad_num;
+  for (int i = 0; i < 5; ++i) { h.tone_a[i] = t->tone_a[i]; h.tone_b[i] = t->tone_b[i]; }
+  for (int i = 0; i < 9; ++i) { h.out_a[i] = t->out_a[i]; h.out_b[i] = t->out_b[i]; }
+  h.len_nose0 = t->len[S_NOSE0]; h.Bw_ph0 = t->Bw[S_PHARYNX0]; h.Mw_ph0 = t->Mw[S_PHARYNX0];
+  h.Kw_ph0 = t->Kw[S_PHARYNX0]; h.area_last_trachea = t->area[S_LAST_TRACHEA]; h.area_last_nose = t->area[S_LAST_NOSE];
+  t->uni.n_rounds = t->n_rounds;
+  t->uni.fwd_carry = t->fwd_carry;
+  t->uni.bwd_carry = t->bwd_carry;
+  t->uni.opt = t->opt;
   std::memcpy(c.step, t->step, sizeof c.step);
   for (int s = 0; s < NS; ++s) {
     c.topo[s][TP_SRC] = (int8_t)t->src[s];

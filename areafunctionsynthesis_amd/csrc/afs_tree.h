@@ -17,6 +17,7 @@ struct TreeArgs {
   void *lane_state;         // per-lane register state, B * TREE_W entries
   double *lds_state;        // per-utterance LDS block, B * tree_lds_doubles()
   int B;
+  Uni uni;                  // copy of tab->uni: scalar kernel arguments
 };
 
 constexpr int TREE_W = 16;  // lanes per utterance

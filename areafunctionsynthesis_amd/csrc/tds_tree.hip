@@ -1,17 +1,6 @@
-// tds_tree.hip -- the cooperative synthesis kernel (afs_solver AFS_SOLVER_TREE).
-//
-// Mapping on gfx950: a wave64 holds four utterances, TREE_W = 16 lanes each.  A lane keeps
-// the state of its 6 sections (3 dynamic + 3 static) and their in-currents in registers
-// for the whole launch; the four utterances' 8.4 KB LDS blocks carry neighbour exchange,
-// the per-sample solver arrays and the small persistent state.  Waves never wait for one
-// another (no __syncthreads): phases of one utterance are ordered by wave-level fences,
-// which is all LDS needs inside a wave.  The time loop runs inside the kernel; a launch
-// covers a range of frame transitions and saves the lane/LDS state at the end, so long
-// utterances and incremental sessions continue exactly where they stopped.
-#include <hip/hip_runtime.h>
-
-#include "afs_tree.h"
-#include "tree_core.h"
+// tds_tree.hip -- the cooperative synthesis kernel (afs_solver AFS_SOLVER_TREE); the body and
+// the wave mapping are described in tree_kernel.h.
+#include "tree_kernel.h"
 
 namespace afs {
 
@@ -19,68 +8,9 @@ using namespace tree;
 
 namespace {
 
-constexpr int TW = TREE_W;
-constexpr int UPW = 64 / TW;  // utterances per wave
-
-struct GpuExec {
-  int gl;
-  Lane<TW> *R;
-  template <class F> __device__ __forceinline__ void par(F f) { f(gl, *R); }
-  template <class F> __device__ __forceinline__ void one(F f) { if (gl == 0) f(*R); }
-  template <class F> __device__ __forceinline__ void lanes(int n, F f) { if (gl < n) f(gl, *R); }
-  __device__ __forceinline__ void sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-};
-
-// One block of LDS per wave: the packed hot tables (shared by the four utterances) and the
-// four utterance blocks.
-struct WaveLds {
-  Consts C;
-  double X[UPW][X_TOTAL];
-};
-
 __global__ void __launch_bounds__(64) tree_synth_kernel(TreeArgs a) {
   __shared__ WaveLds lds;
-  const int lane = threadIdx.x;
-  const int g = lane / TW, gl = lane % TW;
-  const int u = blockIdx.x * UPW + g;
-  const bool valid = u < a.B;
-  const int ue = valid ? u : 0;
-  double *X = lds.X[g];
-  const Tables &T = *a.tab;
-  {  // stage the hot tables (8-byte words; Consts is a multiple of 8 bytes)
-    const uint64_t *src = (const uint64_t *)&T.consts;
-    uint64_t *dst = (uint64_t *)&lds.C;
-    for (int k = lane; k < (int)(sizeof(Consts) / 8); k += 64) dst[k] = src[k];
-  }
-  Lane<TW> R = ((const Lane<TW> *)a.lane_state)[(int64_t)ue * TW + gl];
-  const double *ls = a.lds_state + (int64_t)ue * X_TOTAL;
-  for (int k = gl; k < X_TOTAL; k += TW) X[k] = ls[k];
-  __syncthreads();
-  const Consts &C = lds.C;
-  GpuExec ex{gl, &R};
-  const afs_frame *fu = a.frames + (int64_t)ue * a.frame_stride;
-  double *o = a.out + (int64_t)ue * a.out_stride;
-  int64_t t = 0;
-  for (int k = a.k_begin; k < a.k_end; ++k) {
-    frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
-    ex.sync();
-    for (int i = 0; i < a.hop; ++i) {
-      const double ratio = (double)i / (double)a.hop;
-      sample_step<TW>(ex, X, T, C, ratio);
-      if (valid && gl == 0) o[t] = R.sample;
-      ++t;
-    }
-  }
-  ex.sync();
-  if (valid) {
-    ((Lane<TW> *)a.lane_state)[(int64_t)u * TW + gl] = R;
-    double *ws = a.lds_state + (int64_t)u * X_TOTAL;
-    for (int k = gl; k < X_TOTAL; k += TW) ws[k] = X[k];
-  }
+  tree_synth_body<false>(a, lds, nullptr);
 }
 
 __global__ void tree_reset_kernel(Lane<TW> *lanes, double *lds, int B, const uint32_t *seeds) {

@@ -71,9 +71,16 @@ enum : int {
   X_PREVFLOW = X_OUTF + 16,
   X_NONFIN = X_PREVFLOW + 1,
   X_ART = X_NONFIN + 1,        // 40 articulator bytes
-  X_RNG = X_ART + 5,           // 31 int32 words + ring index (16 doubles)
-  X_GP = X_RNG + 16,           // interpolated glottis controls (6) and teeth position (lane 0)
+  X_RNG = X_ART + 5,           // rand() ring: 64 u32 values, head position, pending count (33 doubles)
+  X_GP = X_RNG + 33,           // interpolated glottis controls (6) and teeth position (lane 0)
   X_TOTAL = X_GP + 8
+};
+
+// Phase ids for Exec::mark (cycle accounting in tools/phase_prof; a no-op otherwise).
+enum : int {
+  PH_GEOMETRY, PH_NETWORK, PH_CONSTRICTIONS, PH_NOISE,
+  PH_C_POS, PH_C_T1, PH_C_T2, PH_C_LIP, PH_N_AMP, PH_N_RNG,
+  PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_COUNT
 };
 
 template <int W>
@@ -93,6 +100,32 @@ AFS_HD inline int static_section(int W, int j, int gl) {
   return k < NSTATS ? (k < 23 ? k : k + 46) : -1;
 }
 
+// Solver chain lane registers: the next step (prefetched) and the unknown this lane updated
+// last together with its new pivot / right-hand side (forward) or solution (backward).
+struct SolveCarry {
+  uint64_t next;  // packed SolveStep
+  double d, y;    // forward: pivot and rhs of the last n0; backward: y = last solution
+};
+
+AFS_HD inline uint64_t load_step(const Consts &C, int r, int k) {
+  return *reinterpret_cast<const uint64_t *>(&C.step[r][k]);
+}
+AFS_HD inline int step_field(uint64_t w, int i) { return (int)(int8_t)(uint8_t)(w >> (8 * i)); }
+
+// 1/d for the pivots: v_rcp_f64 and two Newton steps on the device (within an ulp of the
+// division, a fraction of its latency); plain division in the CPU emulator.
+AFS_HD inline double pivot_recip(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+#else
+  return 1.0 / d;
+#endif
+}
+
 // Lane registers.
 // Only the persistent state and the frame cache live here; per-sample intermediates
 // go through the LDS block or are recomputed from unchanged state.
@@ -107,7 +140,20 @@ struct Lane {
   double rad_u[2], rad_ur[2], rad_un[2];                             // owner of 64 / 83
   double sample;                                                     // lane 0
   int art[S::ND];
+  uint32_t racc[S::NDP];                                             // rand() sums of owned dipoles
+  SolveCarry sc;                                                     // chain lanes, during the solve
 };
+
+// Cross-lane collectives every execution policy provides (results are uniform over the W
+// lanes of one utterance):
+//   x.ballot(f)     -> uint64_t with bit gl = f(gl, R)
+//   x.min_index(f)  -> the smallest MinIdx::v of f(gl, R), ties to the smallest index
+//   x.max_value(f)  -> the largest f(gl, R) under strict ">" (a NaN never wins)
+struct MinIdx { double v; int i; };
+AFS_HD inline MinIdx min_idx_combine(MinIdx a, MinIdx b) {
+  return (b.v < a.v || (b.v == a.v && b.i < a.i)) ? b : a;
+}
+AFS_HD inline double max_combine(double a, double b) { return (b > a) ? b : a; }
 
 template <int W>
 AFS_HD inline int slot_section(int j, int gl) {
@@ -204,6 +250,37 @@ AFS_HD inline void rng_seed(int32_t *r, uint32_t seed) {
   for (int k = 0; k < 310; ++k) (void)rng_next(r);
 }
 
+// The rand() stream as a sequence r_i = r_{i-3} + r_{i-31} (mod 2^32), output r_i >> 1 --
+// glibc's TYPE_3 generator read in generation order.  The LDS ring holds the last 64
+// values (index = sequence number mod 64); RNG_HEAD is the ring index of the next value to
+// generate and RNG_PEND how many generated values have not been drawn yet (< 31).
+constexpr int RNG_RING = 64, RNG_HEAD = 64, RNG_PEND = 65, RNG_BLOCK = 31;
+
+// Ring after srand(seed): the 31 most recent values in generation order at 0..30.
+AFS_HD inline void rng_ring_seed(uint32_t *ring, uint32_t seed) {
+  int32_t st[32];
+  rng_seed(st, seed);
+  const int f = st[31];  // glibc's fptr: the oldest value of the window
+  for (int j = 0; j < RNG_BLOCK; ++j) ring[j] = (uint32_t)st[(f + j) % 31];
+  for (int j = RNG_BLOCK; j < RNG_RING; ++j) ring[j] = 0;
+  ((int32_t *)ring)[RNG_HEAD] = RNG_BLOCK;
+  ((int32_t *)ring)[RNG_PEND] = 0;
+}
+
+// Value k (0..30) of the next block, straight from the 31-value history: unrolling the lag-3
+// term gives r_{h+k} = r_{h+k-3(m+1)} + sum_{j<=m} r_{h+k-31-3j}, m = k / 3.
+AFS_HD inline uint32_t rng_block_value(const uint32_t *ring, int head, int k) {
+  const int m = k / 3;
+  uint32_t v = ring[(head + k - 3 * (m + 1)) & (RNG_RING - 1)];
+  // fixed trip count, every load issued: the compiler batches them before one wait
+#pragma unroll
+  for (int j = 0; j <= RNG_BLOCK / 3; ++j) {
+    const uint32_t t = ring[(head + k - RNG_BLOCK - 3 * j) & (RNG_RING - 1)];
+    v += (j <= m) ? t : 0u;
+  }
+  return v;
+}
+
 // ---------------------------------------------------------------------------
 // Reset (Synthesizer::reset + TdsModel::resetMotion + TriangularGlottis::resetMotion)
 // ---------------------------------------------------------------------------
@@ -225,11 +302,13 @@ AFS_HD inline void reset_lane(int gl, Lane<W> &R) {
   for (int k = 0; k < S::NDP; ++k) { R.damp[k] = 0.0; R.dout[k] = 0.0; R.dcut[k] = 3000.0; }
   for (int k = 0; k < 2; ++k) R.rad_u[k] = R.rad_ur[k] = R.rad_un[k] = 0.0;
   R.sample = 0.0;
+#pragma unroll
+  for (int k = 0; k < S::NDP; ++k) R.racc[k] = 0u;
 }
 
 AFS_HD inline void reset_lds(double *X, uint32_t seed) {
   for (int k = 0; k < X_TOTAL; ++k) X[k] = 0.0;
-  rng_seed((int32_t *)(X + X_RNG), seed);
+  rng_ring_seed((uint32_t *)(X + X_RNG), seed);
 }
 
 // ---------------------------------------------------------------------------
@@ -270,7 +349,7 @@ AFS_HD inline void frame_load(int gl, Lane<W> &R, double *X, const afs_frame *fl
 // Phase G: tube interpolation (all lanes) and the glottis (lane 0).
 // ---------------------------------------------------------------------------
 template <int W>
-AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Tables &T, double ratio) {
+AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C, double ratio) {
   using S = Shape<W>;
   const double r1 = 1.0 - ratio;
 #pragma unroll
@@ -283,7 +362,7 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Tables &T
     } else if (s >= S_NOSE0) {  // nose sections 65..68: velum taper (Tube.cpp:402-416)
       double open = r1 * X[X_FRAME + 2] + ratio * X[X_FRAME + 3];
       int i = s - S_NOSE0;
-      X[X_AREA + s - DYN0] = clampA(open + ((double)(i * i) * (T.nose4_area - open)) / (double)16);
+      X[X_AREA + s - DYN0] = clampA(open + ((double)(i * i) * (C.h.nose4_area - open)) / (double)16);
     }
   }
   if (gl == 0) {
@@ -307,7 +386,7 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Tables &T
     X[X_GLEN + 0] = th0;
     X[X_GLEN + 1] = th1;
     // incTime (TriangularGlottis.cpp:154-330) with the previous sample's pressures
-    const double Tt = 1.0 / T.fs;
+    const double Tt = 1.0 / C.h.fs;
     const double p0 = X[X_P4 + 0], p1 = X[X_P4 + 1], p2 = X[X_P4 + 2], p3 = X[X_P4 + 3];
     double m0 = G_MASS0 / q, m1 = G_MASS1 / q;
     double al0 = clen[0] / cord, al1 = clen[1] / cord;
@@ -343,26 +422,26 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Tables &T
 AFS_HD inline int static_index(int s) { return s < 23 ? s : s - 46; }
 
 template <int W>
-AFS_HD inline double static_beta(const Lane<W> &R, int j, const Tables &T, const Consts &C, int s) {
+AFS_HD inline double static_beta(const Lane<W> &R, int j, const Uni &U, const Consts &C, int s) {
   const double *k = C.stat[static_index(s)];
-  return T.opt.soft_walls ? k[ST_ALPHA] * (R.w[j] * k[ST_WC1] + R.wr[j] * k[ST_WC2] + R.wr2[j] * k[ST_LW] * (TH1 / TH))
+  return U.opt.soft_walls ? k[ST_ALPHA] * (R.w[j] * k[ST_WC1] + R.wr[j] * k[ST_WC2] + R.wr2[j] * k[ST_LW] * (TH1 / TH))
                           : 0.0;
 }
 
 template <int W>
-AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T, const Consts &C) {
+AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  const afs_options &opt = T.opt;
-  const double dt = T.dt;
+  const afs_options &opt = U.opt;
+  const double dt = C.h.dt;
 #pragma unroll
   for (int j = 0; j < S::NST; ++j) {
     const int jj = S::ND + j;
     const int s = static_section(W, j, gl);
     if (s < 0) continue;
     const double E = C.stat[static_index(s)][ST_E];
-    const double beta = static_beta<W>(R, jj, T, C, s);
+    const double beta = static_beta<W>(R, jj, U, C, s);
     X[X_E + s] = E;
-    X[X_D + s] = R.p[jj] + T.dtTH1 * R.pr[jj] - E * (beta - 0.0);
+    X[X_D + s] = R.p[jj] + C.h.dtTH1 * R.pr[jj] - E * (beta - 0.0);
   }
 #pragma unroll
   for (int j = 0; j < S::ND; ++j) {
@@ -370,7 +449,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T,
     if (s < 0) continue;
     const bool glot = (s == S_GLOT_LO || s == S_GLOT_UP);
     const double area = X[X_AREA + s - DYN0];
-    const double len = glot ? X[X_GLEN + s - DYN0] : (s <= S_LAST_MOUTH ? X[X_LEN + s - S_PHARYNX0] : T.len[S_NOSE0]);
+    const double len = glot ? X[X_GLEN + s - DYN0] : (s <= S_LAST_MOUTH ? X[X_LEN + s - S_PHARYNX0] : C.h.len_nose0);
     const double vol = area * len;
     double alpha = 0.0, beta = 0.0;
     double circ = 2.0 * sqrt(area * PI);
@@ -378,18 +457,18 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T,
     double rmin = glot ? 0.8 : 1.6;
     if (a < rmin) { a = rmin; b = area / (PI * a); }
     const double L = (RHO * 0.5 * len) / area;
-    const double C = vol / (RHO * CSND * CSND);
+    const double Cc = vol / (RHO * CSND * CSND);
     const double Rr = ((2.0 * MU * len) * (a * a + b * b)) / (PI * a * a * a * b * b * b);
     if (opt.soft_walls && !glot) {
       double surf = circ * len;
       if (surf < AMIN) surf = AMIN;
-      double Rw = T.Bw[S_PHARYNX0] / surf, Lw = T.Mw[S_PHARYNX0] / surf, Cw = surf / T.Kw[S_PHARYNX0];
+      double Rw = C.h.Bw_ph0 / surf, Lw = C.h.Mw_ph0 / surf, Cw = surf / C.h.Kw_ph0;
       alpha = 1.0 / (Lw / (dt * dt * TH * TH) + Rw / (dt * TH) + 1.0 / Cw);
       beta = alpha * (R.w[j] * (Lw / (dt * dt * TH * TH) + Rw / (dt * TH)) +
                       R.wr[j] * (Lw * (TH1 / TH + 1.0) / (dt * TH) + Rw * (TH1 / TH)) +
                       R.wr2[j] * Lw * (TH1 / TH));
     }
-    const double E = dt * TH / (C + alpha);
+    const double E = dt * TH / (Cc + alpha);
     double R0 = Rr, R1 = Rr;
     // Bernoulli losses between pharynx/mouth sections (TdsModel.cpp:850-877)
     if (opt.turbulence_losses && s >= S_PHARYNX0 && s <= S_LAST_MOUTH) {
@@ -407,7 +486,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T,
       }
     }
     if (s == S_GLOT_LO) {  // glottal entrance and transition (TdsModel.cpp:912-950)
-      double sa = T.area[S_LAST_TRACHEA], ta = area;
+      double sa = C.h.area_last_trachea, ta = area;
       double u = 0.0;
       u += R.u[j];
       if (u > 0) R0 = R0 + 1.0 * 0.5 * RHO * fabs(u) * (1.0 / (ta * ta) - 1.0 / (sa * sa));
@@ -423,7 +502,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T,
     R.al[j] = alpha;
     R.be[j] = beta;
     X[X_E + s] = E;
-    X[X_D + s] = R.p[j] + T.dtTH1 * R.pr[j] - E * (beta - 0.0);
+    X[X_D + s] = R.p[j] + C.h.dtTH1 * R.pr[j] - E * (beta - 0.0);
     X[X_L + s - DYN0] = L;
     X[X_R0 + s - DYN0] = R0;
     X[X_R1 + s - DYN0] = R1;
@@ -437,42 +516,58 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Tables &T,
 }
 
 // ---------------------------------------------------------------------------
-// Phase C (lane 0): constriction detection and dipole targets (TdsModel.cpp:1188-1604).
+// Phase C: constriction detection and dipole targets (TdsModel.cpp:1188-1604).
+// The reference scans the 40 pharynx/mouth sections one after another; here every lane
+// tests the sections it owns and the scans become ballots (bit masks over the 40 sections)
+// and min/max reductions over the W lanes.  All decisions are uniform per utterance.
 // ---------------------------------------------------------------------------
 struct Cons { int first, last, narrow, art; double obst, lat; };
 
-AFS_HD inline void grow(const double *X, const unsigned char *art, Cons &c, double amin_, int a) {
-  double amax = amin_ + 0.2;
-  while (X[X_AREA + c.first - DYN0] < amax && art[c.first - S_PHARYNX0] == a && c.first > S_PHARYNX0) c.first--;
-  while (X[X_AREA + c.last - DYN0] < amax && art[c.last - S_PHARYNX0] == a && c.last < S_LAST_MOUTH) c.last++;
-  c.first++;
-  c.last--;
+// Bit m (0..39) = pred(R, j, m) evaluated by the owner of mouth section 25 + m
+// (dynamic slot j of lane gl holds section 23 + jW + gl).
+template <int W, class Xc, class P>
+AFS_HD inline uint64_t mouth_mask(Xc &x, P pred) {
+  using S = Shape<W>;
+  uint64_t M = 0;
+#pragma unroll
+  for (int j = 0; j < S::ND; ++j)
+    M |= x.ballot([&](int gl, Lane<W> &R) {
+      const int m = j * W + gl - 2;
+      return m >= 0 && m < NPM && pred(R, j, m);
+    }) << (j * W);
+  return (M >> 2) & ((1ull << NPM) - 1);
 }
 
-AFS_HD inline void tongue_obstacle(const double *X, double teeth, Cons &c, double &min_teeth) {
-  for (int i = c.first; i <= c.last; ++i) {
-    double lt = X[X_LAT + i - S_PHARYNX0];
-    if (lt > c.lat) c.lat = lt;
-  }
-  double jet = X[X_POS + c.last - S_PHARYNX0] + X[X_LEN + c.last - S_PHARYNX0];
-  if (teeth - jet < 2.0) {
-    c.obst = teeth;
-    min_teeth = X[X_AREA + c.narrow - DYN0];
-  } else {
-    c.obst = X[X_POS + c.last + 1 - S_PHARYNX0] + 0.5 * X[X_LEN + c.last + 1 - S_PHARYNX0];
-  }
+// First minimum of the area over the mouth sections with pred (the reference's ascending
+// scan with a strict "<"); {1e6, -1} when there is none.
+template <int W, class Xc, class P>
+AFS_HD inline MinIdx mouth_min(Xc &x, const double *X, P pred) {
+  using S = Shape<W>;
+  return x.min_index([&](int gl, Lane<W> &R) {
+    MinIdx b{1000000.0, -1};
+#pragma unroll
+    for (int j = 0; j < S::ND; ++j) {
+      const int m = j * W + gl - 2;
+      if (m >= 0 && m < NPM && pred(R, j, m)) {
+        const double a = X[X_AREA + m + 2];
+        if (a < b.v) b = MinIdx{a, m};
+      }
+    }
+    return b;
+  });
 }
 
 // Dipole targets of one constriction (TdsModel.cpp:1456-1602).
-AFS_HD inline void dipole_targets(double *X, const Tables &T, const Consts &C, double teeth, const Cons &c) {
-  int ob = -1;
-  for (int i = S_PHARYNX0; i <= S_LAST_MOUTH && ob == -1; ++i) {
-    double pos = X[X_POS + i - S_PHARYNX0];
-    if (pos <= c.obst && pos + X[X_LEN + i - S_PHARYNX0] >= c.obst) ob = i;
-  }
-  if (ob == -1) return;
-  int up = ob - S_PHARYNX0;
-  int dn = (ob < S_LAST_MOUTH) ? up + 1 : DIP_LIPS;
+template <int W, class Xc>
+AFS_HD inline void dipole_targets(Xc &x, double *X, const Uni &U, const Consts &C, double teeth, const Cons &c) {
+  const uint64_t M = mouth_mask<W>(x, [&](Lane<W> &R, int j, int m) {
+    (void)R; (void)j;
+    const double pos = X[X_POS + m];
+    return pos <= c.obst && pos + X[X_LEN + m] >= c.obst;
+  });
+  if (M == 0) return;
+  const int up = __builtin_ctzll(M);  // the first section that contains the obstacle
+  const int dn = (up < NPM - 1) ? up + 1 : DIP_LIPS;
   double fdn = (c.obst - X[X_POS + up]) / X[X_LEN + up];
   double fup = 1.0 - fdn;
   double A = X[X_AREA + c.narrow - DYN0];
@@ -497,124 +592,213 @@ AFS_HD inline void dipole_targets(double *X, const Tables &T, const Consts &C, d
   if (c.lat > 0.1) full = 0.0;
   if (fc < 50.0) fc = 50.0;
   if (fc > 2000.0) fc = 2000.0;
-  X[X_TGT + up] = fup * full; X[X_CUTN + up] = fc;
-  X[X_TGT + dn] = fdn * full; X[X_CUTN + dn] = fc;
+  x.one([&](Lane<W> &R) {
+    (void)R;
+    X[X_TGT + up] = fup * full; X[X_CUTN + up] = fc;
+    X[X_TGT + dn] = fdn * full; X[X_CUTN + dn] = fc;
+  });
 }
 
-template <int W>
-AFS_HD inline void phase_constrictions(Lane<W> &R, double *X, const Tables &T, const Consts &C) {
-  const unsigned char *art = (const unsigned char *)(X + X_ART);
-  const double teeth = X[X_GP + 6];
-  {  // section positions (Tube::calcPositions, Tube.cpp:611-622)
-    double x = 0.0;
+template <int W, class Xc>
+AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Consts &C) {
+  using S = Shape<W>;
+  // Section positions (Tube::calcPositions, Tube.cpp:611-622): every lane runs the same
+  // sequential sum and stores the positions of the sections it owns.
+  x.par([&](int gl, Lane<W> &R) {
+    (void)R;
+    double p = 0.0;
+#pragma unroll
     for (int m = 0; m < NPM; ++m) {
-      X[X_POS + m] = x;
-      x += X[X_LEN + m];
+      if ((m + 2) % W == gl) X[X_POS + m] = p;
+      p += X[X_LEN + m];
     }
-  }
+  });
+  x.sync();
+  x.mark(PH_C_POS);
+  const double teeth = X[X_GP + 6];
+  // Extend a constriction over the neighbours with area < amin + 0.2 and the same
+  // articulator (TdsModel.cpp:1247-1262), including the reference's stop rules at the ends.
+  auto grow = [&](Cons &c, double amin, int a) {
+    const double amax = amin + 0.2;
+    const uint64_t M = mouth_mask<W>(x, [&](Lane<W> &R, int j, int m) { return X[X_AREA + m + 2] < amax && R.art[j] == a; });
+    const int lo = c.narrow - S_PHARYNX0;
+    const uint64_t dn = (~M | 1ull) & ((2ull << lo) - 1);
+    const uint64_t up = (~M | (1ull << (NPM - 1))) & ~((1ull << lo) - 1);
+    c.first = S_PHARYNX0 + (63 - __builtin_clzll(dn)) + 1;
+    c.last = S_PHARYNX0 + __builtin_ctzll(up) - 1;
+  };
+  auto tongue_obstacle = [&](Cons &c, double &min_teeth) {
+    const int f = c.first - S_PHARYNX0, l = c.last - S_PHARYNX0;
+    c.lat = x.max_value([&](int gl, Lane<W> &R) {
+      (void)R;
+      double b = 0.0;
+#pragma unroll
+      for (int j = 0; j < S::ND; ++j) {
+        const int m = j * W + gl - 2;
+        if (m >= 0 && m < NPM && m >= f && m <= l) b = max_combine(b, X[X_LAT + m]);
+      }
+      return b;
+    });
+    const double jet = X[X_POS + l] + X[X_LEN + l];
+    if (teeth - jet < 2.0) {
+      c.obst = teeth;
+      min_teeth = X[X_AREA + c.narrow - DYN0];
+    } else {
+      c.obst = X[X_POS + l + 1] + 0.5 * X[X_LEN + l + 1];
+    }
+  };
   // Up to four constrictions in the reference's order: glottis, tongue, second tongue, lip.
   const Cons cg = Cons{S_GLOT_LO, S_GLOT_UP, S_GLOT_UP, VOCAL_FOLDS, 1.5, 0.0};
   Cons ct1 = cg, ct2 = cg, cl = cg;
   bool has_t1 = false, has_t2 = false, has_l = false;
-  double min_teeth = 1000000.0, mt = 1000000.0;
-  int mts = -1;
-  for (int i = S_PHARYNX0; i <= S_LAST_MOUTH; ++i) {
-    double a = X[X_AREA + i - DYN0];
-    if (art[i - S_PHARYNX0] == TONGUE && a < mt) { mt = a; mts = i; }
-  }
-  if (mt < 1.0) {
+  double min_teeth = 1000000.0;
+  const MinIdx t1 = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) { (void)m; return R.art[j] == TONGUE; });
+  if (t1.v < 1.0) {
     has_t1 = true;
-    ct1 = Cons{mts, mts, mts, TONGUE, 0.0, 0.0};
-    grow(X, art, ct1, mt, TONGUE);
-    tongue_obstacle(X, teeth, ct1, min_teeth);
-  }
-  if (has_t1) {
-    const Cons pc = ct1;
-    mt = 1000000.0;
-    mts = -1;
-    for (int i = S_PHARYNX0; i <= S_LAST_MOUTH; ++i) {
-      double a = X[X_AREA + i - DYN0];
-      if (art[i - S_PHARYNX0] == TONGUE && a < mt && (i < pc.first || i > pc.last)) { mt = a; mts = i; }
-    }
-    if (mt < 1.0) {
-      ct2 = Cons{mts, mts, mts, TONGUE, 0.0, 0.0};
-      grow(X, art, ct2, mt, TONGUE);
-      if (ct2.first > pc.last + 1 || ct2.last < pc.first - 1) {
+    const int s = S_PHARYNX0 + t1.i;
+    ct1 = Cons{s, s, s, TONGUE, 0.0, 0.0};
+    grow(ct1, t1.v, TONGUE);
+    tongue_obstacle(ct1, min_teeth);
+    const int pf = ct1.first, pl = ct1.last;
+    const MinIdx t2 = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) {
+      const int sm = S_PHARYNX0 + m;
+      return R.art[j] == TONGUE && (sm < pf || sm > pl);
+    });
+    x.mark(PH_C_T1);
+    if (t2.v < 1.0) {
+      const int s2 = S_PHARYNX0 + t2.i;
+      ct2 = Cons{s2, s2, s2, TONGUE, 0.0, 0.0};
+      grow(ct2, t2.v, TONGUE);
+      if (ct2.first > pl + 1 || ct2.last < pf - 1) {
         has_t2 = true;
-        tongue_obstacle(X, teeth, ct2, min_teeth);
+        tongue_obstacle(ct2, min_teeth);
       }
     }
   }
-  double ml = 1000000.0;
-  int mls = -1;
-  for (int i = S_PHARYNX0; i <= S_LAST_MOUTH; ++i) {
-    double a = X[X_AREA + i - DYN0];
-    if (art[i - S_PHARYNX0] == LOWER_LIP && a < ml) { ml = a; mls = i; }
-  }
-  if (ml < 1.0 && ml < min_teeth) {
+  x.mark(PH_C_T2);
+  const MinIdx lp = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) { (void)m; return R.art[j] == LOWER_LIP; });
+  if (lp.v < 1.0 && lp.v < min_teeth) {
     has_l = true;
-    cl = Cons{mls, mls, mls, LOWER_LIP, 0.0, 0.0};
-    grow(X, art, cl, ml, LOWER_LIP);
+    const int s = S_PHARYNX0 + lp.i;
+    cl = Cons{s, s, s, LOWER_LIP, 0.0, 0.0};
+    grow(cl, lp.v, LOWER_LIP);
     cl.obst = X[X_POS + cl.last + 1 - S_PHARYNX0];
   }
-  dipole_targets(X, T, C, teeth, cg);
-  if (has_t1) dipole_targets(X, T, C, teeth, ct1);
-  if (has_t2) dipole_targets(X, T, C, teeth, ct2);
-  if (has_l) dipole_targets(X, T, C, teeth, cl);
+  x.mark(PH_C_LIP);
+  dipole_targets<W>(x, X, U, C, teeth, cg);
+  if (has_t1) dipole_targets<W>(x, X, U, C, teeth, ct1);
+  if (has_t2) dipole_targets<W>(x, X, U, C, teeth, ct2);
+  if (has_l) dipole_targets<W>(x, X, U, C, teeth, cl);
 }
 
-// Phase A (all lanes): amplitude smoothing of owned dipoles (TdsModel.cpp:1637-1666).
-template <int W>
-AFS_HD inline void phase_noise_amp(int gl, Lane<W> &R, double *X, const Tables &T) {
+// Phase N: noise sources (TdsModel.cpp:1630-1708).  Amplitude smoothing of the owned
+// dipoles, then the rand() draws: source d, the q-th active one in source order, takes
+// draws 12q .. 12q+11 of this sample, and the 16 lanes generate the stream 31 values at a
+// time (rng_block_value) instead of one draw after another.  Then the one-pole shaping
+// filter of the owned active dipoles.
+template <int W, class Xc>
+AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  #pragma unroll
-  for (int k = 0; k < S::NDP; ++k) {
-    int d = gl + k * W;
-    if (d >= NDIP) continue;
-    double cn = X[X_CUTN + d];
-    if (cn != 0.0) R.dcut[k] = cn;  // targeted this step: cutoff was (re)assigned
-    double old = R.damp[k];
-    double amp = old + T.noise_amp_F * (X[X_TGT + d] - old);
-    R.damp[k] = amp;
-    if (old >= THR && amp < THR) R.dout[k] = 0.0;
-    X[X_ACT + d] = (amp < THR) ? 0.0 : 1.0;
-  }
-}
-
-// Phase R (lane 0): random inputs of the active sources, in source order (TdsModel.cpp:1690-1696).
-AFS_HD inline void phase_noise_rng(double *X, const Tables &T) {
-  int32_t *rng = (int32_t *)(X + X_RNG);
-  for (int d = 0; d < NDIP; ++d) {
-    if (X[X_ACT + d] == 0.0) continue;
-    uint32_t acc = 0;
-    for (int k = 0; k < 12; ++k) acc += (uint32_t)rng_next(rng);
-    double xi = (double)(int32_t)acc;
-    xi /= (double)2147483647;
-    xi -= 6.0;
-    xi /= T.sqrt12;
-    X[X_TGT + d] = xi;  // X_TGT is free again: reused for the inputs
-  }
-}
-
-// Phase F (all lanes): one-pole shaping filter of owned active dipoles (TdsModel.cpp:1672-1707).
-template <int W>
-AFS_HD inline void phase_noise_filter(int gl, Lane<W> &R, double *X, const Tables &T) {
-  using S = Shape<W>;
-  #pragma unroll
-  for (int k = 0; k < S::NDP; ++k) {
-    int d = gl + k * W;
-    if (d >= NDIP) continue;
-    double smp = 0.0;
-    if (X[X_ACT + d] != 0.0) {
-      double cut = R.dcut[k];
-      double x = (cut == 2000.0) ? T.noise_x_2000 : exp(-2.0 * PI * (cut * T.dt));
-      double y = (1.0 - x) * X[X_TGT + d];
-      y += x * R.dout[k];
-      R.dout[k] = y;
-      smp = y * R.damp[k];
+  x.par([&](int gl, Lane<W> &R) {
+#pragma unroll
+    for (int k = 0; k < S::NDP; ++k) {
+      const int d = gl + k * W;
+      if (d >= NDIP) continue;
+      double cn = X[X_CUTN + d];
+      if (cn != 0.0) R.dcut[k] = cn;  // targeted this step: cutoff was (re)assigned
+      double old = R.damp[k];
+      double amp = old + C.h.noise_amp_F * (X[X_TGT + d] - old);
+      R.damp[k] = amp;
+      if (old >= THR && amp < THR) R.dout[k] = 0.0;
+      R.racc[k] = 0u;
     }
-    X[X_SMP + d] = smp;
+  });
+  x.mark(PH_N_AMP);
+  uint64_t act = 0;
+#pragma unroll
+  for (int k = 0; k < S::NDP; ++k)
+    act |= x.ballot([&](int gl, Lane<W> &R) { return gl + k * W < NDIP && !(R.damp[k] < THR); }) << (k * W);
+  if (act == 0) {
+    x.par([&](int gl, Lane<W> &R) {
+      (void)R;
+#pragma unroll
+      for (int k = 0; k < S::NDP; ++k)
+        if (gl + k * W < NDIP) X[X_SMP + gl + k * W] = 0.0;
+    });
+    return;
   }
+  uint32_t *ring = (uint32_t *)(X + X_RNG);
+  const int32_t *ctl = (const int32_t *)ring;
+  const int head0 = ctl[RNG_HEAD], pend = ctl[RNG_PEND];
+  const int base = head0 - pend;  // ring index of this sample's first draw
+  const int need = 12 * __builtin_popcountll(act);
+  // draws [lo, hi) of this sample are in the ring: add them to the owners' sums
+  auto consume = [&](int lo, int hi) {
+    x.par([&](int gl, Lane<W> &R) {
+#pragma unroll
+      for (int k = 0; k < S::NDP; ++k) {
+        const int d = gl + k * W;
+        if (d >= NDIP || !((act >> d) & 1)) continue;
+        const int q0 = 12 * __builtin_popcountll(act & ((1ull << d) - 1));
+        uint32_t acc = R.racc[k];
+#pragma unroll
+        for (int t = 0; t < 12; ++t) {
+          const int pos = q0 + t;
+          const uint32_t v = ring[(base + pos) & (RNG_RING - 1)] >> 1;
+          acc += (pos >= lo && pos < hi) ? v : 0u;
+        }
+        R.racc[k] = acc;
+      }
+    });
+  };
+  int avail = pend;
+  if (avail > 0) consume(0, avail);
+  int head = head0;
+  while (avail < need) {
+    // The new block lands at ring indices head..head+30, at least 33 away from the history
+    // head-31..head-1 it is computed from (mod 64), so it can be stored as it is computed.
+    x.par([&](int gl, Lane<W> &R) {
+      (void)R;
+#pragma unroll
+      for (int i = 0; i < (RNG_BLOCK + W - 1) / W; ++i) {
+        const int k = gl + i * W;
+        if (k < RNG_BLOCK) ring[(head + k) & (RNG_RING - 1)] = rng_block_value(ring, head, k);
+      }
+    });
+    x.sync();
+    consume(avail, avail + RNG_BLOCK);
+    avail += RNG_BLOCK;
+    head = (head + RNG_BLOCK) & (RNG_RING - 1);
+  }
+  x.sync();
+  x.mark(PH_N_RNG);
+  x.one([&](Lane<W> &R) {
+    (void)R;
+    int32_t *c = (int32_t *)ring;
+    c[RNG_HEAD] = head;
+    c[RNG_PEND] = avail - need;
+  });
+  x.par([&](int gl, Lane<W> &R) {
+#pragma unroll
+    for (int k = 0; k < S::NDP; ++k) {
+      const int d = gl + k * W;
+      if (d >= NDIP) continue;
+      double smp = 0.0;
+      if ((act >> d) & 1) {
+        double xi = (double)(int32_t)R.racc[k];
+        xi /= (double)2147483647;
+        xi -= 6.0;
+        xi /= C.h.sqrt12;
+        double cut = R.dcut[k];
+        double xx = (cut == 2000.0) ? C.h.noise_x_2000 : exp(-2.0 * PI * (cut * C.h.dt));
+        double y = (1.0 - xx) * xi;
+        y += xx * R.dout[k];
+        R.dout[k] = y;
+        smp = y * R.damp[k];
+      }
+      X[X_SMP + d] = smp;
+    }
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -630,10 +814,10 @@ AFS_HD inline double sec_R1(const double *X, const Consts &C, int s) {
 }
 
 template <int W>
-AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Tables &T, const Consts &C) {
+AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  const double dt = T.dt;
-  const afs_options &opt = T.opt;
+  const double dt = C.h.dt;
+  const afs_options &opt = U.opt;
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const int s = slot_section<W>(j, gl);
@@ -642,9 +826,9 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Tables &T, co
     const int i = s;  // current i flows into section s
     const double *ks = C.stat[static_index(s)];
     const double LB = dyn ? X[X_L + s - DYN0] : ks[ST_L];
-    const double RB = dyn ? X[X_R0 + s - DYN0] : ((s == S_FOSSA0 && !opt.piriform_fossa) ? T.fossa_R0 : ks[ST_R]);
+    const double RB = dyn ? X[X_R0 + s - DYN0] : ((s == S_FOSSA0 && !opt.piriform_fossa) ? C.h.fossa_R0 : ks[ST_R]);
     const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
-    const double AB = dyn ? X[X_AREA + s - DYN0] : T.area[S_LAST_NOSE];  // static: only used by s = 83
+    const double AB = dyn ? X[X_AREA + s - DYN0] : C.h.area_last_nose;  // static: only used by s = 83
     const double EB = X[X_E + s], DB = X[X_D + s];
     const int a = C.topo[i][TP_SRC];
     double LA = 0.0, RA = 0.0, EA = 0.0, DA = 0.0;
@@ -689,14 +873,14 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Tables &T, co
       R.rad_un[0] = X[X_UN + rc]; R.rad_un[1] = X[X_UN + lc];
       const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
       {
-        double Rrad = T.rrad_num / (9.0 * PI * PI * AB);
+        double Rrad = C.h.rrad_num / (9.0 * PI * PI * AB);
         double F = LA2 / (dt * TH) + RA2 + Rrad;
         double H = -(LA2 / (dt * TH)) * (uR + uL) - (LA2 * (TH1 / TH)) * (uRr + uLr) + Sr;
         X[X_DIAG + rc] = -(-EB - F);
         X[X_RHS + rc] = -(H - DB);
       }
       {
-        double Lrad = T.lrad_num / (3.0 * PI * sqrt(AB * PI));
+        double Lrad = C.h.lrad_num / (3.0 * PI * sqrt(AB * PI));
         double LAB2 = LA2 + Lrad;
         double G = LAB2 / (dt * TH) + RA2;
         double H = -(1.0 / (dt * TH)) * (LA2 * uR + LAB2 * uL) - (TH1 / TH) * (LA2 * uRr + LAB2 * uLr) + Sr;
@@ -710,51 +894,85 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Tables &T, co
 // ---------------------------------------------------------------------------
 // Solver rounds (chain lanes 0..3).
 // ---------------------------------------------------------------------------
-AFS_HD inline void solve_forward(int k, int r, double *X, const Consts &C) {
-  const SolveStep st = C.step[r][k];
-  if (st.c < 0) return;
-  double d = X[X_DIAG + st.c];
-  double inv = (d < 0.0) ? NAN : 1.0 / d;  // the reference takes sqrt of a negative pivot
-  double y = X[X_RHS + st.c];
-  if (st.n0 >= 0) {
-    double a0 = X[X_OFF + st.e0];
-    double f0 = a0 * inv;
-    X[X_DIAG + st.n0] -= f0 * a0;
-    X[X_RHS + st.n0] -= f0 * y;
-    if (st.n1 >= 0) {
-      double a1 = X[X_OFF + st.e1];
-      double f1 = a1 * inv;
-      X[X_DIAG + st.n1] -= f1 * a1;
-      X[X_RHS + st.n1] -= f1 * y;
-      X[X_OFF + st.e01] -= f0 * a1;
+// Forward round r of chain lane k.  Rounds touch disjoint unknowns (checked when the
+// schedule is built), so the pivot and right-hand side this lane wrote for n0 stay exact
+// until another lane touches that unknown; in the rounds flagged in U.fwd_carry every
+// active lane continues its chain with it from registers (a uniform branch), and all loads
+// of the neighbours are issued ahead of the reciprocal.
+AFS_HD inline void solve_forward(int k, int r, int n_rounds, bool carried, double *X, const Consts &C,
+                                 SolveCarry &cr) {
+  const uint64_t w = cr.next;
+  if (r + 1 < n_rounds) cr.next = load_step(C, r + 1, k);
+  const int c = step_field(w, 0);
+  if (c < 0) return;
+  const int n0 = step_field(w, 1), n1 = step_field(w, 2);
+  const int i0 = n0 < 0 ? 0 : n0, i1 = n1 < 0 ? 0 : n1;
+  const int e0 = step_field(w, 3), e1 = step_field(w, 4), e01 = step_field(w, 5);
+  double d0 = X[X_DIAG + i0], y0 = X[X_RHS + i0], a0 = X[X_OFF + (e0 < 0 ? 0 : e0)];
+  double d1 = X[X_DIAG + i1], y1 = X[X_RHS + i1], a1 = X[X_OFF + (e1 < 0 ? 0 : e1)];
+  const double a01 = X[X_OFF + (e01 < 0 ? 0 : e01)];
+  double d, y;
+  if (carried) { d = cr.d; y = cr.y; }
+  else { d = X[X_DIAG + c]; y = X[X_RHS + c]; }
+  const double inv = (d < 0.0) ? NAN : pivot_recip(d);  // the reference takes sqrt of a negative pivot
+  X[X_DIAG + c] = inv;  // X_RHS[c] already holds y (written back by whoever updated it last)
+  if (n0 >= 0) {
+    const double f0 = a0 * inv;
+    d0 -= f0 * a0;
+    y0 -= f0 * y;
+    X[X_DIAG + n0] = d0;
+    X[X_RHS + n0] = y0;
+    cr.d = d0; cr.y = y0;
+    if (n1 >= 0) {
+      const double f1 = a1 * inv;
+      d1 -= f1 * a1;
+      y1 -= f1 * y;
+      X[X_DIAG + n1] = d1;
+      X[X_RHS + n1] = y1;
+      X[X_OFF + e01] = a01 - f0 * a1;
     }
   }
-  X[X_DIAG + st.c] = inv;
 }
 
-AFS_HD inline void solve_backward(int k, int r, double *X, const Consts &C) {
-  const SolveStep st = C.step[r][k];
-  if (st.c < 0) return;
-  double y = X[X_RHS + st.c];
-  if (st.n0 >= 0) y -= X[X_OFF + st.e0] * X[X_U + st.n0];
-  if (st.n1 >= 0) y -= X[X_OFF + st.e1] * X[X_U + st.n1];
-  X[X_U + st.c] = y * X[X_DIAG + st.c];
+// Backward round r: x_c = (y_c - a0 x_n0 - a1 x_n1) / d_c.  In the rounds flagged in
+// U.bwd_carry, x_n0 is the solution this lane produced last (registers) and there is no n1.
+AFS_HD inline void solve_backward(int k, int r, bool carried, double *X, const Consts &C, SolveCarry &cr) {
+  const uint64_t w = cr.next;
+  if (r > 0) cr.next = load_step(C, r - 1, k);
+  const int c = step_field(w, 0);
+  if (c < 0) return;
+  const int n0 = step_field(w, 1), n1 = step_field(w, 2);
+  const int e0 = step_field(w, 3), e1 = step_field(w, 4);
+  double y = X[X_RHS + c];
+  const double inv = X[X_DIAG + c];
+  const double a0 = X[X_OFF + (e0 < 0 ? 0 : e0)];
+  if (carried) {
+    if (n0 >= 0) y -= a0 * cr.y;
+  } else {
+    const double a1 = X[X_OFF + (e1 < 0 ? 0 : e1)];
+    const double x0 = X[X_U + (n0 < 0 ? 0 : n0)], x1 = X[X_U + (n1 < 0 ? 0 : n1)];
+    if (n0 >= 0) y -= a0 * x0;
+    if (n1 >= 0) y -= a1 * x1;
+  }
+  const double xc = y * inv;
+  X[X_U + c] = xc;
+  cr.y = xc;
 }
 
 // ---------------------------------------------------------------------------
 // Phase U: updateVariables (TdsModel.cpp:2046-2098).
 // ---------------------------------------------------------------------------
 template <int W>
-AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Tables &T, const Consts &C) {
+AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  const double dt = T.dt, c = T.noise_lp_c;
+  const double dt = C.h.dt, c = C.h.noise_lp_c;
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const int s = slot_section<W>(j, gl);
     if (s < 0) continue;
     double alpha, beta;
     if (j < S::ND) { alpha = R.al[j]; beta = R.be[j]; }
-    else { alpha = C.stat[static_index(s)][ST_ALPHA]; beta = static_beta<W>(R, j, T, C, s); }  // same values as phase_network
+    else { alpha = C.stat[static_index(s)][ST_ALPHA]; beta = static_beta<W>(R, j, U, C, s); }  // same values as phase_network
     const double unew = X[X_U + s];
     const double uold = R.u[j];
     R.u[j] = unew;
@@ -795,16 +1013,16 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Tables &T, 
 
 // Phase O (lane 0): radiated flow, glottal tone, output filter (TdsModel.cpp:687-705,
 // Synthesizer.cpp:614-627).  Returns the audio sample.
-AFS_HD inline double phase_output(double *X, const Tables &T) {
+AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C) {
   double flow = 0.0;
   flow += X[X_U + 93];
   flow += X[X_U + 94];
   flow += X[X_U + 95];
   flow += X[X_U + 96];
-  if (T.opt.radiation_from_skin) flow += iir_run(X + X_TONE, 4, T.tone_a, T.tone_b, X[X_P4 + 3]);
-  double op = (flow - X[X_PREVFLOW]) / T.dt;
+  if (U.opt.radiation_from_skin) flow += iir_run(X + X_TONE, 4, C.h.tone_a, C.h.tone_b, X[X_P4 + 3]);
+  double op = (flow - X[X_PREVFLOW]) / C.h.dt;
   X[X_PREVFLOW] = flow;
-  double y = iir_run(X + X_OUTF, 8, T.out_a, T.out_b, op);
+  double y = iir_run(X + X_OUTF, 8, C.h.out_a, C.h.out_b, op);
   double smp = y * 0.004;
   smp = smp / 32767;
   if (!isfinite(smp)) X[X_NONFIN] = 1.0;
@@ -814,20 +1032,20 @@ AFS_HD inline double phase_output(double *X, const Tables &T) {
 // ---------------------------------------------------------------------------
 // One audio sample.  Xc: execution policy (par / one / lanes / sync).
 // ---------------------------------------------------------------------------
+
 template <int W, class Xc>
-AFS_HD inline void sample_step(Xc &x, double *X, const Tables &T, const Consts &C, double ratio) {
-  x.par([&](int gl, Lane<W> &R) { phase_geometry<W>(gl, R, X, T, ratio); });
+AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
+  x.par([&](int gl, Lane<W> &R) { phase_geometry<W>(gl, R, X, U, C, ratio); });
   x.sync();
-  x.par([&](int gl, Lane<W> &R) { phase_network<W>(gl, R, X, T, C); });
+  x.mark(PH_GEOMETRY);
+  x.par([&](int gl, Lane<W> &R) { phase_network<W>(gl, R, X, U, C); });
   x.sync();
-  if (T.opt.generate_noise_sources) {
-    x.one([&](Lane<W> &R) { phase_constrictions<W>(R, X, T, C); });
+  x.mark(PH_NETWORK);
+  if (U.opt.generate_noise_sources) {
+    phase_constrictions<W>(x, X, U, C);
     x.sync();
-    x.par([&](int gl, Lane<W> &R) { phase_noise_amp<W>(gl, R, X, T); });
-    x.sync();
-    x.one([&](Lane<W> &R) { (void)R; phase_noise_rng(X, T); });
-    x.sync();
-    x.par([&](int gl, Lane<W> &R) { phase_noise_filter<W>(gl, R, X, T); });
+    x.mark(PH_CONSTRICTIONS);
+    phase_noise<W>(x, X, U, C);
   } else {
     x.par([&](int gl, Lane<W> &R) {
       (void)R;
@@ -835,19 +1053,30 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Tables &T, const Consts &
     });
   }
   x.sync();
-  x.par([&](int gl, Lane<W> &R) { phase_rows<W>(gl, R, X, T, C); });
+  x.mark(PH_NOISE);
+  x.par([&](int gl, Lane<W> &R) { phase_rows<W>(gl, R, X, U, C); });
   x.sync();
-  for (int r = 0; r < T.n_rounds; ++r) {
-    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { (void)R; solve_forward(k, r, X, C); });
+  x.mark(PH_ROWS);
+  const int nr = U.n_rounds;
+  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { R.sc.next = load_step(C, 0, k); });
+  for (int r = 0; r < nr; ++r) {
+    const bool carried = (U.fwd_carry >> r) & 1;
+    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { solve_forward(k, r, nr, carried, X, C, R.sc); });
     x.sync();
   }
-  for (int r = T.n_rounds - 1; r >= 0; --r) {
-    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { (void)R; solve_backward(k, r, X, C); });
+  x.mark(PH_FORWARD);
+  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { R.sc.next = load_step(C, nr - 1, k); });
+  for (int r = nr - 1; r >= 0; --r) {
+    const bool carried = (U.bwd_carry >> r) & 1;
+    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { solve_backward(k, r, carried, X, C, R.sc); });
     x.sync();
   }
-  x.par([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, T, C); });
+  x.mark(PH_BACKWARD);
+  x.par([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, U, C); });
   x.sync();
-  x.one([&](Lane<W> &R) { R.sample = phase_output(X, T); });
+  x.mark(PH_UPDATE);
+  x.one([&](Lane<W> &R) { R.sample = phase_output(X, U, C); });
+  x.mark(PH_OUTPUT);
 }
 
 }  // namespace tree

@@ -1,0 +1,140 @@
+// tree_kernel.h -- body of the cooperative synthesis kernel (afs_solver AFS_SOLVER_TREE),
+// shared by tds_tree.hip (the product kernel) and tools/phase_prof (the same body with
+// per-phase cycle counters).
+//
+// Mapping on gfx950: a wave64 holds four utterances, TREE_W = 16 lanes each.  A lane keeps
+// the state of its 6 sections (3 dynamic + 3 static) and their in-currents in registers
+// for the whole launch; the four utterances' 8.4 KB LDS blocks carry neighbour exchange,
+// the per-sample solver arrays and the small persistent state.  Waves never wait for one
+// another (no __syncthreads in the time loop): phases of one utterance are ordered by
+// wave-level fences, which is all LDS needs inside a wave.  The time loop runs inside the
+// kernel; a launch covers a range of frame transitions and saves the lane/LDS state at the
+// end, so long utterances and incremental sessions continue exactly where they stopped.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "afs_tree.h"
+#include "tree_core.h"
+
+namespace afs {
+namespace tree {
+
+constexpr int TW = TREE_W;
+constexpr int UPW = 64 / TW;  // utterances per wave
+
+template <bool PROF>
+struct GpuExec {
+  int gl;
+  Lane<TW> *R;
+  uint64_t last = 0;
+  uint64_t acc[PROF ? PH_COUNT : 1] = {};
+  template <class F> __device__ __forceinline__ void par(F f) { f(gl, *R); }
+  template <class F> __device__ __forceinline__ void one(F f) { if (gl == 0) f(*R); }
+  template <class F> __device__ __forceinline__ void lanes(int n, F f) { if (gl < n) f(gl, *R); }
+  __device__ __forceinline__ void sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // Collectives over the 16 lanes of this utterance = one DPP row: quad_perm xor 1 and
+  // xor 2, then row_half_mirror and row_mirror combine quads and halves (all lanes of the
+  // row end with the same result).
+  template <class F> __device__ __forceinline__ uint64_t ballot(F f) {
+    const bool p = f(gl, *R);
+    const uint64_t b = __ballot(p);
+    return (b >> (__lane_id() & ~(TW - 1))) & ((1ull << TW) - 1);
+  }
+  template <int CTRL> __device__ __forceinline__ static int dpp(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+  }
+  template <int CTRL> __device__ __forceinline__ static double dpp(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const int lo = dpp<CTRL>((int)(uint32_t)b), hi = dpp<CTRL>((int)(uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  }
+  template <int CTRL> __device__ __forceinline__ static MinIdx min_step(MinIdx a) {
+    return min_idx_combine(a, MinIdx{dpp<CTRL>(a.v), dpp<CTRL>(a.i)});
+  }
+  template <class F> __device__ __forceinline__ MinIdx min_index(F f) {
+    static_assert(TW == 16, "DPP row collectives assume 16 lanes per utterance");
+    MinIdx b = f(gl, *R);
+    b = min_step<0xB1>(b);   // quad_perm [1,0,3,2]
+    b = min_step<0x4E>(b);   // quad_perm [2,3,0,1]
+    b = min_step<0x141>(b);  // row_half_mirror
+    b = min_step<0x140>(b);  // row_mirror
+    return b;
+  }
+  template <class F> __device__ __forceinline__ double max_value(F f) {
+    double b = f(gl, *R);
+    b = max_combine(b, dpp<0xB1>(b));
+    b = max_combine(b, dpp<0x4E>(b));
+    b = max_combine(b, dpp<0x141>(b));
+    b = max_combine(b, dpp<0x140>(b));
+    return b;
+  }
+  __device__ __forceinline__ void mark(int ph) {
+    if constexpr (PROF) {
+      uint64_t t = __builtin_amdgcn_s_memtime();
+      acc[ph] += t - last;
+      last = t;
+    }
+  }
+};
+
+// One block of LDS per wave: the packed hot tables (shared by the four utterances) and the
+// four utterance blocks.
+struct WaveLds {
+  Consts C;
+  double X[UPW][X_TOTAL];
+};
+
+// prof (PROF only): per wave, PH_COUNT cycle sums (s_memtime) over the launch.
+template <bool PROF>
+__device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds, uint64_t *prof) {
+  const int lane = threadIdx.x;
+  const int g = lane / TW, gl = lane % TW;
+  const int u = blockIdx.x * UPW + g;
+  const bool valid = u < a.B;
+  const int ue = valid ? u : 0;
+  double *X = lds.X[g];
+  const Tables &T = *a.tab;
+  {  // stage the hot tables (8-byte words; Consts is a multiple of 8 bytes)
+    const uint64_t *src = (const uint64_t *)&T.consts;
+    uint64_t *dst = (uint64_t *)&lds.C;
+    for (int k = lane; k < (int)(sizeof(Consts) / 8); k += 64) dst[k] = src[k];
+  }
+  Lane<TW> R = ((const Lane<TW> *)a.lane_state)[(int64_t)ue * TW + gl];
+  const double *ls = a.lds_state + (int64_t)ue * X_TOTAL;
+  for (int k = gl; k < X_TOTAL; k += TW) X[k] = ls[k];
+  __syncthreads();
+  const Consts &C = lds.C;
+  GpuExec<PROF> ex{gl, &R};
+  if constexpr (PROF) ex.last = __builtin_amdgcn_s_memtime();
+  const afs_frame *fu = a.frames + (int64_t)ue * a.frame_stride;
+  double *o = a.out + (int64_t)ue * a.out_stride;
+  int64_t t = 0;
+  for (int k = a.k_begin; k < a.k_end; ++k) {
+    frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
+    ex.sync();
+    for (int i = 0; i < a.hop; ++i) {
+      const double ratio = (double)i / (double)a.hop;
+      sample_step<TW>(ex, X, a.uni, C, ratio);
+      if (valid && gl == 0) o[t] = R.sample;
+      ++t;
+    }
+  }
+  ex.sync();
+  if (valid) {
+    ((Lane<TW> *)a.lane_state)[(int64_t)u * TW + gl] = R;
+    double *ws = a.lds_state + (int64_t)u * X_TOTAL;
+    for (int k = gl; k < X_TOTAL; k += TW) ws[k] = X[k];
+  }
+  if constexpr (PROF) {
+    if (lane == 0)
+      for (int p = 0; p < PH_COUNT; ++p) prof[(int64_t)blockIdx.x * PH_COUNT + p] = ex.acc[p];
+  }
+}
+
+}  // namespace tree
+}  // namespace afs

@@ -22,6 +22,23 @@ struct CpuExec {
   template <class F> void one(F f) { f(R[0]); }
   template <class F> void lanes(int n, F f) { for (int k = 0; k < n; ++k) f(k, R[k]); }
   void sync() {}
+  void mark(int) {}
+  template <class F> uint64_t ballot(F f) {
+    uint64_t m = 0;
+    for (int gl = 0; gl < W; ++gl)
+      if (f(gl, R[gl])) m |= 1ull << gl;
+    return m;
+  }
+  template <class F> MinIdx min_index(F f) {
+    MinIdx b = f(0, R[0]);
+    for (int gl = 1; gl < W; ++gl) b = min_idx_combine(b, f(gl, R[gl]));
+    return b;
+  }
+  template <class F> double max_value(F f) {
+    double b = f(0, R[0]);
+    for (int gl = 1; gl < W; ++gl) b = max_combine(b, f(gl, R[gl]));
+    return b;
+  }
 };
 
 template <int W>
@@ -40,7 +57,7 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
     for (int gl = 0; gl < W; ++gl) frame_load<W>(gl, R[gl], X.data(), frames + k - 1, frames + k);
     for (int i = 0; i < hop; ++i) {
       double ratio = (double)i / (double)hop;
-      sample_step<W>(ex, X.data(), T, T.consts, ratio);
+      sample_step<W>(ex, X.data(), T.uni, T.consts, ratio);
       out[t] = R[0].sample;
       if (t < ndump) {
         for (int gl = 0; gl < W; ++gl)

@@ -1,0 +1,75 @@
+// phase_prof.hip -- development tool: the tree kernel body with per-phase cycle counters
+// (s_memtime deltas, accumulated per wave).  Not part of libafs; built by this directory's
+// Makefile and driven by run.py on the GPU box.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#include "tree_kernel.h"
+
+using namespace afs;
+using namespace afs::tree;
+
+__global__ void __launch_bounds__(64) tree_prof_kernel(TreeArgs a, uint64_t *prof) {
+  __shared__ WaveLds lds;
+  tree_synth_body<true>(a, lds, prof);
+}
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      return -1;                                                               \
+    }                                                                          \
+  } while (0)
+
+extern "C" int pp_phase_count() { return PH_COUNT; }
+
+// frames[B][F] host; cycles[PH_COUNT] = sum over waves; returns kernel ms in *ms.
+extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int F, int hop, double fs,
+                      uint64_t *cycles, double *ms) {
+  Tables *ht = new Tables();
+  afs_options opt{1, 1, 1, 1, 0, 1};
+  build_tables(ht, fs, opt);
+  Tables *dt;
+  afs_frame *df;
+  uint32_t *ds;
+  double *dout, *dlds;
+  void *dlanes;
+  uint64_t *dprof;
+  const int waves = (B + UPW - 1) / UPW;
+  CK(hipMalloc(&dt, sizeof(Tables)));
+  CK(hipMemcpy(dt, ht, sizeof(Tables), hipMemcpyHostToDevice));
+  CK(hipMalloc(&df, sizeof(afs_frame) * B * F));
+  CK(hipMemcpy(df, frames, sizeof(afs_frame) * B * F, hipMemcpyHostToDevice));
+  CK(hipMalloc(&ds, 4 * B));
+  CK(hipMemcpy(ds, seeds, 4 * B, hipMemcpyHostToDevice));
+  CK(hipMalloc(&dout, sizeof(double) * (size_t)B * (F - 1) * hop));
+  CK(hipMalloc(&dlds, sizeof(double) * (size_t)B * tree_lds_doubles()));
+  CK(hipMalloc(&dlanes, (size_t)B * TW * tree_lane_bytes()));
+  CK(hipMalloc(&dprof, sizeof(uint64_t) * waves * PH_COUNT));
+  CK(launch_tree_reset(dlanes, dlds, B, ds, nullptr));
+  TreeArgs a{dt, df, F, 1, F, hop, dout, (int64_t)(F - 1) * hop, dlanes, dlds, B, ht->uni};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, nullptr));
+  hipLaunchKernelGGL(tree_prof_kernel, dim3(waves), dim3(64), 0, nullptr, a, dprof);
+  CK(hipGetLastError());
+  CK(hipEventRecord(e1, nullptr));
+  CK(hipEventSynchronize(e1));
+  float fms = 0;
+  CK(hipEventElapsedTime(&fms, e0, e1));
+  *ms = fms;
+  std::vector<uint64_t> h((size_t)waves * PH_COUNT);
+  CK(hipMemcpy(h.data(), dprof, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
+  for (int p = 0; p < PH_COUNT; ++p) cycles[p] = 0;
+  for (int w = 0; w < waves; ++w)
+    for (int p = 0; p < PH_COUNT; ++p) cycles[p] += h[(size_t)w * PH_COUNT + p];
+  (void)hipFree(dt); (void)hipFree(df); (void)hipFree(ds); (void)hipFree(dout);
+  (void)hipFree(dlds); (void)hipFree(dlanes); (void)hipFree(dprof);
+  delete ht;
+  return waves;
+}
