@@ -27,7 +27,10 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters (spec)
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (spec)
-FLOPS_PER_SAMPLE = 1.8e4       # reference algorithm, analytic estimate
+# fp64 flops per utterance-sample executed by the tree kernel, counted on the GPU:
+# SQ_INSTS_VALU_FLOPS_FP64 / (utterances x samples), profiles/r01_pmc_sq_v2c.txt.  (SURVEY.md
+# 8(a)'s 1.8e4 is the reference's dense-envelope Cholesky path, not this algorithm.)
+FLOPS_PER_SAMPLE = 1068.0
 
 
 def frame_bytes_per_sample(hop: int) -> float:
