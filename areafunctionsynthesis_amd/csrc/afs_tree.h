@@ -20,7 +20,17 @@ struct TreeArgs {
   Uni uni;                  // copy of tab->uni: scalar kernel arguments
 };
 
-constexpr int TREE_W = 16;  // lanes per utterance
+#ifndef AFS_TREE_W
+#define AFS_TREE_W 16
+#endif
+#ifndef AFS_TREE_WPB
+#define AFS_TREE_WPB 1
+#endif
+#ifndef AFS_TREE_MIN_WAVES
+#define AFS_TREE_MIN_WAVES 1  // waves per SIMD the register allocation must allow
+#endif
+constexpr int TREE_W = AFS_TREE_W;      // lanes per utterance (16 or 32)
+constexpr int TREE_WPB = AFS_TREE_WPB;  // waves per block
 int64_t tree_lane_bytes();
 int64_t tree_lds_doubles();
 hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const uint32_t *seeds, hipStream_t st);

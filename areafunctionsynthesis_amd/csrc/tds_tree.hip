@@ -8,7 +8,7 @@ using namespace tree;
 
 namespace {
 
-__global__ void __launch_bounds__(64) tree_synth_kernel(TreeArgs a) {
+__global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_synth_kernel(TreeArgs a) {
   __shared__ WaveLds lds;
   tree_synth_body<false>(a, lds, nullptr);
 }
@@ -44,7 +44,7 @@ hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const u
 
 hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st) {
   if (a.B <= 0 || a.k_end <= a.k_begin) return hipSuccess;
-  hipLaunchKernelGGL(tree_synth_kernel, dim3((a.B + UPW - 1) / UPW), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(tree_synth_kernel, dim3((a.B + UPB - 1) / UPB), dim3(64 * WPB), 0, st, a);
   return hipGetLastError();
 }
 

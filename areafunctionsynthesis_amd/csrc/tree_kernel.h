@@ -21,7 +21,10 @@ namespace afs {
 namespace tree {
 
 constexpr int TW = TREE_W;
-constexpr int UPW = 64 / TW;  // utterances per wave
+constexpr int UPW = 64 / TW;          // utterances per wave
+constexpr int WPB = TREE_WPB;         // waves per block (they share one copy of the tables)
+constexpr int UPB = UPW * WPB;        // utterances per block
+static_assert(TW == 16 || TW == 32, "collectives are written for 16 or 32 lanes per utterance");
 
 template <bool PROF>
 struct GpuExec {
@@ -37,9 +40,9 @@ struct GpuExec {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  // Collectives over the 16 lanes of this utterance = one DPP row: quad_perm xor 1 and
-  // xor 2, then row_half_mirror and row_mirror combine quads and halves (all lanes of the
-  // row end with the same result).
+  // Collectives over the lanes of this utterance.  16 lanes = one DPP row: quad_perm xor 1
+  // and xor 2, then row_half_mirror and row_mirror combine quads and halves (all lanes of
+  // the row end with the same result); 32 lanes add a swap of the two rows (lane ^ 16).
   template <class F> __device__ __forceinline__ uint64_t ballot(F f) {
     const bool p = f(gl, *R);
     const uint64_t b = __ballot(p);
@@ -56,13 +59,15 @@ struct GpuExec {
   template <int CTRL> __device__ __forceinline__ static MinIdx min_step(MinIdx a) {
     return min_idx_combine(a, MinIdx{dpp<CTRL>(a.v), dpp<CTRL>(a.i)});
   }
+  __device__ __forceinline__ static double xor16(double v) { return __shfl_xor(v, 16, 64); }
+  __device__ __forceinline__ static int xor16(int v) { return __shfl_xor(v, 16, 64); }
   template <class F> __device__ __forceinline__ MinIdx min_index(F f) {
-    static_assert(TW == 16, "DPP row collectives assume 16 lanes per utterance");
     MinIdx b = f(gl, *R);
     b = min_step<0xB1>(b);   // quad_perm [1,0,3,2]
     b = min_step<0x4E>(b);   // quad_perm [2,3,0,1]
     b = min_step<0x141>(b);  // row_half_mirror
     b = min_step<0x140>(b);  // row_mirror
+    if constexpr (TW == 32) b = min_idx_combine(b, MinIdx{xor16(b.v), xor16(b.i)});
     return b;
   }
   template <class F> __device__ __forceinline__ double max_value(F f) {
@@ -71,6 +76,7 @@ struct GpuExec {
     b = max_combine(b, dpp<0x4E>(b));
     b = max_combine(b, dpp<0x141>(b));
     b = max_combine(b, dpp<0x140>(b));
+    if constexpr (TW == 32) b = max_combine(b, xor16(b));
     return b;
   }
   __device__ __forceinline__ void mark(int ph) {
@@ -82,19 +88,19 @@ struct GpuExec {
   }
 };
 
-// One block of LDS per wave: the packed hot tables (shared by the four utterances) and the
-// four utterance blocks.
+// LDS of one block: the packed hot tables (shared by all its utterances) and one block per
+// utterance.
 struct WaveLds {
   Consts C;
-  double X[UPW][X_TOTAL];
+  double X[UPB][X_TOTAL];
 };
 
 // prof (PROF only): per wave, PH_COUNT cycle sums (s_memtime) over the launch.
 template <bool PROF>
 __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds, uint64_t *prof) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x;  // 0 .. 64 WPB - 1
   const int g = lane / TW, gl = lane % TW;
-  const int u = blockIdx.x * UPW + g;
+  const int u = blockIdx.x * UPB + g;
   const bool valid = u < a.B;
   const int ue = valid ? u : 0;
   double *X = lds.X[g];
@@ -102,7 +108,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   {  // stage the hot tables (8-byte words; Consts is a multiple of 8 bytes)
     const uint64_t *src = (const uint64_t *)&T.consts;
     uint64_t *dst = (uint64_t *)&lds.C;
-    for (int k = lane; k < (int)(sizeof(Consts) / 8); k += 64) dst[k] = src[k];
+    for (int k = lane; k < (int)(sizeof(Consts) / 8); k += 64 * WPB) dst[k] = src[k];
   }
   Lane<TW> R = ((const Lane<TW> *)a.lane_state)[(int64_t)ue * TW + gl];
   const double *ls = a.lds_state + (int64_t)ue * X_TOTAL;
@@ -131,8 +137,9 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
     for (int k = gl; k < X_TOTAL; k += TW) ws[k] = X[k];
   }
   if constexpr (PROF) {
-    if (lane == 0)
-      for (int p = 0; p < PH_COUNT; ++p) prof[(int64_t)blockIdx.x * PH_COUNT + p] = ex.acc[p];
+    if (lane % 64 == 0)
+      for (int p = 0; p < PH_COUNT; ++p)
+        prof[((int64_t)blockIdx.x * WPB + lane / 64) * PH_COUNT + p] = ex.acc[p];
   }
 }
 

@@ -11,7 +11,7 @@
 using namespace afs;
 using namespace afs::tree;
 
-__global__ void __launch_bounds__(64) tree_prof_kernel(TreeArgs a, uint64_t *prof) {
+__global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_prof_kernel(TreeArgs a, uint64_t *prof) {
   __shared__ WaveLds lds;
   tree_synth_body<true>(a, lds, prof);
 }
@@ -39,7 +39,7 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   double *dout, *dlds;
   void *dlanes;
   uint64_t *dprof;
-  const int waves = (B + UPW - 1) / UPW;
+  const int blocks = (B + UPB - 1) / UPB, waves = blocks * WPB;
   CK(hipMalloc(&dt, sizeof(Tables)));
   CK(hipMemcpy(dt, ht, sizeof(Tables), hipMemcpyHostToDevice));
   CK(hipMalloc(&df, sizeof(afs_frame) * B * F));
@@ -56,7 +56,7 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0, nullptr));
-  hipLaunchKernelGGL(tree_prof_kernel, dim3(waves), dim3(64), 0, nullptr, a, dprof);
+  hipLaunchKernelGGL(tree_prof_kernel, dim3(blocks), dim3(64 * WPB), 0, nullptr, a, dprof);
   CK(hipGetLastError());
   CK(hipEventRecord(e1, nullptr));
   CK(hipEventSynchronize(e1));
