@@ -67,9 +67,19 @@ AFS_HD constexpr bool is_static_section(int s) {
 constexpr int TREE_CHAINS = 4;
 constexpr int TREE_MAX_ROUNDS = 36;
 constexpr int TREE_NE = 104;
-struct alignas(8) SolveStep {  // 8 bytes: one LDS load, kept packed until it is used
-  int8_t c, n0, n1, e0, e1, e01, pad0, pad1;
+struct SolveStep {
+  int8_t c, n0, n1, e0, e1, e01;
 };
+// The kernel's form of a step: LDS byte offsets inside the utterance block, 16 bytes = one
+// LDS load.  c/n0/n1 address the pivot (rhs at a fixed distance), e0/e1/e01 the edges,
+// un0/un1 the solutions of n0/n1.  Absent neighbours and idle lanes point at sink slots
+// (written, never read for real work) or zero slots (0.0, never written), so a round has
+// no branches.
+struct alignas(16) StepRec {
+  uint16_t c, n0, n1, e0, e1, e01, un0, un1;
+};
+// Currents whose d/dt another lane reads (branch partners and radiation; tree_core.h X_UR).
+constexpr int NUR = 16;
 
 // The tables the cooperative kernel reads inside its time loop, packed so that one copy
 // per wave fits in LDS next to the four utterance blocks (tds_tree.hip).
@@ -91,7 +101,8 @@ struct Uni {
 };
 struct Consts {
   Hot h;
-  SolveStep step[TREE_MAX_ROUNDS][TREE_CHAINS];
+  StepRec step[TREE_MAX_ROUNDS][TREE_CHAINS];
+  int8_t ur_slot[NC];  // X_UR slot of a current, -1: none
   int8_t topo[NS][TP_N];
   double stat[NSTATIC][ST_N];
 };

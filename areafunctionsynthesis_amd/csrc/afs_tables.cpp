@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "afs_model.h"
+#include "tree_core.h"
 
 namespace afs {
 
@@ -195,7 +196,7 @@ bool tree_schedule(Tables *t) {
   if (rounds > TREE_MAX_ROUNDS) return false;
   t->n_rounds = rounds;
   for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
-    for (int k = 0; k < TREE_CHAINS; ++k) t->step[r][k] = SolveStep{-1, -1, -1, -1, -1, -1, 0, 0};
+    for (int k = 0; k < TREE_CHAINS; ++k) t->step[r][k] = SolveStep{-1, -1, -1, -1, -1, -1};
   // symbolic elimination: adjacency of remaining currents
   static bool adj[NC][NC];
   std::memset(adj, 0, sizeof adj);
@@ -212,7 +213,7 @@ bool tree_schedule(Tables *t) {
       if (!gone[j] && adj[c][j]) nb[n++] = j;
     if (n > 2) return false;                                   // would create fill
     if (n == 2 && !adj[nb[0]][nb[1]]) return false;            // neighbours must be a clique
-    SolveStep st{(int8_t)c, -1, -1, -1, -1, -1, 0, 0};
+    SolveStep st{(int8_t)c, -1, -1, -1, -1, -1};
     int id;
     if (n >= 1) { st.n0 = (int8_t)nb[0]; if (!sec_of_pair(c, nb[0], &id)) return false; st.e0 = (int8_t)id; }
     if (n == 2) {
@@ -249,8 +250,9 @@ bool tree_schedule(Tables *t) {
     if (!gone[c]) return false;
   if (t->step[rounds - 1][0].n0 != -1) return false;
   // Register carries (tree_core.h solve_forward / solve_backward).  Forward: after a step
-  // the lane holds the new pivot of its n0, valid until another lane touches that unknown.
-  // Backward: the lane holds the solution of the unknown it solved last.
+  // the lane holds the new pivot of its n0, valid until another lane touches that unknown;
+  // an idle round (sink step) overwrites it.  Backward: the lane holds the solution of the
+  // unknown it solved last; a round is flagged when every active lane's n0 is that unknown.
   t->fwd_carry = 0;
   int carry[TREE_CHAINS];
   for (int k = 0; k < TREE_CHAINS; ++k) carry[k] = -1;
@@ -263,7 +265,7 @@ bool tree_schedule(Tables *t) {
     if (all) t->fwd_carry |= 1ull << r;
     for (int k = 0; k < TREE_CHAINS; ++k) {
       const SolveStep &st = t->step[r][k];
-      if (st.c >= 0) carry[k] = st.n0;
+      carry[k] = st.c >= 0 ? st.n0 : -1;
       for (int q : {(int)st.c, (int)st.n0, (int)st.n1})  // touched by lane k: others' carries die
         for (int j = 0; j < TREE_CHAINS; ++j)
           if (j != k && q >= 0 && carry[j] == q) carry[j] = -1;
@@ -275,11 +277,10 @@ bool tree_schedule(Tables *t) {
     bool all = true;
     for (int k = 0; k < TREE_CHAINS; ++k) {
       const SolveStep &st = t->step[r][k];
-      if (st.c >= 0 && (st.n1 >= 0 || (st.n0 >= 0 && st.n0 != carry[k]))) all = false;
+      if (st.c >= 0 && (st.n0 < 0 || st.n0 != carry[k])) all = false;
     }
     if (all) t->bwd_carry |= 1ull << r;
-    for (int k = 0; k < TREE_CHAINS; ++k)
-      if (t->step[r][k].c >= 0) carry[k] = t->step[r][k].c;
+    for (int k = 0; k < TREE_CHAINS; ++k) carry[k] = t->step[r][k].c;
   }
   return true;
 }
@@ -374,11 +375,36 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   for (int i = 0; i < 9; ++i) { h.out_a[i] = t->out_a[i]; h.out_b[i] = t->out_b[i]; }
   h.len_nose0 = t->len[S_NOSE0]; h.Bw_ph0 = t->Bw[S_PHARYNX0]; h.Mw_ph0 = t->Mw[S_PHARYNX0];
   h.Kw_ph0 = t->Kw[S_PHARYNX0]; h.area_last_trachea = t->area[S_LAST_TRACHEA]; h.area_last_nose = t->area[S_LAST_NOSE];
+  // step records: LDS byte offsets of the tree kernel's utterance block (tree_core.h)
+  using namespace tree;
+  auto off = [](int slot) { return (uint16_t)(slot * 8); };
+  for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
+    for (int k = 0; k < TREE_CHAINS; ++k) {
+      const SolveStep &st = t->step[r][k];
+      const bool on = r < t->n_rounds && st.c >= 0;
+      StepRec &q = c.step[r][k];
+      q.c = off(X_DIAG + (on ? st.c : NODE_SINK));
+      q.n0 = off(X_DIAG + (on && st.n0 >= 0 ? st.n0 : NODE_SINK));
+      q.n1 = off(X_DIAG + (on && st.n1 >= 0 ? st.n1 : NODE_SINK));
+      q.e0 = off(X_OFF + (on && st.n0 >= 0 ? st.e0 : EDGE_ZERO));
+      q.e1 = off(X_OFF + (on && st.n1 >= 0 ? st.e1 : EDGE_ZERO));
+      q.e01 = off(X_OFF + (on && st.n0 >= 0 && st.n1 >= 0 ? st.e01 : EDGE_SINK));
+      q.un0 = off(X_U + (on && st.n0 >= 0 ? st.n0 : U_ZERO));
+      q.un1 = off(X_U + (on && st.n1 >= 0 ? st.n1 : U_ZERO));
+    }
+  // X_UR slots: both outputs of every bifurcation (their partner reads d/dt of the flow)
+  std::memset(c.ur_slot, -1, sizeof c.ur_slot);
+  int nur = 0;
+  for (int s = 0; s < NS; ++s)
+    if (t->cout0[s] >= 0 && t->cout1[s] >= 0) {
+      if (nur + 2 > NUR) { t->n_rounds = -1; break; }
+      c.ur_slot[t->cout0[s]] = (int8_t)nur++;
+      c.ur_slot[t->cout1[s]] = (int8_t)nur++;
+    }
   t->uni.n_rounds = t->n_rounds;
   t->uni.fwd_carry = t->fwd_carry;
   t->uni.bwd_carry = t->bwd_carry;
   t->uni.opt = t->opt;
-  std::memcpy(c.step, t->step, sizeof c.step);
   for (int s = 0; s < NS; ++s) {
     c.topo[s][TP_SRC] = (int8_t)t->src[s];
     c.topo[s][TP_OUT0] = (int8_t)t->cout0[s];

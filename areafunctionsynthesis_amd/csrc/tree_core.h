@@ -48,7 +48,8 @@ constexpr double THR = 0.001;  // MIN_DIPOLE_AMP (TdsModel.cpp:1611)
 // and alias the solver arrays, which are only live from the row phase on.
 // ---------------------------------------------------------------------------
 enum : int {
-  X_U = 0, X_UR = X_U + NC, X_UN = X_UR + NC,           // currents; 93..96 are persistent
+  // currents; X_U has two extra slots: U_SINK (idle / absent writes) and U_ZERO (0.0)
+  X_U = 0, X_UR = X_U + NC + 2, X_UN = X_UR + NUR,
   X_P4 = X_UN + NC,                                      // p[22], p[23], p[24], p[25]
   X_E = X_P4 + 4, X_D = X_E + NS,                        // per section
   X_L = X_D + NS, X_R1 = X_L + NDYNS, X_R0 = X_R1 + NDYNS, X_AREA = X_R0 + NDYNS,  // dynamic, s-23
@@ -59,7 +60,8 @@ enum : int {
   X_LEN = X_UNION, X_LAT = X_LEN + NPM, X_POS = X_LAT + NPM, X_TGT = X_POS + NPM,
   X_CUTN = X_TGT + NDIP, X_ACT = X_CUTN + NDIP, X_NOISE_END = X_ACT + NDIP,
   //   solver
-  X_DIAG = X_UNION, X_RHS = X_DIAG + NC, X_OFF = X_RHS + NC, X_SOLVE_END = X_OFF + TREE_NE,
+  //   (pivot / rhs with a sink slot at NC; edges with EDGE_ZERO and EDGE_SINK after TREE_NE)
+  X_DIAG = X_UNION, X_RHS = X_DIAG + NC + 2, X_OFF = X_RHS + NC + 2, X_SOLVE_END = X_OFF + TREE_NE + 2,
   X_AFTER = (X_NOISE_END > X_SOLVE_END ? X_NOISE_END : X_SOLVE_END),
   // frame-rate values written by lane 0 at every frame transition
   X_FRAME = X_AFTER,           // teethL, teethR, velL, velR, gL[6], gR[6]
@@ -83,6 +85,11 @@ enum : int {
   PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_COUNT
 };
 
+// Solver sink / zero slots (see StepRec).
+constexpr int NODE_SINK = NC, U_SINK = NC, U_ZERO = NC + 1, EDGE_ZERO = TREE_NE, EDGE_SINK = TREE_NE + 1;
+constexpr uint32_t RHS_DELTA = (uint32_t)(X_RHS - X_DIAG) * 8u;  // bytes from a pivot to its rhs
+constexpr uint32_t U_DELTA = (uint32_t)(X_DIAG - X_U) * 8u;      // bytes from a pivot to its solution
+
 template <int W>
 struct Shape {
   static constexpr int ND = (NDYNS + W - 1) / W;
@@ -103,14 +110,10 @@ AFS_HD inline int static_section(int W, int j, int gl) {
 // Solver chain lane registers: the next step (prefetched) and the unknown this lane updated
 // last together with its new pivot / right-hand side (forward) or solution (backward).
 struct SolveCarry {
-  uint64_t next;  // packed SolveStep
-  double d, y;    // forward: pivot and rhs of the last n0; backward: y = last solution
+  StepRec cur, next;  // this round's step and the next (prefetched)
+  double d, y;        // forward: pivot and rhs of the last n0; backward: y = last solution
 };
 
-AFS_HD inline uint64_t load_step(const Consts &C, int r, int k) {
-  return *reinterpret_cast<const uint64_t *>(&C.step[r][k]);
-}
-AFS_HD inline int step_field(uint64_t w, int i) { return (int)(int8_t)(uint8_t)(w >> (8 * i)); }
 
 // 1/d for the pivots: v_rcp_f64 and two Newton steps on the device (within an ulp of the
 // division, a fraction of its latency); plain division in the CPU emulator.
@@ -841,7 +844,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
     if (s == 0) Sx -= X[X_GP + 1];  // lung pressure source at section 0
     double m, rhs;
     if (br != -1) {
-      double uB = R.u[j], uBr = R.ur[j], uD = X[X_U + br], uDr = X[X_UR + br];
+      double uB = R.u[j], uBr = R.ur[j], uD = X[X_U + br], uDr = X[X_UR + C.ur_slot[br]];
       double F = LAB / (dt * TH) + RAB;
       double H = -(1.0 / (dt * TH)) * (LAB * uB + LA * uD) - (TH1 / TH) * (LAB * uBr + LA * uDr) + Sx;
       m = -EB - EA - F;
@@ -861,6 +864,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
     X[X_RHS + i] = -rhs;
     // edges of section s: (in, out0) = -E, (in, out1) = -E, (out0, out1) = E + L/(dt th) + R1
     const int e0 = C.topo[s][TP_E0], e1 = C.topo[s][TP_E1], e2 = C.topo[s][TP_E2];
+    if (gl == 0 && j == 0) X[X_OFF + EDGE_ZERO] = 0.0;  // the solver's zero edge (union slot)
     if (e0 >= 0) X[X_OFF + e0] = -EB;
     if (e1 >= 0) {
       X[X_OFF + e1] = -EB;
@@ -868,7 +872,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
     }
     if (s == S_LAST_MOUTH || s == S_LAST_NOSE) {  // radiation rows (TdsModel.cpp:1841-1911)
       const int rc = C.topo[s][TP_OUT0], lc = C.topo[s][TP_OUT1];
-      double uR = X[X_U + rc], uL = X[X_U + lc], uRr = X[X_UR + rc], uLr = X[X_UR + lc];
+      double uR = X[X_U + rc], uL = X[X_U + lc], uRr = X[X_UR + C.ur_slot[rc]], uLr = X[X_UR + C.ur_slot[lc]];
       R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
       R.rad_un[0] = X[X_UN + rc]; R.rad_un[1] = X[X_UN + lc];
       const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
@@ -894,68 +898,57 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
 // ---------------------------------------------------------------------------
 // Solver rounds (chain lanes 0..3).
 // ---------------------------------------------------------------------------
-// Forward round r of chain lane k.  Rounds touch disjoint unknowns (checked when the
-// schedule is built), so the pivot and right-hand side this lane wrote for n0 stay exact
-// until another lane touches that unknown; in the rounds flagged in U.fwd_carry every
-// active lane continues its chain with it from registers (a uniform branch), and all loads
-// of the neighbours are issued ahead of the reciprocal.
-AFS_HD inline void solve_forward(int k, int r, int n_rounds, bool carried, double *X, const Consts &C,
-                                 SolveCarry &cr) {
-  const uint64_t w = cr.next;
-  if (r + 1 < n_rounds) cr.next = load_step(C, r + 1, k);
-  const int c = step_field(w, 0);
-  if (c < 0) return;
-  const int n0 = step_field(w, 1), n1 = step_field(w, 2);
-  const int i0 = n0 < 0 ? 0 : n0, i1 = n1 < 0 ? 0 : n1;
-  const int e0 = step_field(w, 3), e1 = step_field(w, 4), e01 = step_field(w, 5);
-  double d0 = X[X_DIAG + i0], y0 = X[X_RHS + i0], a0 = X[X_OFF + (e0 < 0 ? 0 : e0)];
-  double d1 = X[X_DIAG + i1], y1 = X[X_RHS + i1], a1 = X[X_OFF + (e1 < 0 ? 0 : e1)];
-  const double a01 = X[X_OFF + (e01 < 0 ? 0 : e01)];
-  double d, y;
-  if (carried) { d = cr.d; y = cr.y; }
-  else { d = X[X_DIAG + c]; y = X[X_RHS + c]; }
-  const double inv = (d < 0.0) ? NAN : pivot_recip(d);  // the reference takes sqrt of a negative pivot
-  X[X_DIAG + c] = inv;  // X_RHS[c] already holds y (written back by whoever updated it last)
-  if (n0 >= 0) {
-    const double f0 = a0 * inv;
-    d0 -= f0 * a0;
-    y0 -= f0 * y;
-    X[X_DIAG + n0] = d0;
-    X[X_RHS + n0] = y0;
-    cr.d = d0; cr.y = y0;
-    if (n1 >= 0) {
-      const double f1 = a1 * inv;
-      d1 -= f1 * a1;
-      y1 -= f1 * y;
-      X[X_DIAG + n1] = d1;
-      X[X_RHS + n1] = y1;
-      X[X_OFF + e01] = a01 - f0 * a1;
-    }
-  }
+AFS_HD inline double &lds_at(double *X, uint32_t byte_off) {
+  return *reinterpret_cast<double *>(reinterpret_cast<char *>(X) + byte_off);
 }
 
-// Backward round r: x_c = (y_c - a0 x_n0 - a1 x_n1) / d_c.  In the rounds flagged in
-// U.bwd_carry, x_n0 is the solution this lane produced last (registers) and there is no n1.
+// Forward round of chain lane k: eliminate c, update n0 and n1 (the sink when absent) and
+// the edge n0-n1.  Rounds touch disjoint unknowns (checked when the schedule is built), so
+// the pivot and right-hand side this lane computes for n0 stay exact until another lane
+// touches that unknown: in the rounds of U.fwd_carry every active lane continues its chain
+// with them from registers (a uniform branch).  (Loading the next round's operands ahead
+// was measured slower: the extra live registers cost more than the latency they hide.)
+AFS_HD inline void solve_forward(int k, int r, bool carried, double *X, const Consts &C, SolveCarry &cr) {
+  const StepRec s = cr.cur;
+  cr.cur = cr.next;
+  cr.next = C.step[r + 2 < TREE_MAX_ROUNDS ? r + 2 : TREE_MAX_ROUNDS - 1][k];
+  double d0 = lds_at(X, s.n0), y0 = lds_at(X, s.n0 + RHS_DELTA);
+  const double d1 = lds_at(X, s.n1), y1 = lds_at(X, s.n1 + RHS_DELTA);
+  const double a0 = lds_at(X, s.e0), a1 = lds_at(X, s.e1), a01 = lds_at(X, s.e01);
+  double d, y;
+  if (carried) { d = cr.d; y = cr.y; }
+  else { d = lds_at(X, s.c); y = lds_at(X, s.c + RHS_DELTA); }
+  const double inv = (d < 0.0) ? NAN : pivot_recip(d);  // the reference takes sqrt of a negative pivot
+  lds_at(X, s.c) = inv;  // the rhs slot of c already holds y (written by whoever updated it last)
+  const double f0 = a0 * inv, f1 = a1 * inv;
+  d0 -= f0 * a0;
+  y0 -= f0 * y;
+  lds_at(X, s.n0) = d0;
+  lds_at(X, s.n0 + RHS_DELTA) = y0;
+  cr.d = d0;
+  cr.y = y0;
+  lds_at(X, s.n1) = d1 - f1 * a1;
+  lds_at(X, s.n1 + RHS_DELTA) = y1 - f1 * y;
+  lds_at(X, s.e01) = a01 - f0 * a1;
+}
+
+// Backward round (descending): x_c = (y_c - a0 x_n0 - a1 x_n1) / d_c (absent neighbours read
+// a zero edge and a zero solution).  In the rounds of U.bwd_carry x_n0 is the solution this
+// lane produced last (registers).
 AFS_HD inline void solve_backward(int k, int r, bool carried, double *X, const Consts &C, SolveCarry &cr) {
-  const uint64_t w = cr.next;
-  if (r > 0) cr.next = load_step(C, r - 1, k);
-  const int c = step_field(w, 0);
-  if (c < 0) return;
-  const int n0 = step_field(w, 1), n1 = step_field(w, 2);
-  const int e0 = step_field(w, 3), e1 = step_field(w, 4);
-  double y = X[X_RHS + c];
-  const double inv = X[X_DIAG + c];
-  const double a0 = X[X_OFF + (e0 < 0 ? 0 : e0)];
-  if (carried) {
-    if (n0 >= 0) y -= a0 * cr.y;
-  } else {
-    const double a1 = X[X_OFF + (e1 < 0 ? 0 : e1)];
-    const double x0 = X[X_U + (n0 < 0 ? 0 : n0)], x1 = X[X_U + (n1 < 0 ? 0 : n1)];
-    if (n0 >= 0) y -= a0 * x0;
-    if (n1 >= 0) y -= a1 * x1;
-  }
+  const StepRec s = cr.cur;
+  cr.cur = cr.next;
+  cr.next = C.step[r >= 2 ? r - 2 : 0][k];
+  double y = lds_at(X, s.c + RHS_DELTA);
+  const double inv = lds_at(X, s.c);
+  const double a0 = lds_at(X, s.e0), a1 = lds_at(X, s.e1), x1 = lds_at(X, s.un1);
+  double x0;
+  if (carried) x0 = cr.y;
+  else x0 = lds_at(X, s.un0);
+  y -= a0 * x0;
+  y -= a1 * x1;
   const double xc = y * inv;
-  X[X_U + c] = xc;
+  lds_at(X, s.c - U_DELTA) = xc;
   cr.y = xc;
 }
 
@@ -978,7 +971,7 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
     R.u[j] = unew;
     R.ur[j] = (unew - uold) / (dt * TH) - (TH1 / TH) * R.ur[j];
     R.un[j] = (1.0 - c) * unew + c * R.un[j];
-    X[X_UR + s] = R.ur[j];
+    if (C.ur_slot[s] >= 0) X[X_UR + C.ur_slot[s]] = R.ur[j];
     X[X_UN + s] = R.un[j];
     double cin = 0.0;
     cin += unew;
@@ -1004,7 +997,7 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
         const int rc = q == 0 ? o0 : o1;
         double un = X[X_U + rc];
         double ur = (un - R.rad_u[q]) / (dt * TH) - (TH1 / TH) * R.rad_ur[q];
-        X[X_UR + rc] = ur;
+        X[X_UR + C.ur_slot[rc]] = ur;
         X[X_UN + rc] = (1.0 - c) * un + c * R.rad_un[q];
       }
     }
@@ -1058,14 +1051,22 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.sync();
   x.mark(PH_ROWS);
   const int nr = U.n_rounds;
-  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { R.sc.next = load_step(C, 0, k); });
+  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) {
+    R.sc.cur = C.step[0][k];
+    R.sc.next = C.step[1][k];
+    R.sc.d = R.sc.y = 0.0;
+  });
   for (int r = 0; r < nr; ++r) {
     const bool carried = (U.fwd_carry >> r) & 1;
-    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { solve_forward(k, r, nr, carried, X, C, R.sc); });
+    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { solve_forward(k, r, carried, X, C, R.sc); });
     x.sync();
   }
   x.mark(PH_FORWARD);
-  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { R.sc.next = load_step(C, nr - 1, k); });
+  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) {
+    R.sc.cur = C.step[nr - 1][k];
+    R.sc.next = C.step[nr >= 2 ? nr - 2 : 0][k];
+    R.sc.y = 0.0;
+  });
   for (int r = nr - 1; r >= 0; --r) {
     const bool carried = (U.bwd_carry >> r) & 1;
     x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { solve_backward(k, r, carried, X, C, R.sc); });

@@ -28,7 +28,7 @@ def main():
     w = getattr(workloads, args.workload)(args.batch, seconds=args.seconds, fs=44100.0)
     frames = workloads.build_frames(w, ctx.af_to_frames)
     ctx.close()
-    lib = ctypes.CDLL(os.path.join(HERE, "libphase_prof.so"))
+    lib = ctypes.CDLL(os.path.join(HERE, os.environ.get("PP_LIB", "libphase_prof.so")))
     n = lib.pp_phase_count()
     cyc = (ctypes.c_uint64 * n)()
     ms = ctypes.c_double()
@@ -38,7 +38,7 @@ def main():
         raise SystemExit("pp_run failed")
     T = w.samples_per_utterance
     tot = sum(cyc)
-    print(f"{args.workload} B={w.batch} T={T} waves={waves} kernel {ms.value:.2f} ms "
+    print(f"[{os.environ.get('PP_LIB', 'libphase_prof.so')}] {args.workload} B={w.batch} T={T} waves={waves} kernel {ms.value:.2f} ms "
           f"({w.batch * T / ms.value * 1e3 / 1e6:.2f} M samples/s)")
     for p in range(n):
         print(f"  {PHASES[p]:14s} {cyc[p] / waves / T:10.1f} clk/sample  {100 * cyc[p] / tot:5.1f} %")
