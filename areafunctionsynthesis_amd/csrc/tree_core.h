@@ -73,8 +73,8 @@ enum : int {
   X_PREVFLOW = X_OUTF + 16,
   X_NONFIN = X_PREVFLOW + 1,
   X_ART = X_NONFIN + 1,        // 40 articulator bytes
-  X_RNG = X_ART + 5,           // rand() ring: 64 u32 values, head position, pending count (33 doubles)
-  X_GP = X_RNG + 33,           // interpolated glottis controls (6) and teeth position (lane 0)
+  X_RNG = X_ART + 5,           // rand(): value ring, prefix-sum ring (64 u32 each), head, pending (65 doubles)
+  X_GP = X_RNG + 65,           // interpolated glottis controls (6) and teeth position (lane 0)
   X_TOTAL = X_GP + 8
 };
 
@@ -144,6 +144,7 @@ struct Lane {
   double sample;                                                     // lane 0
   int art[S::ND];
   uint32_t racc[S::NDP];                                             // rand() sums of owned dipoles
+  uint32_t rtmp[3];                                                  // rand() block scratch
   SolveCarry sc;                                                     // chain lanes, during the solve
 };
 
@@ -153,6 +154,9 @@ struct Lane {
 //   x.min_index(f)  -> the smallest MinIdx::v of f(gl, R), ties to the smallest index
 //   x.max_value(f)  -> the largest f(gl, R) under strict ">" (a NaN never wins)
 struct MinIdx { double v; int i; };
+// x.scan_add<N>(f, g): f(gl, R) -> U4; inclusive prefix sums (mod 2^32) of the first N
+// components over lanes 0..gl are handed to g(gl, R, sums).
+struct U4 { uint32_t v[4]; };
 AFS_HD inline MinIdx min_idx_combine(MinIdx a, MinIdx b) {
   return (b.v < a.v || (b.v == a.v && b.i < a.i)) ? b : a;
 }
@@ -254,34 +258,25 @@ AFS_HD inline void rng_seed(int32_t *r, uint32_t seed) {
 }
 
 // The rand() stream as a sequence r_i = r_{i-3} + r_{i-31} (mod 2^32), output r_i >> 1 --
-// glibc's TYPE_3 generator read in generation order.  The LDS ring holds the last 64
-// values (index = sequence number mod 64); RNG_HEAD is the ring index of the next value to
-// generate and RNG_PEND how many generated values have not been drawn yet (< 31).
-constexpr int RNG_RING = 64, RNG_HEAD = 64, RNG_PEND = 65, RNG_BLOCK = 31;
+// glibc's TYPE_3 generator read in generation order.  The LDS block holds the last 64
+// values (RNG_R, index = sequence number mod 64), the inclusive prefix sums of the outputs
+// S_i = sum_{i' <= i} (r_i' >> 1) (RNG_S, same indexing; sums of draws are differences of
+// two of them), RNG_HEAD = ring index of the next value to generate and RNG_PEND = how many
+// generated values have not been drawn yet (< one block).
+constexpr int RNG_RING = 64, RNG_R = 0, RNG_S = 64, RNG_HEAD = 128, RNG_PEND = 129;
+// values per generation block: 3 residue chains x min(W, 10) lanes (<= 30 keeps every
+// term of the block in the 31-value history)
+template <int W> constexpr int rng_lanes() { return W < 10 ? W : 10; }
 
 // Ring after srand(seed): the 31 most recent values in generation order at 0..30.
-AFS_HD inline void rng_ring_seed(uint32_t *ring, uint32_t seed) {
+AFS_HD inline void rng_ring_seed(uint32_t *g, uint32_t seed) {
   int32_t st[32];
   rng_seed(st, seed);
   const int f = st[31];  // glibc's fptr: the oldest value of the window
-  for (int j = 0; j < RNG_BLOCK; ++j) ring[j] = (uint32_t)st[(f + j) % 31];
-  for (int j = RNG_BLOCK; j < RNG_RING; ++j) ring[j] = 0;
-  ((int32_t *)ring)[RNG_HEAD] = RNG_BLOCK;
-  ((int32_t *)ring)[RNG_PEND] = 0;
-}
-
-// Value k (0..30) of the next block, straight from the 31-value history: unrolling the lag-3
-// term gives r_{h+k} = r_{h+k-3(m+1)} + sum_{j<=m} r_{h+k-31-3j}, m = k / 3.
-AFS_HD inline uint32_t rng_block_value(const uint32_t *ring, int head, int k) {
-  const int m = k / 3;
-  uint32_t v = ring[(head + k - 3 * (m + 1)) & (RNG_RING - 1)];
-  // fixed trip count, every load issued: the compiler batches them before one wait
-#pragma unroll
-  for (int j = 0; j <= RNG_BLOCK / 3; ++j) {
-    const uint32_t t = ring[(head + k - RNG_BLOCK - 3 * j) & (RNG_RING - 1)];
-    v += (j <= m) ? t : 0u;
-  }
-  return v;
+  for (int j = 0; j < RNG_S + RNG_RING; ++j) g[j] = 0;
+  for (int j = 0; j < 31; ++j) g[RNG_R + j] = (uint32_t)st[(f + j) % 31];
+  ((int32_t *)g)[RNG_HEAD] = 31;  // S[30] = 0 is the base of the prefix sums
+  ((int32_t *)g)[RNG_PEND] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -696,9 +691,10 @@ AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Con
 
 // Phase N: noise sources (TdsModel.cpp:1630-1708).  Amplitude smoothing of the owned
 // dipoles, then the rand() draws: source d, the q-th active one in source order, takes
-// draws 12q .. 12q+11 of this sample, and the 16 lanes generate the stream 31 values at a
-// time (rng_block_value) instead of one draw after another.  Then the one-pole shaping
-// filter of the owned active dipoles.
+// draws 12q .. 12q+11 of this sample; the lanes generate the stream 30 values at a time
+// (lane scans instead of one draw after another) and each source's sum of 12 draws is a
+// difference of two output prefix sums.  Then the one-pole shaping filter of the owned
+// active dipoles.
 template <int W, class Xc>
 AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
@@ -730,12 +726,11 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
     });
     return;
   }
-  uint32_t *ring = (uint32_t *)(X + X_RNG);
-  const int32_t *ctl = (const int32_t *)ring;
-  const int head0 = ctl[RNG_HEAD], pend = ctl[RNG_PEND];
+  uint32_t *g = (uint32_t *)(X + X_RNG);
+  const int head0 = ((const int32_t *)g)[RNG_HEAD], pend = ((const int32_t *)g)[RNG_PEND];
   const int base = head0 - pend;  // ring index of this sample's first draw
   const int need = 12 * __builtin_popcountll(act);
-  // draws [lo, hi) of this sample are in the ring: add them to the owners' sums
+  // draws [lo, hi) of this sample are generated: add their share to the owners' sums
   auto consume = [&](int lo, int hi) {
     x.par([&](int gl, Lane<W> &R) {
 #pragma unroll
@@ -743,31 +738,52 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
         const int d = gl + k * W;
         if (d >= NDIP || !((act >> d) & 1)) continue;
         const int q0 = 12 * __builtin_popcountll(act & ((1ull << d) - 1));
-        uint32_t acc = R.racc[k];
-#pragma unroll
-        for (int t = 0; t < 12; ++t) {
-          const int pos = q0 + t;
-          const uint32_t v = ring[(base + pos) & (RNG_RING - 1)] >> 1;
-          acc += (pos >= lo && pos < hi) ? v : 0u;
-        }
-        R.racc[k] = acc;
+        const int a = q0 > lo ? q0 : lo, b = q0 + 12 < hi ? q0 + 12 : hi;
+        if (a < b)
+          R.racc[k] += g[RNG_S + ((base + b - 1) & (RNG_RING - 1))] - g[RNG_S + ((base + a - 1) & (RNG_RING - 1))];
       }
     });
   };
   int avail = pend;
   if (avail > 0) consume(0, avail);
   int head = head0;
+  constexpr int RJ = rng_lanes<W>(), RNG_BLOCK = 3 * RJ;
   while (avail < need) {
-    // The new block lands at ring indices head..head+30, at least 33 away from the history
-    // head-31..head-1 it is computed from (mod 64), so it can be stored as it is computed.
-    x.par([&](int gl, Lane<W> &R) {
-      (void)R;
-#pragma unroll
-      for (int i = 0; i < (RNG_BLOCK + W - 1) / W; ++i) {
-        const int k = gl + i * W;
-        if (k < RNG_BLOCK) ring[(head + k) & (RNG_RING - 1)] = rng_block_value(ring, head, k);
-      }
-    });
+    // Block of 3 RJ values = the next 10 of each residue chain c (i = head + 3j + c):
+    // r_{head+3j+c} = r_{head+c-3} + sum_{t<=j} r_{head+3t+c-31}, an inclusive prefix sum
+    // over the lanes j = 0..9 of history values.
+    const uint32_t b0 = g[RNG_R + ((head - 3) & (RNG_RING - 1))], b1 = g[RNG_R + ((head - 2) & (RNG_RING - 1))],
+                   b2 = g[RNG_R + ((head - 1) & (RNG_RING - 1))], sb = g[RNG_S + ((head - 1) & (RNG_RING - 1))];
+    x.template scan_add<3>(
+        [&](int gl, Lane<W> &R) {
+          (void)R;
+          U4 v{{0u, 0u, 0u, 0u}};
+          if (gl < RJ)
+            for (int c = 0; c < 3; ++c) v.v[c] = g[RNG_R + ((head + 3 * gl + c - 31) & (RNG_RING - 1))];
+          return v;
+        },
+        [&](int gl, Lane<W> &R, const U4 &p) {
+          if (gl >= RJ) return;
+          const uint32_t n0 = b0 + p.v[0], n1 = b1 + p.v[1], n2 = b2 + p.v[2];
+          g[RNG_R + ((head + 3 * gl) & (RNG_RING - 1))] = n0;
+          g[RNG_R + ((head + 3 * gl + 1) & (RNG_RING - 1))] = n1;
+          g[RNG_R + ((head + 3 * gl + 2) & (RNG_RING - 1))] = n2;
+          R.rtmp[0] = n0 >> 1; R.rtmp[1] = n1 >> 1; R.rtmp[2] = n2 >> 1;
+        });
+    // prefix sums of the outputs in sequence order
+    x.template scan_add<1>(
+        [&](int gl, Lane<W> &R) {
+          U4 v{{0u, 0u, 0u, 0u}};
+          if (gl < RJ) v.v[0] = R.rtmp[0] + R.rtmp[1] + R.rtmp[2];
+          return v;
+        },
+        [&](int gl, Lane<W> &R, const U4 &p) {
+          if (gl >= RJ) return;
+          const uint32_t s2 = sb + p.v[0], s1 = s2 - R.rtmp[2], s0 = s1 - R.rtmp[1];
+          g[RNG_S + ((head + 3 * gl) & (RNG_RING - 1))] = s0;
+          g[RNG_S + ((head + 3 * gl + 1) & (RNG_RING - 1))] = s1;
+          g[RNG_S + ((head + 3 * gl + 2) & (RNG_RING - 1))] = s2;
+        });
     x.sync();
     consume(avail, avail + RNG_BLOCK);
     avail += RNG_BLOCK;
@@ -777,7 +793,7 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
   x.mark(PH_N_RNG);
   x.one([&](Lane<W> &R) {
     (void)R;
-    int32_t *c = (int32_t *)ring;
+    int32_t *c = (int32_t *)g;
     c[RNG_HEAD] = head;
     c[RNG_PEND] = avail - need;
   });

@@ -79,6 +79,26 @@ struct GpuExec {
     if constexpr (TW == 32) b = max_combine(b, xor16(b));
     return b;
   }
+  // Inclusive prefix sums over the utterance's lanes: row_shr 1, 2, 4, 8 with zero fill
+  // (bound_ctrl) inside the 16-lane row; for 32 lanes, lane 15 of the first row is added to
+  // the second (row_bcast15 into rows 1 and 3).
+  template <int CTRL> __device__ __forceinline__ static uint32_t shr(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+  }
+  template <int N, class F, class G> __device__ __forceinline__ void scan_add(F f, G g) {
+    U4 v = f(gl, *R);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      uint32_t x = v.v[i];
+      x += shr<0x111>(x);
+      x += shr<0x112>(x);
+      x += shr<0x114>(x);
+      x += shr<0x118>(x);
+      if constexpr (TW == 32) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+      v.v[i] = x;
+    }
+    g(gl, *R, v);
+  }
   __device__ __forceinline__ void mark(int ph) {
     if constexpr (PROF) {
       uint64_t t = __builtin_amdgcn_s_memtime();

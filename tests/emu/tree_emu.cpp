@@ -34,6 +34,16 @@ struct CpuExec {
     for (int gl = 1; gl < W; ++gl) b = min_idx_combine(b, f(gl, R[gl]));
     return b;
   }
+  template <int N, class F, class G> void scan_add(F f, G g) {
+    std::vector<U4> out(W);
+    U4 acc{{0u, 0u, 0u, 0u}};
+    for (int gl = 0; gl < W; ++gl) {
+      const U4 v = f(gl, R[gl]);
+      for (int i = 0; i < N; ++i) acc.v[i] += v.v[i];
+      out[gl] = acc;
+    }
+    for (int gl = 0; gl < W; ++gl) g(gl, R[gl], out[gl]);
+  }
   template <class F> double max_value(F f) {
     double b = f(0, R[0]);
     for (int gl = 1; gl < W; ++gl) b = max_combine(b, f(gl, R[gl]));
