@@ -924,16 +924,15 @@ AFS_HD inline double &lds_at(double *X, uint32_t byte_off) {
 // touches that unknown: in the rounds of U.fwd_carry every active lane continues its chain
 // with them from registers (a uniform branch).  (Loading the next round's operands ahead
 // was measured slower: the extra live registers cost more than the latency they hide.)
-AFS_HD inline void solve_forward(int k, int r, bool carried, double *X, const Consts &C, SolveCarry &cr) {
-  const StepRec s = cr.cur;
-  cr.cur = cr.next;
-  cr.next = C.step[r + 2 < TREE_MAX_ROUNDS ? r + 2 : TREE_MAX_ROUNDS - 1][k];
+// The round body, instantiated separately for a pivot from registers and from LDS so that
+// the reciprocal of a carried pivot does not wait for the neighbours' loads.
+template <bool CARRIED>
+AFS_HD inline void forward_body(const StepRec &s, double *X, SolveCarry &cr) {
   double d0 = lds_at(X, s.n0), y0 = lds_at(X, s.n0 + RHS_DELTA);
   const double d1 = lds_at(X, s.n1), y1 = lds_at(X, s.n1 + RHS_DELTA);
   const double a0 = lds_at(X, s.e0), a1 = lds_at(X, s.e1), a01 = lds_at(X, s.e01);
-  double d, y;
-  if (carried) { d = cr.d; y = cr.y; }
-  else { d = lds_at(X, s.c); y = lds_at(X, s.c + RHS_DELTA); }
+  const double d = CARRIED ? cr.d : lds_at(X, s.c);
+  const double y = CARRIED ? cr.y : lds_at(X, s.c + RHS_DELTA);
   const double inv = (d < 0.0) ? NAN : pivot_recip(d);  // the reference takes sqrt of a negative pivot
   lds_at(X, s.c) = inv;  // the rhs slot of c already holds y (written by whoever updated it last)
   const double f0 = a0 * inv, f1 = a1 * inv;
@@ -948,24 +947,36 @@ AFS_HD inline void solve_forward(int k, int r, bool carried, double *X, const Co
   lds_at(X, s.e01) = a01 - f0 * a1;
 }
 
+AFS_HD inline void solve_forward(int k, int r, bool carried, double *X, const Consts &C, SolveCarry &cr) {
+  const StepRec s = cr.cur;
+  cr.cur = cr.next;
+  cr.next = C.step[r + 2 < TREE_MAX_ROUNDS ? r + 2 : TREE_MAX_ROUNDS - 1][k];
+  if (carried) forward_body<true>(s, X, cr);
+  else forward_body<false>(s, X, cr);
+}
+
 // Backward round (descending): x_c = (y_c - a0 x_n0 - a1 x_n1) / d_c (absent neighbours read
 // a zero edge and a zero solution).  In the rounds of U.bwd_carry x_n0 is the solution this
 // lane produced last (registers).
-AFS_HD inline void solve_backward(int k, int r, bool carried, double *X, const Consts &C, SolveCarry &cr) {
-  const StepRec s = cr.cur;
-  cr.cur = cr.next;
-  cr.next = C.step[r >= 2 ? r - 2 : 0][k];
+template <bool CARRIED>
+AFS_HD inline void backward_body(const StepRec &s, double *X, SolveCarry &cr) {
   double y = lds_at(X, s.c + RHS_DELTA);
   const double inv = lds_at(X, s.c);
   const double a0 = lds_at(X, s.e0), a1 = lds_at(X, s.e1), x1 = lds_at(X, s.un1);
-  double x0;
-  if (carried) x0 = cr.y;
-  else x0 = lds_at(X, s.un0);
+  const double x0 = CARRIED ? cr.y : lds_at(X, s.un0);
   y -= a0 * x0;
   y -= a1 * x1;
   const double xc = y * inv;
   lds_at(X, s.c - U_DELTA) = xc;
   cr.y = xc;
+}
+
+AFS_HD inline void solve_backward(int k, int r, bool carried, double *X, const Consts &C, SolveCarry &cr) {
+  const StepRec s = cr.cur;
+  cr.cur = cr.next;
+  cr.next = C.step[r >= 2 ? r - 2 : 0][k];
+  if (carried) backward_body<true>(s, X, cr);
+  else backward_body<false>(s, X, cr);
 }
 
 // ---------------------------------------------------------------------------
