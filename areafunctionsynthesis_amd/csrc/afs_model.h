@@ -91,6 +91,7 @@ struct Hot {
   double fs, dt, dtTH1, noise_amp_F, noise_lp_c, noise_x_2000, sqrt12, nose4_area, fossa_R0;
   double rrad_num, lrad_num, tone_a[5], tone_b[5], out_a[9], out_b[9];
   double len_nose0, Bw_ph0, Mw_ph0, Kw_ph0, area_last_trachea, area_last_nose;
+  double inv_dtTH, inv_dt2TH2;  // 1 / (dt theta), 1 / (dt theta)^2
 };
 // Values that steer branches in the time loop: kernel arguments on the device, so the
 // compiler keeps them in scalar registers and branches on them uniformly.

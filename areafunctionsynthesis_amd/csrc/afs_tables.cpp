@@ -375,6 +375,8 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   for (int i = 0; i < 9; ++i) { h.out_a[i] = t->out_a[i]; h.out_b[i] = t->out_b[i]; }
   h.len_nose0 = t->len[S_NOSE0]; h.Bw_ph0 = t->Bw[S_PHARYNX0]; h.Mw_ph0 = t->Mw[S_PHARYNX0];
   h.Kw_ph0 = t->Kw[S_PHARYNX0]; h.area_last_trachea = t->area[S_LAST_TRACHEA]; h.area_last_nose = t->area[S_LAST_NOSE];
+  h.inv_dtTH = 1.0 / (t->dt * TH);
+  h.inv_dt2TH2 = 1.0 / (t->dt * t->dt * TH * TH);
   // step records: LDS byte offsets of the tree kernel's utterance block (tree_core.h)
   using namespace tree;
   auto off = [](int slot) { return (uint16_t)(slot * 8); };

@@ -85,6 +85,13 @@ enum : int {
   PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_COUNT
 };
 
+// Keeps the loads above it from being interleaved with the arithmetic below it (device).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define AFS_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define AFS_SCHED_BARRIER() ((void)0)
+#endif
+
 // Solver sink / zero slots (see StepRec).
 constexpr int NODE_SINK = NC, U_SINK = NC, U_ZERO = NC + 1, EDGE_ZERO = TREE_NE, EDGE_SINK = TREE_NE + 1;
 constexpr uint32_t RHS_DELTA = (uint32_t)(X_RHS - X_DIAG) * 8u;  // bytes from a pivot to its rhs
@@ -430,7 +437,7 @@ template <int W>
 AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
   const afs_options &opt = U.opt;
-  const double dt = C.h.dt;
+  const double dt = C.h.dt, idt = C.h.inv_dtTH, idt2 = C.h.inv_dt2TH2;
 #pragma unroll
   for (int j = 0; j < S::NST; ++j) {
     const int jj = S::ND + j;
@@ -448,22 +455,27 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     const bool glot = (s == S_GLOT_LO || s == S_GLOT_UP);
     const double area = X[X_AREA + s - DYN0];
     const double len = glot ? X[X_GLEN + s - DYN0] : (s <= S_LAST_MOUTH ? X[X_LEN + s - S_PHARYNX0] : C.h.len_nose0);
+    // prepareTimeStep's section quantities (TdsModel.cpp:732-834), with the repeated
+    // divisions folded into one reciprocal of the area and one of the wall surface.
     const double vol = area * len;
+    const double inv_area = 1.0 / area;
     double alpha = 0.0, beta = 0.0;
-    double circ = 2.0 * sqrt(area * PI);
-    double a = sqrt(area / PI), b = a;
-    double rmin = glot ? 0.8 : 1.6;
-    if (a < rmin) { a = rmin; b = area / (PI * a); }
-    const double L = (RHO * 0.5 * len) / area;
-    const double Cc = vol / (RHO * CSND * CSND);
+    const double r0 = sqrt(area * (1.0 / PI));
+    const double circ = 2.0 * PI * r0;
+    double a = r0, b = r0;
+    const double rmin = glot ? 0.8 : 1.6;
+    if (a < rmin) { a = rmin; b = area * (glot ? 1.0 / (PI * 0.8) : 1.0 / (PI * 1.6)); }
+    const double L = (RHO * 0.5 * len) * inv_area;
+    const double Cc = vol * (1.0 / (RHO * CSND * CSND));
     const double Rr = ((2.0 * MU * len) * (a * a + b * b)) / (PI * a * a * a * b * b * b);
     if (opt.soft_walls && !glot) {
       double surf = circ * len;
       if (surf < AMIN) surf = AMIN;
-      double Rw = C.h.Bw_ph0 / surf, Lw = C.h.Mw_ph0 / surf, Cw = surf / C.h.Kw_ph0;
-      alpha = 1.0 / (Lw / (dt * dt * TH * TH) + Rw / (dt * TH) + 1.0 / Cw);
-      beta = alpha * (R.w[j] * (Lw / (dt * dt * TH * TH) + Rw / (dt * TH)) +
-                      R.wr[j] * (Lw * (TH1 / TH + 1.0) / (dt * TH) + Rw * (TH1 / TH)) +
+      const double inv_surf = 1.0 / surf;
+      double Rw = C.h.Bw_ph0 * inv_surf, Lw = C.h.Mw_ph0 * inv_surf;
+      alpha = 1.0 / (Lw * idt2 + Rw * idt + C.h.Kw_ph0 * inv_surf);
+      beta = alpha * (R.w[j] * (Lw * idt2 + Rw * idt) +
+                      R.wr[j] * (Lw * (TH1 / TH + 1.0) * idt + Rw * (TH1 / TH)) +
                       R.wr2[j] * Lw * (TH1 / TH));
     }
     const double E = dt * TH / (Cc + alpha);
@@ -474,13 +486,13 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
         double u = 0.0;
         u += X[X_U + s + 1];
         double Ai = X[X_AREA + s + 1 - DYN0];
-        if ((Ai < area && u > 0) || (Ai > area && u < 0)) R1 = R1 - u * 0.5 * RHO / (area * area);
+        if ((Ai < area && u > 0) || (Ai > area && u < 0)) R1 = R1 - u * (0.5 * RHO) * (inv_area * inv_area);
       }
       if (s > S_PHARYNX0 && s - 1 != S_PHARYNX0 + 3 && s - 1 != S_LAST_PHARYNX) {  // pair (s-1, s)
         double u = 0.0;
         u += R.u[j];
         double Aa = X[X_AREA + s - 1 - DYN0];
-        if ((area < Aa && u > 0) || (area > Aa && u < 0)) R0 = R0 + u * 0.5 * RHO / (area * area);
+        if ((area < Aa && u > 0) || (area > Aa && u < 0)) R0 = R0 + u * (0.5 * RHO) * (inv_area * inv_area);
       }
     }
     if (s == S_GLOT_LO) {  // glottal entrance and transition (TdsModel.cpp:912-950)
@@ -600,15 +612,22 @@ AFS_HD inline void dipole_targets(Xc &x, double *X, const Uni &U, const Consts &
 template <int W, class Xc>
 AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  // Section positions (Tube::calcPositions, Tube.cpp:611-622): every lane runs the same
-  // sequential sum and stores the positions of the sections it owns.
-  x.par([&](int gl, Lane<W> &R) {
+  // Section positions (Tube::calcPositions, Tube.cpp:611-622): one sequential sum, as in
+  // the reference (the comparisons against obstacle positions depend on its rounding).
+  x.one([&](Lane<W> &R) {
     (void)R;
     double p = 0.0;
 #pragma unroll
-    for (int m = 0; m < NPM; ++m) {
-      if ((m + 2) % W == gl) X[X_POS + m] = p;
-      p += X[X_LEN + m];
+    for (int m0 = 0; m0 < NPM; m0 += 8) {  // 8 loads in flight, then the sequential adds
+      double l[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) l[i] = X[X_LEN + m0 + i];
+      AFS_SCHED_BARRIER();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        X[X_POS + m0 + i] = p;
+        p += l[i];
+      }
     }
   });
   x.sync();
@@ -835,7 +854,7 @@ AFS_HD inline double sec_R1(const double *X, const Consts &C, int s) {
 template <int W>
 AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  const double dt = C.h.dt;
+  const double dt = C.h.dt, idt = C.h.inv_dtTH, idt2 = C.h.inv_dt2TH2;
   const afs_options &opt = U.opt;
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
@@ -861,16 +880,16 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
     double m, rhs;
     if (br != -1) {
       double uB = R.u[j], uBr = R.ur[j], uD = X[X_U + br], uDr = X[X_UR + C.ur_slot[br]];
-      double F = LAB / (dt * TH) + RAB;
-      double H = -(1.0 / (dt * TH)) * (LAB * uB + LA * uD) - (TH1 / TH) * (LAB * uBr + LA * uDr) + Sx;
+      double F = LAB * idt + RAB;
+      double H = -idt * (LAB * uB + LA * uD) - (TH1 / TH) * (LAB * uBr + LA * uDr) + Sx;
       m = -EB - EA - F;
       rhs = H + DB - DA;
     } else {
       double uu = R.u[j], uur = R.ur[j];
       if (opt.inner_length_corrections && a >= S_PHARYNX0 && s <= S_LAST_MOUTH)
         LAB += junction_l(X[X_AREA + a - DYN0], AB);
-      double G = LAB / (dt * TH) + RAB;
-      double H = -uur * LAB * (TH1 / TH) - (LAB * uu) / (dt * TH) + Sx;
+      double G = LAB * idt + RAB;
+      double H = -uur * LAB * (TH1 / TH) - (LAB * uu) * idt + Sx;
       m = -EB - G;
       if (a != -1) m -= EA;
       rhs = H + DB;
@@ -884,7 +903,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
     if (e0 >= 0) X[X_OFF + e0] = -EB;
     if (e1 >= 0) {
       X[X_OFF + e1] = -EB;
-      X[X_OFF + e2] = -(-EB - (LB / (dt * TH) + R1B));
+      X[X_OFF + e2] = -(-EB - (LB * idt + R1B));
     }
     if (s == S_LAST_MOUTH || s == S_LAST_NOSE) {  // radiation rows (TdsModel.cpp:1841-1911)
       const int rc = C.topo[s][TP_OUT0], lc = C.topo[s][TP_OUT1];
@@ -894,16 +913,16 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
       const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
       {
         double Rrad = C.h.rrad_num / (9.0 * PI * PI * AB);
-        double F = LA2 / (dt * TH) + RA2 + Rrad;
-        double H = -(LA2 / (dt * TH)) * (uR + uL) - (LA2 * (TH1 / TH)) * (uRr + uLr) + Sr;
+        double F = LA2 * idt + RA2 + Rrad;
+        double H = -(LA2 * idt) * (uR + uL) - (LA2 * (TH1 / TH)) * (uRr + uLr) + Sr;
         X[X_DIAG + rc] = -(-EB - F);
         X[X_RHS + rc] = -(H - DB);
       }
       {
         double Lrad = C.h.lrad_num / (3.0 * PI * sqrt(AB * PI));
         double LAB2 = LA2 + Lrad;
-        double G = LAB2 / (dt * TH) + RA2;
-        double H = -(1.0 / (dt * TH)) * (LA2 * uR + LAB2 * uL) - (TH1 / TH) * (LA2 * uRr + LAB2 * uLr) + Sr;
+        double G = LAB2 * idt + RA2;
+        double H = -idt * (LA2 * uR + LAB2 * uL) - (TH1 / TH) * (LA2 * uRr + LAB2 * uLr) + Sr;
         X[X_DIAG + lc] = -(-EB - G);
         X[X_RHS + lc] = -(H - DB);
       }
@@ -985,7 +1004,7 @@ AFS_HD inline void solve_backward(int k, int r, bool carried, double *X, const C
 template <int W>
 AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  const double dt = C.h.dt, c = C.h.noise_lp_c;
+  const double dt = C.h.dt, c = C.h.noise_lp_c, idt = C.h.inv_dtTH;
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const int s = slot_section<W>(j, gl);
@@ -996,7 +1015,7 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
     const double unew = X[X_U + s];
     const double uold = R.u[j];
     R.u[j] = unew;
-    R.ur[j] = (unew - uold) / (dt * TH) - (TH1 / TH) * R.ur[j];
+    R.ur[j] = (unew - uold) * idt - (TH1 / TH) * R.ur[j];
     R.un[j] = (1.0 - c) * unew + c * R.un[j];
     if (C.ur_slot[s] >= 0) X[X_UR + C.ur_slot[s]] = R.ur[j];
     X[X_UN + s] = R.un[j];
@@ -1010,20 +1029,20 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
     double old = R.p[j];
     double p = X[X_D + s] + X[X_E + s] * net;
     R.p[j] = p;
-    double prr = (p - old) / (dt * TH) - R.pr[j] * (TH1 / TH);
+    double prr = (p - old) * idt - R.pr[j] * (TH1 / TH);
     R.pr[j] = prr;
     double ow = R.w[j], owr = R.wr[j];
     double w = prr * alpha + beta;
     R.w[j] = w;
-    double wr = (w - ow) / (dt * TH) - owr * (TH1 / TH);
+    double wr = (w - ow) * idt - owr * (TH1 / TH);
     R.wr[j] = wr;
-    R.wr2[j] = (wr - owr) / (dt * TH) - R.wr2[j] * (TH1 / TH);
+    R.wr2[j] = (wr - owr) * idt - R.wr2[j] * (TH1 / TH);
     if (s >= S_LAST_TRACHEA && s <= S_PHARYNX0) X[X_P4 + s - S_LAST_TRACHEA] = p;
     if (s == S_LAST_MOUTH || s == S_LAST_NOSE) {  // the two radiation currents of this section
       for (int q = 0; q < 2; ++q) {
         const int rc = q == 0 ? o0 : o1;
         double un = X[X_U + rc];
-        double ur = (un - R.rad_u[q]) / (dt * TH) - (TH1 / TH) * R.rad_ur[q];
+        double ur = (un - R.rad_u[q]) * idt - (TH1 / TH) * R.rad_ur[q];
         X[X_UR + C.ur_slot[rc]] = ur;
         X[X_UN + rc] = (1.0 - c) * un + c * R.rad_un[q];
       }
