@@ -85,7 +85,12 @@ constexpr int NUR = 16;
 // per wave fits in LDS next to the four utterance blocks (tds_tree.hip).
 constexpr int NSTATIC = 47;  // static sections 0..22, 69..92 -> index s < 23 ? s : s - 46
 enum : int { ST_E, ST_ALPHA, ST_WC1, ST_WC2, ST_LW, ST_L, ST_R, ST_N };
-enum : int { TP_SRC, TP_OUT0, TP_OUT1, TP_E0, TP_E1, TP_E2, TP_N };
+// Per section s (= per current i = s flowing into it): source section of the current, the
+// other output current of that source (its bifurcation partner, -1: none) and that
+// partner's X_UR slot, the section's output currents and its edges.  8 bytes: one load.
+struct alignas(8) Topo {
+  int8_t src, br, urbr, out0, out1, e0, e1, e2;
+};
 // Scalars of the time loop (copies of Tables fields; see build_tables).
 struct Hot {
   double fs, dt, dtTH1, noise_amp_F, noise_lp_c, noise_x_2000, sqrt12, nose4_area, fossa_R0;
@@ -104,7 +109,7 @@ struct Consts {
   Hot h;
   StepRec step[TREE_MAX_ROUNDS][TREE_CHAINS];
   int8_t ur_slot[NC];  // X_UR slot of a current, -1: none
-  int8_t topo[NS][TP_N];
+  Topo topo[NS];
   double stat[NSTATIC][ST_N];
 };
 

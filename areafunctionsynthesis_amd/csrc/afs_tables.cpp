@@ -408,12 +408,21 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   t->uni.bwd_carry = t->bwd_carry;
   t->uni.opt = t->opt;
   for (int s = 0; s < NS; ++s) {
-    c.topo[s][TP_SRC] = (int8_t)t->src[s];
-    c.topo[s][TP_OUT0] = (int8_t)t->cout0[s];
-    c.topo[s][TP_OUT1] = (int8_t)t->cout1[s];
-    c.topo[s][TP_E0] = (int8_t)t->edge[s][0];
-    c.topo[s][TP_E1] = (int8_t)t->edge[s][1];
-    c.topo[s][TP_E2] = (int8_t)t->edge[s][2];
+    Topo &q = c.topo[s];
+    q.src = (int8_t)t->src[s];
+    q.br = -1;
+    q.urbr = -1;
+    const int a = t->src[s];
+    if (a >= 0) {
+      const int br = (t->cout0[a] == s) ? t->cout1[a] : t->cout0[a];
+      q.br = (int8_t)br;
+      if (br >= 0) q.urbr = c.ur_slot[br];
+    }
+    q.out0 = (int8_t)t->cout0[s];
+    q.out1 = (int8_t)t->cout1[s];
+    q.e0 = (int8_t)t->edge[s][0];
+    q.e1 = (int8_t)t->edge[s][1];
+    q.e2 = (int8_t)t->edge[s][2];
   }
   for (int k = 0; k < NSTATIC; ++k) {
     int s = k < 23 ? k : k + 46;

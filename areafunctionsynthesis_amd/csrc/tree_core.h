@@ -214,14 +214,16 @@ AFS_HD inline void glottis_open_close(const double *gp, double cord, double rel0
 }
 
 // getJunctionInductance (TdsModel.cpp:1745-1778)
+// (one reciprocal for b / a and H / b)
 AFS_HD inline double junction_l(double A1, double A2) {
   if (A1 < AMIN) A1 = AMIN;
   if (A2 < AMIN) A2 = AMIN;
   double a, b;
-  if (A1 > A2) { a = sqrt(A1 / PI); b = sqrt(A2 / PI); }
-  else { a = sqrt(A2 / PI); b = sqrt(A1 / PI); }
-  double H = 1.0 - b / a;
-  return 8.0 * RHO * H / (3.0 * PI * PI * b);
+  if (A1 > A2) { a = sqrt(A1 * (1.0 / PI)); b = sqrt(A2 * (1.0 / PI)); }
+  else { a = sqrt(A2 * (1.0 / PI)); b = sqrt(A1 * (1.0 / PI)); }
+  const double r = 1.0 / (a * b);
+  const double H = 1.0 - (b * b) * r;
+  return (8.0 * RHO / (3.0 * PI * PI)) * H * (a * r);
 }
 
 // IirFilter::getOutputSample on a shift-register state x[0..n-1], y[0..n-1] (newest first)
@@ -583,7 +585,8 @@ AFS_HD inline void dipole_targets(Xc &x, double *X, const Uni &U, const Consts &
   double A = X[X_AREA + c.narrow - DYN0];
   if (A < 0.1) A = 0.1;
   double flow = 0.0;
-  int o0 = C.topo[c.narrow][TP_OUT0], o1 = C.topo[c.narrow][TP_OUT1];
+  const Topo tn = C.topo[c.narrow];
+  const int o0 = tn.out0, o1 = tn.out1;
   if (o0 != -1) flow += X[X_UN + o0];
   if (o1 != -1) flow += X[X_UN + o1];
   if (flow < 0.0) flow = 0.0;
@@ -868,18 +871,18 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
     const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
     const double AB = dyn ? X[X_AREA + s - DYN0] : C.h.area_last_nose;  // static: only used by s = 83
     const double EB = X[X_E + s], DB = X[X_D + s];
-    const int a = C.topo[i][TP_SRC];
+    const Topo tp = C.topo[s];
+    const int a = tp.src;
     double LA = 0.0, RA = 0.0, EA = 0.0, DA = 0.0;
     if (a != -1) { LA = sec_L(X, C, a); RA = sec_R1(X, C, a); EA = X[X_E + a]; DA = X[X_D + a]; }
     double LAB = LA + LB, RAB = RA + RB;
-    int br = -1;
-    if (a != -1) br = (C.topo[a][TP_OUT0] == i) ? C.topo[a][TP_OUT1] : C.topo[a][TP_OUT0];
+    const int br = tp.br;  // the other output of the source section (bifurcations)
     double Sx = 0.0;
     if (s >= S_PHARYNX0 && s <= S_LAST_MOUTH) Sx -= X[X_SMP + s - S_PHARYNX0];
     if (s == 0) Sx -= X[X_GP + 1];  // lung pressure source at section 0
     double m, rhs;
     if (br != -1) {
-      double uB = R.u[j], uBr = R.ur[j], uD = X[X_U + br], uDr = X[X_UR + C.ur_slot[br]];
+      double uB = R.u[j], uBr = R.ur[j], uD = X[X_U + br], uDr = X[X_UR + tp.urbr];
       double F = LAB * idt + RAB;
       double H = -idt * (LAB * uB + LA * uD) - (TH1 / TH) * (LAB * uBr + LA * uDr) + Sx;
       m = -EB - EA - F;
@@ -898,7 +901,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
     X[X_DIAG + i] = -m;
     X[X_RHS + i] = -rhs;
     // edges of section s: (in, out0) = -E, (in, out1) = -E, (out0, out1) = E + L/(dt th) + R1
-    const int e0 = C.topo[s][TP_E0], e1 = C.topo[s][TP_E1], e2 = C.topo[s][TP_E2];
+    const int e0 = tp.e0, e1 = tp.e1, e2 = tp.e2;
     if (gl == 0 && j == 0) X[X_OFF + EDGE_ZERO] = 0.0;  // the solver's zero edge (union slot)
     if (e0 >= 0) X[X_OFF + e0] = -EB;
     if (e1 >= 0) {
@@ -906,7 +909,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
       X[X_OFF + e2] = -(-EB - (LB * idt + R1B));
     }
     if (s == S_LAST_MOUTH || s == S_LAST_NOSE) {  // radiation rows (TdsModel.cpp:1841-1911)
-      const int rc = C.topo[s][TP_OUT0], lc = C.topo[s][TP_OUT1];
+      const int rc = tp.out0, lc = tp.out1;
       double uR = X[X_U + rc], uL = X[X_U + lc], uRr = X[X_UR + C.ur_slot[rc]], uLr = X[X_UR + C.ur_slot[lc]];
       R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
       R.rad_un[0] = X[X_UN + rc]; R.rad_un[1] = X[X_UN + lc];
@@ -1022,7 +1025,8 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
     double cin = 0.0;
     cin += unew;
     double cout = 0.0;
-    const int o0 = C.topo[s][TP_OUT0], o1 = C.topo[s][TP_OUT1];
+    const Topo tu = C.topo[s];
+    const int o0 = tu.out0, o1 = tu.out1;
     if (o0 != -1) cout += X[X_U + o0];
     if (o1 != -1) cout += X[X_U + o1];
     double net = cin - cout;
