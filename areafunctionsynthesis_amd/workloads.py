@@ -14,7 +14,10 @@ kernel (``Context.af_to_frames``) or any other ``params -> frames`` function.
 * ``fricatives``     config 5: fricative shapes with the velum open 1.0 cm^2
   (the GUI's default port area, MainPage.cpp:127-131), so the noise sources and the
   nasal side branch are active.
-Utterance ``u`` is seeded ``u + 1`` (srand per utterance), independent of GPU count.
+Utterance ``u`` is seeded ``u + 1`` (srand per utterance) and draws its shape and
+glottis settings from its own generator (SeedSequence [build seed, u]), so a shard built
+with ``first_utterance`` holds exactly the rows of the full batch and the audio does not
+depend on the GPU count.
 """
 from __future__ import annotations
 
@@ -56,6 +59,19 @@ def _seeds(B: int, first: int) -> np.ndarray:
     return (np.arange(B, dtype=np.uint64) + 1 + first).astype(np.uint32)
 
 
+def _rows(seed: int, first: int, B: int, n_choices: int):
+    """Per-utterance draws: shape index, 16 N(0,1) jitters, U[0,1) x 2 (global index u)."""
+    pick = np.empty(B, np.int64)
+    jit = np.empty((B, 16))
+    uni = np.empty((B, 2))
+    for k in range(B):
+        g = np.random.default_rng([seed, first + k])
+        pick[k] = g.integers(0, n_choices)
+        jit[k] = g.standard_normal(16)
+        uni[k] = g.random(2)
+    return pick, jit, uni
+
+
 def static_vowels(B: int, seconds: float = 1.0, fs: float = 44100.0, frame_rate: float = 100.0,
                   first_utterance: int = 0, seed: int = BUILD_SEED) -> Workload:
     """Config 2/4 generator.  ``first_utterance`` offsets the per-utterance draws so a
@@ -64,12 +80,9 @@ def static_vowels(B: int, seconds: float = 1.0, fs: float = 44100.0, frame_rate:
     base = np.stack([shapes[v] for v in VOWELS])
     hop = int(round(fs / frame_rate))
     F = int(round(seconds * fs / hop)) + 1
-    rng = np.random.default_rng(seed)
-    total = first_utterance + B
-    pick = rng.integers(0, len(VOWELS), size=total)[first_utterance:]
-    jit = rng.standard_normal((total, 16))[first_utterance:]
-    f0 = rng.uniform(90.0, 180.0, size=total)[first_utterance:]
-    pl = rng.uniform(6000.0, 10000.0, size=total)[first_utterance:]
+    pick, jit, uni = _rows(seed, first_utterance, B, len(VOWELS))
+    f0 = 90.0 + 90.0 * uni[:, 0]
+    pl = 6000.0 + 4000.0 * uni[:, 1]
     p = clamp_monotonic(base[pick] * (1.0 + 0.02 * jit))
     params = np.repeat(p[:, None, :], F, axis=1)
     glottis = np.zeros((B, F, 6))
@@ -88,11 +101,8 @@ def fricatives(B: int, seconds: float = 1.0, fs: float = 44100.0, frame_rate: fl
     base = np.stack([shapes[v] for v in FRICATIVES])
     hop = int(round(fs / frame_rate))
     F = int(round(seconds * fs / hop)) + 1
-    rng = np.random.default_rng(seed)
-    total = first_utterance + B
-    pick = rng.integers(0, len(FRICATIVES), size=total)[first_utterance:]
-    jit = rng.standard_normal((total, 16))[first_utterance:]
-    f0 = rng.uniform(90.0, 180.0, size=total)[first_utterance:]
+    pick, jit, uni = _rows(seed, first_utterance, B, len(FRICATIVES))
+    f0 = 90.0 + 90.0 * uni[:, 0]
     p = clamp_monotonic(base[pick] * (1.0 + 0.02 * jit))
     params = np.repeat(p[:, None, :], F, axis=1)
     glottis = np.zeros((B, F, 6))
@@ -121,10 +131,8 @@ def vcv(B: int, fs: float = 44100.0, frame_rate: float = 100.0, first_utterance:
                      transition[2], stationary[3]])
     total_s = float(bnd[-1])
     F = int(math.floor(total_s * fs / hop)) + 1
-    rng = np.random.default_rng(seed)
-    total = first_utterance + B
-    vi = rng.integers(0, len(vowels), size=total)[first_utterance:]
-    ci = rng.integers(0, len(cons), size=total)[first_utterance:]
+    pick, _, _ = _rows(seed, first_utterance, B, len(vowels) * len(cons))
+    vi, ci = pick // len(cons), pick % len(cons)
     f0s = (100.0, 115.0, 105.0, 80.0)  # Synthesizer.cpp:1311
     P = 8000.0
     params = np.zeros((B, F, 16))

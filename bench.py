@@ -100,6 +100,7 @@ def main() -> None:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    from areafunctionsynthesis_amd import sharding
     from areafunctionsynthesis_amd.frames import FRAME_DTYPE
     from areafunctionsynthesis_amd.synthesizer import Context
     from areafunctionsynthesis_amd.workloads import build_frames, static_vowels
@@ -109,23 +110,20 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
 
-    w = static_vowels(B, seconds=args.seconds, fs=args.fs, first_utterance=rank * B)
+    first, _ = sharding.shard_range(rank, world, B)
+    w = static_vowels(B, seconds=args.seconds, fs=args.fs, first_utterance=first)
     frames = build_frames(w, ctx.af_to_frames)
     F, hop, T = w.num_frames, w.hop, w.samples_per_utterance
     frames_dev = torch.from_numpy(frames.view(np.uint8).reshape(B, F, FRAME_DTYPE.itemsize)).to(dev)
     seeds_dev = torch.from_numpy(w.seeds.astype(np.int32)).to(dev)
     out_dev = torch.empty((B, T), dtype=torch.float64, device=dev)
-    gather_list = None
-    if world > 1 and rank == 0:
-        gather_list = [torch.empty_like(out_dev) for _ in range(world)]
 
     max_launch_samples = 65536 if args.solver == "tree" else 8192
     launches_per_step = -(-(F - 1) // max(1, max_launch_samples // hop))
 
     def step():
         ctx.synthesize(frames_dev, hop, seeds=seeds_dev, out=out_dev)
-        if world > 1:
-            dist.gather(out_dev, gather_list=gather_list, dst=0)
+        sharding.gather_to_rank0(out_dev, world, rank, dist)
 
     for _ in range(args.warmup):
         step()
@@ -140,8 +138,7 @@ def main() -> None:
         ev[k][0].record(stream)
         ctx.synthesize(frames_dev, hop, seeds=seeds_dev, out=out_dev)
         ev[k][1].record(stream)
-        if world > 1:
-            dist.gather(out_dev, gather_list=gather_list, dst=0)
+        sharding.gather_to_rank0(out_dev, world, rank, dist)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

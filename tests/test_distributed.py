@@ -1,0 +1,75 @@
+"""Multi-process path of bench.py on CPU (gloo, world size 2): shards cover the batch
+exactly once, rank-local workloads equal the rows of the full batch, seeds are the global
+u + 1, and the gather reassembles the audio in utterance order.  The GPU synthesis is
+replaced by a deterministic stand-in of the same shape (no GPU here)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from areafunctionsynthesis_amd import sharding, workloads
+
+B, SECONDS, FS = 6, 0.03, 44100.0
+
+
+def _standin(w) -> torch.Tensor:
+    """[B, T] float64 that depends on every row's parameters, glottis and seed."""
+    T = w.samples_per_utterance
+    base = w.params[:, 0, :].sum(axis=1) + w.glottis[:, 0, 0] * 1e-3 + w.seeds.astype(np.float64) * 1e-6
+    return torch.from_numpy(base[:, None] + np.arange(T)[None, :] * 1e-9)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, n = sharding.shard_range(rank, world, B)
+    w = workloads.static_vowels(n, seconds=SECONDS, fs=FS, first_utterance=first)
+    out = _standin(w)
+    got = sharding.gather_to_rank0(out, world, rank, dist)
+    t = torch.tensor([float(out.numel())], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks timing reduction
+    if rank == 0:
+        q.put((torch.cat(got).numpy(), w.seeds.copy(), float(t.item())))
+    else:
+        q.put(("seeds", w.seeds.copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_range():
+    assert sharding.shard_range(0, 2, 5) == (0, 5)
+    assert sharding.shard_range(1, 2, 5) == (5, 5)
+    with pytest.raises(ValueError):
+        sharding.shard_range(2, 2, 5)
+
+
+def test_gloo_world2_gather_matches_single_process():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    gathered = next(r for r in res if not isinstance(r[0], str))
+    audio, seeds0, numel = gathered
+    seeds1 = next(r[1] for r in res if isinstance(r[0], str))
+    full = workloads.static_vowels(world * B, seconds=SECONDS, fs=FS)
+    assert np.array_equal(audio, _standin(full).numpy())
+    assert np.array_equal(np.concatenate([seeds0, seeds1]), np.arange(1, world * B + 1, dtype=np.uint32))
+    assert numel == B * full.samples_per_utterance
