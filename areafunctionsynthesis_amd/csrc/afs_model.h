@@ -59,16 +59,18 @@ AFS_HD constexpr bool is_static_section(int s) {
   return s <= S_LAST_TRACHEA || (s >= S_NOSE0 + 4);
 }
 
-// Fill-free leaf-first LDL^T schedule for the per-sample system (tree solver).
+// LDL^T schedule for the per-sample system (tree solver, afs_tables.cpp tree_schedule).
 // Edges of the current graph: for section s with in-current a and out-currents b (c),
 // edge[s][0] = (a,b), edge[s][1] = (a,c), edge[s][2] = (b,c).  In round r, chain lane k
 // eliminates step[r][k].c, whose remaining neighbours are n0 (and n1) through edges e0
-// (e1); e01 is the edge n0-n1 that receives the fill-free update.  c = -1: idle.
-constexpr int TREE_CHAINS = 4;
-constexpr int TREE_MAX_ROUNDS = 36;
+// (e1); e01 is the edge n0-n1 that receives the update (a fill edge when n0 and n1 were not
+// adjacent).  Edge storage ids: 0..TREE_NE-1 = X_OFF slots, TREE_NE + x = a fill edge kept
+// in the solution slot of current x (free during the forward pass).  c = -1: idle.
+constexpr int TREE_CHAINS = 12;
+constexpr int TREE_MAX_ROUNDS = 20;
 constexpr int TREE_NE = 104;
 struct SolveStep {
-  int8_t c, n0, n1, e0, e1, e01;
+  int16_t c, n0, n1, e0, e1, e01;
 };
 // The kernel's form of a step: LDS byte offsets inside the utterance block, 16 bytes = one
 // LDS load.  c/n0/n1 address the pivot (rhs at a fixed distance), e0/e1/e01 the edges,
@@ -80,6 +82,9 @@ struct alignas(16) StepRec {
 };
 // Currents whose d/dt another lane reads (branch partners and radiation; tree_core.h X_UR).
 constexpr int NUR = 16;
+// Currents whose noise-filtered value another lane reads (outputs of the constriction
+// candidates 24..64 and the radiation currents; tree_core.h X_UN).
+constexpr int NUN = 48;
 
 // The tables the cooperative kernel reads inside its time loop, packed so that one copy
 // per wave fits in LDS next to the four utterance blocks (tds_tree.hip).
@@ -109,6 +114,7 @@ struct Consts {
   Hot h;
   StepRec step[TREE_MAX_ROUNDS][TREE_CHAINS];
   int8_t ur_slot[NC];  // X_UR slot of a current, -1: none
+  int8_t un_slot[NC];  // X_UN slot of a current, -1: none
   Topo topo[NS];
   double stat[NSTATIC][ST_N];
 };

@@ -162,93 +162,110 @@ bool tree_schedule(Tables *t) {
   }
   t->n_edges = e;
   if (e != TREE_NE) return false;
-  // edge lookup between two currents (shared section)
-  auto sec_of_pair = [&](int a, int b, int *eid) -> bool {
-    for (int s = 0; s < NS; ++s) {
-      int in = t->cin[s], o0 = t->cout0[s], o1 = t->cout1[s];
-      int m[3] = {in, o0, o1};
-      int pa = -1, pb = -1;
-      for (int k = 0; k < 3; ++k) {
-        if (m[k] == a) pa = k;
-        if (m[k] == b) pb = k;
-      }
-      if (pa < 0 || pb < 0 || m[pa] == -1 || m[pb] == -1) continue;
-      int lo = pa < pb ? pa : pb, hi = pa < pb ? pb : pa;
-      int k = (lo == 0 && hi == 1) ? 0 : (lo == 0 && hi == 2) ? 1 : 2;
-      *eid = t->edge[s][k];
-      return *eid >= 0;
-    }
-    return false;
-  };
-  std::vector<int> chain[TREE_CHAINS];
-  for (int c = 0; c <= 31; ++c) chain[0].push_back(c);
-  chain[1].push_back(94);
-  chain[1].push_back(93);
-  for (int c = 64; c >= 34; --c) chain[1].push_back(c);
-  chain[2].push_back(96);
-  chain[2].push_back(95);
-  for (int c = 83; c >= 65; --c) chain[2].push_back(c);
-  for (int c = 89; c <= 92; ++c) chain[3].push_back(c);
-  for (int c = 88; c >= 84; --c) chain[3].push_back(c);
-  size_t longest = 0;
-  for (auto &ch : chain) longest = std::max(longest, ch.size());
-  const int rounds = (int)longest + 2;  // + eliminate 32, + root 33
-  if (rounds > TREE_MAX_ROUNDS) return false;
-  t->n_rounds = rounds;
-  for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
-    for (int k = 0; k < TREE_CHAINS; ++k) t->step[r][k] = SolveStep{-1, -1, -1, -1, -1, -1};
-  // symbolic elimination: adjacency of remaining currents
-  static bool adj[NC][NC];
-  std::memset(adj, 0, sizeof adj);
+  // current graph: edge storage id per pair (-1: not adjacent)
+  static int16_t eid[NC][NC];
+  for (int i = 0; i < NC; ++i)
+    for (int j = 0; j < NC; ++j) eid[i][j] = -1;
   for (int s = 0; s < NS; ++s) {
-    int m[3] = {t->cin[s], t->cout0[s], t->cout1[s]};
+    const int m[3] = {t->cin[s], t->cout0[s], t->cout1[s]};
+    const int pk[3][3] = {{-1, 0, 1}, {0, -1, 2}, {1, 2, -1}};  // edge index of pair (a,b)
     for (int a = 0; a < 3; ++a)
       for (int b = 0; b < 3; ++b)
-        if (a != b && m[a] != -1 && m[b] != -1) adj[m[a]][m[b]] = true;
+        if (a != b && m[a] >= 0 && m[b] >= 0) eid[m[a]][m[b]] = t->edge[s][pk[a][b]];
   }
-  bool gone[NC] = {false};
-  auto plan = [&](int r, int k, int c) -> bool {
-    int nb[NC], n = 0;
-    for (int j = 0; j < NC; ++j)
-      if (!gone[j] && adj[c][j]) nb[n++] = j;
-    if (n > 2) return false;                                   // would create fill
-    if (n == 2 && !adj[nb[0]][nb[1]]) return false;            // neighbours must be a clique
-    SolveStep st{(int8_t)c, -1, -1, -1, -1, -1};
-    int id;
-    if (n >= 1) { st.n0 = (int8_t)nb[0]; if (!sec_of_pair(c, nb[0], &id)) return false; st.e0 = (int8_t)id; }
-    if (n == 2) {
-      st.n1 = (int8_t)nb[1];
-      if (!sec_of_pair(c, nb[1], &id)) return false;
-      st.e1 = (int8_t)id;
-      if (!sec_of_pair(nb[0], nb[1], &id)) return false;
-      st.e01 = (int8_t)id;
-    }
-    t->step[r][k] = st;
-    return true;
+  // Lane programs: nested dissection of the tube graph (verified below).  Main path 0..64:
+  // an end chain from the lungs (0..9) and segments eliminated towards separators with fill
+  // into the separator behind them (11..19 -> 10, 21..27 -> 20, 39..30 -> 40, 42..52 -> 41);
+  // the lips end chain (after the radiation leaves 94, 93) 64..54; nose: 96, 95 then 83..77,
+  // and 66..76 with fill into 65, then 65 into the velum junction 40/41; fossa 88..84 into
+  // 28/29; sinus leaves; finally the separator path 10-20-28-29 and 53-41-40.
+  struct Prog { int start; std::vector<int> nodes; };
+  auto span = [](int a, int b) {
+    std::vector<int> v;
+    if (a <= b) for (int i = a; i <= b; ++i) v.push_back(i);
+    else for (int i = a; i >= b; --i) v.push_back(i);
+    return v;
   };
-  for (int r = 0; r < (int)longest; ++r) {
-    // all lanes of one round must touch disjoint unknowns
-    bool touched[NC] = {false};
+  auto cat = [](std::vector<int> a, const std::vector<int> &b) { a.insert(a.end(), b.begin(), b.end()); return a; };
+  std::vector<std::vector<Prog>> lanes(TREE_CHAINS);
+  lanes[0] = {{0, span(0, 9)}};
+  lanes[1] = {{0, span(11, 19)}};
+  lanes[2] = {{0, span(21, 27)}};
+  lanes[3] = {{0, span(88, 84)}};
+  lanes[4] = {{0, span(39, 30)}};
+  lanes[5] = {{0, span(42, 52)}};
+  lanes[6] = {{0, cat({94, 93}, span(64, 54))}, {13, {53, 41, 40}}};
+  lanes[7] = {{0, cat({96, 95}, span(83, 77))}};
+  lanes[8] = {{0, cat(span(66, 76), {65})}};
+  lanes[9] = {{0, {89, 90}}};
+  lanes[10] = {{0, {91, 92}}};
+  lanes[11] = {{10, {10, 20, 28, 29}}};
+  int prog[TREE_MAX_ROUNDS][TREE_CHAINS];
+  int order[NC];
+  for (int i = 0; i < NC; ++i) order[i] = -1;
+  for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
+    for (int k = 0; k < TREE_CHAINS; ++k) prog[r][k] = -1;
+  int rounds = 0;
+  for (int k = 0; k < TREE_CHAINS; ++k)
+    for (const Prog &p : lanes[k])
+      for (size_t i = 0; i < p.nodes.size(); ++i) {
+        const int r = p.start + (int)i, c = p.nodes[i];
+        if (r >= TREE_MAX_ROUNDS - 2 || prog[r][k] != -1 || order[c] != -1) return false;
+        prog[r][k] = c;
+        order[c] = r;
+        rounds = std::max(rounds, r + 1);
+      }
+  for (int i = 0; i < NC; ++i)
+    if (order[i] < 0) return false;
+  t->n_rounds = rounds;
+  // Symbolic elimination in lock step: at most two remaining neighbours per step, lanes of a
+  // round touch disjoint unknowns and edges, fill edges go to the solution slot of their
+  // first-eliminated end (whose backward step reads them before writing its solution).
+  bool gone[NC] = {false};
+  bool uslot[NC] = {false};
+  for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
+    for (int k = 0; k < TREE_CHAINS; ++k) t->step[r][k] = SolveStep{-1, -1, -1, -1, -1, -1};
+  for (int r = 0; r < rounds; ++r) {
+    std::vector<int> wr[TREE_CHAINS], rd[TREE_CHAINS];  // ids: unknowns, 1000 + edge storage
     for (int k = 0; k < TREE_CHAINS; ++k) {
-      if (r >= (int)chain[k].size()) continue;
-      if (!plan(r, k, chain[k][r])) return false;
-      const SolveStep &st = t->step[r][k];
-      for (int q : {(int)st.c, (int)st.n0, (int)st.n1}) {
-        if (q < 0) continue;
-        if (touched[q]) return false;
-        touched[q] = true;
+      const int c = prog[r][k];
+      if (c < 0) continue;
+      int nb[NC], n = 0;
+      for (int j = 0; j < NC; ++j)
+        if (!gone[j] && j != c && eid[c][j] >= 0) nb[n++] = j;
+      if (n > 2) return false;
+      const int nxt = (r + 1 < rounds) ? prog[r + 1][k] : -1;
+      if (n == 2 && nb[1] == nxt) std::swap(nb[0], nb[1]);
+      SolveStep st{(int16_t)c, -1, -1, -1, -1, -1};
+      if (n >= 1) { st.n0 = (int16_t)nb[0]; st.e0 = eid[c][nb[0]]; }
+      if (n == 2) { st.n1 = (int16_t)nb[1]; st.e1 = eid[c][nb[1]]; st.e01 = eid[nb[0]][nb[1]]; }
+      for (int q : {(int)st.c, (int)st.n0, (int)st.n1}) if (q >= 0) { wr[k].push_back(q); rd[k].push_back(q); }
+      for (int q : {(int)st.e0, (int)st.e1}) if (q >= 0) rd[k].push_back(1000 + q);
+      if (st.e01 >= 0) { wr[k].push_back(1000 + st.e01); rd[k].push_back(1000 + st.e01); }
+      t->step[r][k] = st;
+    }
+    for (int a = 0; a < TREE_CHAINS; ++a)
+      for (int b = 0; b < TREE_CHAINS; ++b)
+        if (a != b)
+          for (int x : wr[a])
+            for (int y : rd[b])
+              if (x == y) return false;
+    // apply: fill edges, eliminations
+    for (int k = 0; k < TREE_CHAINS; ++k) {
+      SolveStep &st = t->step[r][k];
+      if (st.c < 0) continue;
+      if (st.n1 >= 0 && st.e01 < 0) {
+        const int x = order[st.n0] < order[st.n1] ? st.n0 : st.n1;
+        if (uslot[x]) return false;
+        uslot[x] = true;
+        const int id = TREE_NE + x;
+        eid[st.n0][st.n1] = eid[st.n1][st.n0] = (int16_t)id;
+        st.e01 = (int16_t)id;
       }
     }
     for (int k = 0; k < TREE_CHAINS; ++k)
-      if (r < (int)chain[k].size()) gone[chain[k][r]] = true;
+      if (t->step[r][k].c >= 0) gone[t->step[r][k].c] = true;
   }
-  if (!plan(rounds - 2, 0, 32)) return false;
-  gone[32] = true;
-  if (!plan(rounds - 1, 0, 33)) return false;
-  gone[33] = true;
-  for (int c = 0; c < NC; ++c)
-    if (!gone[c]) return false;
-  if (t->step[rounds - 1][0].n0 != -1) return false;
   // Register carries (tree_core.h solve_forward / solve_backward).  Forward: after a step
   // the lane holds the new pivot of its n0, valid until another lane touches that unknown;
   // an idle round (sink step) overwrites it.  Backward: the lane holds the solution of the
@@ -380,6 +397,7 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   // step records: LDS byte offsets of the tree kernel's utterance block (tree_core.h)
   using namespace tree;
   auto off = [](int slot) { return (uint16_t)(slot * 8); };
+  auto eoff = [&](int id) { return id < TREE_NE ? off(X_OFF + id) : off(X_U + (id - TREE_NE)); };
   for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
     for (int k = 0; k < TREE_CHAINS; ++k) {
       const SolveStep &st = t->step[r][k];
@@ -388,9 +406,9 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
       q.c = off(X_DIAG + (on ? st.c : NODE_SINK));
       q.n0 = off(X_DIAG + (on && st.n0 >= 0 ? st.n0 : NODE_SINK));
       q.n1 = off(X_DIAG + (on && st.n1 >= 0 ? st.n1 : NODE_SINK));
-      q.e0 = off(X_OFF + (on && st.n0 >= 0 ? st.e0 : EDGE_ZERO));
-      q.e1 = off(X_OFF + (on && st.n1 >= 0 ? st.e1 : EDGE_ZERO));
-      q.e01 = off(X_OFF + (on && st.n0 >= 0 && st.n1 >= 0 ? st.e01 : EDGE_SINK));
+      q.e0 = on && st.n0 >= 0 ? eoff(st.e0) : off(X_OFF + EDGE_ZERO);
+      q.e1 = on && st.n1 >= 0 ? eoff(st.e1) : off(X_OFF + EDGE_ZERO);
+      q.e01 = on && st.n0 >= 0 && st.n1 >= 0 ? eoff(st.e01) : off(X_OFF + EDGE_SINK);
       q.un0 = off(X_U + (on && st.n0 >= 0 ? st.n0 : U_ZERO));
       q.un1 = off(X_U + (on && st.n1 >= 0 ? st.n1 : U_ZERO));
     }
@@ -403,6 +421,17 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
       c.ur_slot[t->cout0[s]] = (int8_t)nur++;
       c.ur_slot[t->cout1[s]] = (int8_t)nur++;
     }
+  // X_UN slots: outputs of the sections a constriction can narrow (24..64) and radiation
+  std::memset(c.un_slot, -1, sizeof c.un_slot);
+  int nun = 0;
+  auto add_un = [&](int i) {
+    if (i < 0 || c.un_slot[i] >= 0) return;
+    if (nun >= NUN) { t->n_rounds = -1; return; }
+    c.un_slot[i] = (int8_t)nun++;
+  };
+  for (int s = S_GLOT_UP; s <= S_LAST_MOUTH; ++s) { add_un(t->cout0[s]); add_un(t->cout1[s]); }
+  add_un(t->cout0[S_LAST_NOSE]);
+  add_un(t->cout1[S_LAST_NOSE]);
   t->uni.n_rounds = t->n_rounds;
   t->uni.fwd_carry = t->fwd_carry;
   t->uni.bwd_carry = t->bwd_carry;

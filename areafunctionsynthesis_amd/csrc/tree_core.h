@@ -50,8 +50,8 @@ constexpr double THR = 0.001;  // MIN_DIPOLE_AMP (TdsModel.cpp:1611)
 enum : int {
   // currents; X_U has two extra slots: U_SINK (idle / absent writes) and U_ZERO (0.0)
   X_U = 0, X_UR = X_U + NC + 2, X_UN = X_UR + NUR,
-  X_P4 = X_UN + NC,                                      // p[22], p[23], p[24], p[25]
-  X_E = X_P4 + 4, X_D = X_E + NS,                        // per section
+  X_P4 = X_UN + NUN,                                     // p[22], p[23], p[24], p[25]
+  X_E = X_P4 + 4, X_D = X_E + NDYNS,                     // E: dynamic sections (s-23), D: all
   X_L = X_D + NS, X_R1 = X_L + NDYNS, X_R0 = X_R1 + NDYNS, X_AREA = X_R0 + NDYNS,  // dynamic, s-23
   X_GLEN = X_AREA + NDYNS,                               // glottis section lengths (2)
   X_SMP = X_GLEN + 2,                                    // dipole samples (41)
@@ -447,8 +447,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     if (s < 0) continue;
     const double E = C.stat[static_index(s)][ST_E];
     const double beta = static_beta<W>(R, jj, U, C, s);
-    X[X_E + s] = E;
-    X[X_D + s] = R.p[jj] + C.h.dtTH1 * R.pr[jj] - E * (beta - 0.0);
+    X[X_D + s] = R.p[jj] + C.h.dtTH1 * R.pr[jj] - E * (beta - 0.0);  // (E: a table constant)
   }
 #pragma unroll
   for (int j = 0; j < S::ND; ++j) {
@@ -513,7 +512,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     }
     R.al[j] = alpha;
     R.be[j] = beta;
-    X[X_E + s] = E;
+    X[X_E + s - DYN0] = E;
     X[X_D + s] = R.p[j] + C.h.dtTH1 * R.pr[j] - E * (beta - 0.0);
     X[X_L + s - DYN0] = L;
     X[X_R0 + s - DYN0] = R0;
@@ -587,8 +586,8 @@ AFS_HD inline void dipole_targets(Xc &x, double *X, const Uni &U, const Consts &
   double flow = 0.0;
   const Topo tn = C.topo[c.narrow];
   const int o0 = tn.out0, o1 = tn.out1;
-  if (o0 != -1) flow += X[X_UN + o0];
-  if (o1 != -1) flow += X[X_UN + o1];
+  if (o0 != -1) flow += X[X_UN + C.un_slot[o0]];
+  if (o1 != -1) flow += X[X_UN + C.un_slot[o1]];
   if (flow < 0.0) flow = 0.0;
   double v = flow / A;
   double fc = 6000.0, gain = 0.0;
@@ -850,6 +849,9 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
 AFS_HD inline double sec_L(const double *X, const Consts &C, int s) {
   return (s >= DYN0 && s < DYN0 + NDYNS) ? X[X_L + s - DYN0] : C.stat[static_index(s)][ST_L];
 }
+AFS_HD inline double sec_E(const double *X, const Consts &C, int s) {
+  return (s >= DYN0 && s < DYN0 + NDYNS) ? X[X_E + s - DYN0] : C.stat[static_index(s)][ST_E];
+}
 AFS_HD inline double sec_R1(const double *X, const Consts &C, int s) {
   return (s >= DYN0 && s < DYN0 + NDYNS) ? X[X_R1 + s - DYN0] : C.stat[static_index(s)][ST_R];
 }
@@ -870,11 +872,11 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
     const double RB = dyn ? X[X_R0 + s - DYN0] : ((s == S_FOSSA0 && !opt.piriform_fossa) ? C.h.fossa_R0 : ks[ST_R]);
     const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
     const double AB = dyn ? X[X_AREA + s - DYN0] : C.h.area_last_nose;  // static: only used by s = 83
-    const double EB = X[X_E + s], DB = X[X_D + s];
+    const double EB = sec_E(X, C, s), DB = X[X_D + s];
     const Topo tp = C.topo[s];
     const int a = tp.src;
     double LA = 0.0, RA = 0.0, EA = 0.0, DA = 0.0;
-    if (a != -1) { LA = sec_L(X, C, a); RA = sec_R1(X, C, a); EA = X[X_E + a]; DA = X[X_D + a]; }
+    if (a != -1) { LA = sec_L(X, C, a); RA = sec_R1(X, C, a); EA = sec_E(X, C, a); DA = X[X_D + a]; }
     double LAB = LA + LB, RAB = RA + RB;
     const int br = tp.br;  // the other output of the source section (bifurcations)
     double Sx = 0.0;
@@ -912,7 +914,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
       const int rc = tp.out0, lc = tp.out1;
       double uR = X[X_U + rc], uL = X[X_U + lc], uRr = X[X_UR + C.ur_slot[rc]], uLr = X[X_UR + C.ur_slot[lc]];
       R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
-      R.rad_un[0] = X[X_UN + rc]; R.rad_un[1] = X[X_UN + lc];
+      R.rad_un[0] = X[X_UN + C.un_slot[rc]]; R.rad_un[1] = X[X_UN + C.un_slot[lc]];
       const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
       {
         double Rrad = C.h.rrad_num / (9.0 * PI * PI * AB);
@@ -934,7 +936,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
 }
 
 // ---------------------------------------------------------------------------
-// Solver rounds (chain lanes 0..3).
+// Solver rounds (chain lanes 0 .. TREE_CHAINS-1).
 // ---------------------------------------------------------------------------
 AFS_HD inline double &lds_at(double *X, uint32_t byte_off) {
   return *reinterpret_cast<double *>(reinterpret_cast<char *>(X) + byte_off);
@@ -1021,7 +1023,7 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
     R.ur[j] = (unew - uold) * idt - (TH1 / TH) * R.ur[j];
     R.un[j] = (1.0 - c) * unew + c * R.un[j];
     if (C.ur_slot[s] >= 0) X[X_UR + C.ur_slot[s]] = R.ur[j];
-    X[X_UN + s] = R.un[j];
+    if (C.un_slot[s] >= 0) X[X_UN + C.un_slot[s]] = R.un[j];
     double cin = 0.0;
     cin += unew;
     double cout = 0.0;
@@ -1031,7 +1033,7 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
     if (o1 != -1) cout += X[X_U + o1];
     double net = cin - cout;
     double old = R.p[j];
-    double p = X[X_D + s] + X[X_E + s] * net;
+    double p = X[X_D + s] + sec_E(X, C, s) * net;
     R.p[j] = p;
     double prr = (p - old) * idt - R.pr[j] * (TH1 / TH);
     R.pr[j] = prr;
@@ -1048,7 +1050,7 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
         double un = X[X_U + rc];
         double ur = (un - R.rad_u[q]) * idt - (TH1 / TH) * R.rad_ur[q];
         X[X_UR + C.ur_slot[rc]] = ur;
-        X[X_UN + rc] = (1.0 - c) * un + c * R.rad_un[q];
+        X[X_UN + C.un_slot[rc]] = (1.0 - c) * un + c * R.rad_un[q];
       }
     }
   }
@@ -1078,6 +1080,7 @@ AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C) {
 
 template <int W, class Xc>
 AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
+  static_assert(W >= TREE_CHAINS, "every solver chain needs a lane of the utterance");
   x.par([&](int gl, Lane<W> &R) { phase_geometry<W>(gl, R, X, U, C, ratio); });
   x.sync();
   x.mark(PH_GEOMETRY);
@@ -1101,6 +1104,12 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.sync();
   x.mark(PH_ROWS);
   const int nr = U.n_rounds;
+  // X_U is free until the backward pass rewrites it: it holds the fill edges (zero at first)
+  x.par([&](int gl, Lane<W> &R) {
+    (void)R;
+    for (int i = gl; i < NC; i += W) X[X_U + i] = 0.0;
+  });
+  x.sync();
   x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) {
     R.sc.cur = C.step[0][k];
     R.sc.next = C.step[1][k];

@@ -90,7 +90,6 @@ extern "C" long emu_tree_utterance(const afs_frame *frames, int F, int hop, unsi
   afs_options opt{1, 1, 1, 1, 0, 1};
   switch (W) {
     case 16: return run<16>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
-    case 8: return run<8>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
     case 32: return run<32>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
     case 64: return run<64>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
   }
