@@ -102,6 +102,9 @@ struct Hot {
   double rrad_num, lrad_num, tone_a[5], tone_b[5], out_a[9], out_b[9];
   double len_nose0, Bw_ph0, Mw_ph0, Kw_ph0, area_last_trachea, area_last_nose;
   double inv_dtTH, inv_dt2TH2;  // 1 / (dt theta), 1 / (dt theta)^2
+  double Tt;                    // glottis time step 1 / fs
+  double inv_dt;                // 1 / dt
+  double g_smk0, g_smk1;        // sqrt(mass * stiffness) of the two glottis masses (q-free)
 };
 // Values that steer branches in the time loop: kernel arguments on the device, so the
 // compiler keeps them in scalar registers and branches on them uniformly.

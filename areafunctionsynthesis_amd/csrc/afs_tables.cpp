@@ -394,6 +394,10 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   h.Kw_ph0 = t->Kw[S_PHARYNX0]; h.area_last_trachea = t->area[S_LAST_TRACHEA]; h.area_last_nose = t->area[S_LAST_NOSE];
   h.inv_dtTH = 1.0 / (t->dt * TH);
   h.inv_dt2TH2 = 1.0 / (t->dt * t->dt * TH * TH);
+  h.Tt = 1.0 / t->fs;
+  h.inv_dt = 1.0 / t->dt;
+  h.g_smk0 = std::sqrt(G_MASS0 * G_K0);
+  h.g_smk1 = std::sqrt(G_MASS1 * G_K1);
   // step records: LDS byte offsets of the tree kernel's utterance block (tree_core.h)
   using namespace tree;
   auto off = [](int slot) { return (uint16_t)(slot * 8); };

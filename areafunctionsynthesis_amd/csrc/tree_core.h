@@ -35,6 +35,13 @@ using std::sqrt;
 
 #include "afs_model.h"
 
+// Keeps the loads above it from being interleaved with the arithmetic below it (device).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define AFS_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define AFS_SCHED_BARRIER() ((void)0)
+#endif
+
 namespace afs {
 namespace tree {
 
@@ -84,13 +91,6 @@ enum : int {
   PH_C_POS, PH_C_T1, PH_C_T2, PH_C_LIP, PH_N_AMP, PH_N_RNG,
   PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_COUNT
 };
-
-// Keeps the loads above it from being interleaved with the arithmetic below it (device).
-#if defined(__HIP_DEVICE_COMPILE__)
-#define AFS_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
-#else
-#define AFS_SCHED_BARRIER() ((void)0)
-#endif
 
 // Solver sink / zero slots (see StepRec).
 constexpr int NODE_SINK = NC, U_SINK = NC, U_ZERO = NC + 1, EDGE_ZERO = TREE_NE, EDGE_SINK = TREE_NE + 1;
@@ -226,16 +226,27 @@ AFS_HD inline double junction_l(double A1, double A2) {
   return (8.0 * RHO / (3.0 * PI * PI)) * H * (a * r);
 }
 
-// IirFilter::getOutputSample on a shift-register state x[0..n-1], y[0..n-1] (newest first)
-AFS_HD inline double iir_run(double *st, int n, const double *a, const double *b, double x) {
-  double acc = a[0] * x;
-  for (int k = 1; k <= n; ++k) {
-    acc += a[k] * st[k - 1];
-    acc += b[k] * st[n + k - 1];
+// IirFilter::getOutputSample on a shift-register state x[0..n-1], y[0..n-1] (newest first).
+// State and coefficients are read into registers first (one batch of loads), the shifted
+// state is written back with independent stores.
+template <int N>
+AFS_HD inline double iir_run(double *st, const double *a, const double *b, double x) {
+  double sx[N], sy[N], ca[N + 1], cb[N + 1];
+#pragma unroll
+  for (int k = 0; k < N; ++k) { sx[k] = st[k]; sy[k] = st[N + k]; }
+#pragma unroll
+  for (int k = 0; k <= N; ++k) { ca[k] = a[k]; cb[k] = b[k]; }
+  AFS_SCHED_BARRIER();
+  double acc = ca[0] * x;
+#pragma unroll
+  for (int k = 1; k <= N; ++k) {
+    acc += ca[k] * sx[k - 1];
+    acc += cb[k] * sy[k - 1];
   }
-  for (int k = n - 1; k > 0; --k) { st[k] = st[k - 1]; st[n + k] = st[n + k - 1]; }
   st[0] = x;
-  st[n] = acc;
+  st[N] = acc;
+#pragma unroll
+  for (int k = 1; k < N; ++k) { st[k] = sx[k - 1]; st[N + k] = sy[k - 1]; }
   return acc;
 }
 
@@ -381,11 +392,15 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, c
     X[X_GP + 6] = r1 * X[X_FRAME + 0] + ratio * X[X_FRAME + 1];
     double rel0 = X[X_RELX + 0], rel1 = X[X_RELX + 1];
     // calcGeometry + getTubeData + Tube::setGlottisGeometry (TriangularGlottis.cpp:338-411)
+    // (divisions sharing a denominator use one reciprocal; sqrt(m k) is a constant since
+    // m ~ 1/q and k ~ q)
     double chink = gp[4] < 0.0 ? 0.0 : gp[4];
     double q = glottis_q(gp[0]);
     double f = sqrt(q);
+    const double inv_f = 1.0 / f, inv_q = 1.0 / q;
     double cord = G_REST_LEN * f;
-    double th0 = G_REST_THICK0 / f, th1 = G_REST_THICK1 / f;
+    const double inv_cord = 1.0 / cord;
+    double th0 = G_REST_THICK0 * inv_f, th1 = G_REST_THICK1 * inv_f;
     double olen[2], clen[2], ow[2], cz[2];
     glottis_open_close(gp, cord, rel0, rel1, olen, clen, ow, cz);
     X[X_AREA + 0] = clampA(olen[0] * ow[0] + chink);
@@ -393,20 +408,20 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, c
     X[X_GLEN + 0] = th0;
     X[X_GLEN + 1] = th1;
     // incTime (TriangularGlottis.cpp:154-330) with the previous sample's pressures
-    const double Tt = 1.0 / C.h.fs;
+    const double Tt = C.h.Tt;
     const double p0 = X[X_P4 + 0], p1 = X[X_P4 + 1], p2 = X[X_P4 + 2], p3 = X[X_P4 + 3];
-    double m0 = G_MASS0 / q, m1 = G_MASS1 / q;
-    double al0 = clen[0] / cord, al1 = clen[1] / cord;
+    double m0 = G_MASS0 * inv_q, m1 = G_MASS1 * inv_q;
+    double al0 = clen[0] * inv_cord, al1 = clen[1] * inv_cord;
     double k0 = G_K0 * q, k1 = G_K1 * q, kc0 = G_KC0 * q, kc1 = G_KC1 * q;
     double kcp = G_KCOUPLE * q * q;
     double dr0 = G_DAMP0 + al0 * 1.0, dr1 = G_DAMP1 + al1 * 1.0;
-    double rr0 = 2.0 * dr0 * sqrt(m0 * k0), rr1 = 2.0 * dr1 * sqrt(m1 * k1);
+    double rr0 = 2.0 * dr0 * C.h.g_smk0, rr1 = 2.0 * dr1 * C.h.g_smk1;
     double fo0 = p1 * olen[0] * th0;
     double fo1 = p2 * olen[1] * th1;
     fo0 += 0.5 * 0.5 * (p0 + p1) * G_INLET * cord;
     fo1 += 0.5 * 0.5 * (p3 + p2) * G_OUTLET * cord;
-    double rs0 = (gp[2] >= 0.0) ? gp[2] * (1.0 - cz[0] / cord) : gp[2];
-    double rs1 = (gp[3] >= 0.0) ? gp[3] * (1.0 - cz[1] / cord) : gp[3];
+    double rs0 = (gp[2] >= 0.0) ? gp[2] * (1.0 - cz[0] * inv_cord) : gp[2];
+    double rs1 = (gp[3] >= 0.0) ? gp[3] * (1.0 - cz[1] * inv_cord) : gp[3];
     double A = m0 + rr0 * Tt + Tt * Tt * (k0 + kc0 * al0) + kcp * Tt * Tt;
     double B = -kcp * Tt * Tt;
     double Cq = -kcp * Tt * Tt;
@@ -415,10 +430,11 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, c
     double Ff = fo1 * Tt * Tt + 2.0 * m1 * rel1 - m1 * X[X_RELX + 3] + rr1 * Tt * rel1 - Tt * Tt * kc1 * al1 * rs1;
     double det = A * Dq - B * Cq;
     if (fabs(det) < 0.000000001) det = 0.000000001;
+    const double inv_det = 1.0 / det;
     X[X_RELX + 2] = rel0;
     X[X_RELX + 3] = rel1;
-    X[X_RELX + 0] = (Ee * Dq - B * Ff) / det;
-    X[X_RELX + 1] = (A * Ff - Ee * Cq) / det;
+    X[X_RELX + 0] = (Ee * Dq - B * Ff) * inv_det;
+    X[X_RELX + 1] = (A * Ff - Ee * Cq) * inv_det;
   }
 }
 
@@ -583,21 +599,21 @@ AFS_HD inline void dipole_targets(Xc &x, double *X, const Uni &U, const Consts &
   double fup = 1.0 - fdn;
   double A = X[X_AREA + c.narrow - DYN0];
   if (A < 0.1) A = 0.1;
+  const double inv_A = 1.0 / A;
   double flow = 0.0;
   const Topo tn = C.topo[c.narrow];
   const int o0 = tn.out0, o1 = tn.out1;
   if (o0 != -1) flow += X[X_UN + C.un_slot[o0]];
   if (o1 != -1) flow += X[X_UN + C.un_slot[o1]];
   if (flow < 0.0) flow = 0.0;
-  double v = flow / A;
+  double v = flow * inv_A;
   double fc = 6000.0, gain = 0.0;
   if (c.art == LOWER_LIP) {
     gain = 2.0e-7;
   } else if (c.art == VOCAL_FOLDS) {
-    gain = 0.5e-7 * pow(10.0, X[X_GP + 5] / 20.0);
+    gain = 0.5e-7 * exp(X[X_GP + 5] * (2.302585092994045684 / 20.0));  // 10^(dB/20)
   } else {
-    double d = sqrt(4.0 * A / PI);
-    fc = 0.15 * v / d;
+    fc = 0.15 * v * sqrt((PI / 4.0) * inv_A);  // 0.15 v / d, d = sqrt(4 A / pi)
     gain = (fabs(c.obst - teeth) < 0.0001) ? 10.0e-7 : 5.0e-7;
   }
   double full = gain * fabs(v) * v * v * sqrt(A);
@@ -1064,12 +1080,12 @@ AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C) {
   flow += X[X_U + 94];
   flow += X[X_U + 95];
   flow += X[X_U + 96];
-  if (U.opt.radiation_from_skin) flow += iir_run(X + X_TONE, 4, C.h.tone_a, C.h.tone_b, X[X_P4 + 3]);
-  double op = (flow - X[X_PREVFLOW]) / C.h.dt;
+  if (U.opt.radiation_from_skin) flow += iir_run<4>(X + X_TONE, C.h.tone_a, C.h.tone_b, X[X_P4 + 3]);
+  double op = (flow - X[X_PREVFLOW]) * C.h.inv_dt;
   X[X_PREVFLOW] = flow;
-  double y = iir_run(X + X_OUTF, 8, C.h.out_a, C.h.out_b, op);
+  double y = iir_run<8>(X + X_OUTF, C.h.out_a, C.h.out_b, op);
   double smp = y * 0.004;
-  smp = smp / 32767;
+  smp = smp * (1.0 / 32767);
   if (!isfinite(smp)) X[X_NONFIN] = 1.0;
   return smp;
 }
