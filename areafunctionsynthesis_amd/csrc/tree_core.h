@@ -38,8 +38,11 @@ using std::sqrt;
 // Keeps the loads above it from being interleaved with the arithmetic below it (device).
 #if defined(__HIP_DEVICE_COMPILE__)
 #define AFS_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+// s_waitcnt lgkmcnt(0) (gfx9 encoding: vmcnt and expcnt left at their maximum)
+#define AFS_LDS_DRAIN() __builtin_amdgcn_s_waitcnt(0xC07F)
 #else
 #define AFS_SCHED_BARRIER() ((void)0)
+#define AFS_LDS_DRAIN() ((void)0)
 #endif
 
 namespace afs {
@@ -1131,6 +1134,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
     R.sc.next = C.step[1][k];
     R.sc.d = R.sc.y = 0.0;
   });
+  AFS_LDS_DRAIN();  // the loop head must not wait for the previous round's stores
   for (int r = 0; r < nr; ++r) {
     const bool carried = (U.fwd_carry >> r) & 1;
     x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { solve_forward(k, r, carried, X, C, R.sc); });
@@ -1142,6 +1146,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
     R.sc.next = C.step[nr >= 2 ? nr - 2 : 0][k];
     R.sc.y = 0.0;
   });
+  AFS_LDS_DRAIN();
   for (int r = nr - 1; r >= 0; --r) {
     const bool carried = (U.bwd_carry >> r) & 1;
     x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { solve_backward(k, r, carried, X, C, R.sc); });

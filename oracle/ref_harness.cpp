@@ -138,6 +138,27 @@ void afsref_currents(void *v, double *u) {
 long afsref_rand_calls(void) { return g_rand_calls; }
 
 // One utterance end to end: latch frames[0], then (F-1) calls of hop samples.
+// opt6 (optional): turbulence losses, soft walls, noise sources, radiation from skin,
+// piriform fossa, inner length corrections -- TdsModel::Options (TdsModel.h:83-95).
+long afsref_utterance_opt(const ao_frame *frames, int F, int hop, unsigned seed, double fs, double *out,
+                          const int *opt6) {
+  RefVoice *v = new RefVoice(fs, seed);
+  if (opt6) {
+    TdsModel::Options &o = v->tds.options;
+    o.turbulenceLosses = opt6[0] != 0;
+    o.softWalls = opt6[1] != 0;
+    o.generateNoiseSources = opt6[2] != 0;
+    o.radiationFromSkin = opt6[3] != 0;
+    o.piriformFossa = opt6[4] != 0;
+    o.innerLengthCorrections = opt6[5] != 0;
+  }
+  long n = 0;
+  v->call(&frames[0], hop, nullptr);
+  for (int k = 1; k < F; ++k) n += v->call(&frames[k], hop, out + n);
+  delete v;
+  return n;
+}
+
 long afsref_utterance(const ao_frame *frames, int F, int hop, unsigned seed, double fs, double *out) {
   RefVoice *v = new RefVoice(fs, seed);
   long n = 0;

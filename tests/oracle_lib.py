@@ -36,6 +36,19 @@ def build_oracle() -> None:
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")] + targets)
 
 
+# TdsModel::Options (TdsModel.h:83-95) in afs_options / ao_options order, with defaults
+OPTION_NAMES = ("turbulence_losses", "soft_walls", "generate_noise_sources", "radiation_from_skin",
+                "piriform_fossa", "inner_length_corrections")
+OPTION_DEFAULTS = (1, 1, 1, 1, 0, 1)
+
+
+def option_vector(opt: dict):
+    unknown = set(opt) - set(OPTION_NAMES)
+    if unknown:
+        raise KeyError(f"unknown options {sorted(unknown)}")
+    return [int(bool(opt.get(n, d))) for n, d in zip(OPTION_NAMES, OPTION_DEFAULTS)]
+
+
 class Oracle:
     """Restatement: one utterance at a time (batch 1), fp64."""
 
@@ -68,11 +81,16 @@ class Oracle:
         lib.ao_chebyshev.restype = ctypes.c_int
         self.lib = lib
 
-    def utterance(self, frames: np.ndarray, hop: int, seed: int, fs: float) -> np.ndarray:
+    def utterance(self, frames: np.ndarray, hop: int, seed: int, fs: float, opt=None) -> np.ndarray:
+        """opt: dict of TdsModel options (OPTION_NAMES) overriding the defaults."""
         frames = np.ascontiguousarray(frames, dtype=FRAME_DTYPE)
         F = frames.shape[0]
         out = np.zeros((F - 1) * hop, dtype=np.float64)
-        n = self.lib.ao_synthesize_utterance(_ptr(frames), F, hop, seed, fs, None, _ptr(out))
+        o = None
+        if opt:
+            vals = option_vector(opt)
+            o = (ctypes.c_int * 6)(*vals)
+        n = self.lib.ao_synthesize_utterance(_ptr(frames), F, hop, seed, fs, o, _ptr(out))
         assert n == out.size
         return out
 
@@ -146,16 +164,20 @@ class RefLib:
         lib.afsref_utterance.restype = ctypes.c_long
         lib.afsref_utterance.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint,
                                          ctypes.c_double, _vp]
+        lib.afsref_utterance_opt.restype = ctypes.c_long
+        lib.afsref_utterance_opt.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint,
+                                             ctypes.c_double, _vp, _vp]
         lib.afsref_chebyshev.restype = ctypes.c_int
         lib.afsref_chebyshev.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int, _vp, _vp]
         lib.afsref_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, _vp]
         self.lib = lib
 
-    def utterance(self, frames: np.ndarray, hop: int, seed: int, fs: float) -> np.ndarray:
+    def utterance(self, frames: np.ndarray, hop: int, seed: int, fs: float, opt=None) -> np.ndarray:
         frames = np.ascontiguousarray(frames, dtype=FRAME_DTYPE)
         F = frames.shape[0]
         out = np.zeros((F - 1) * hop, dtype=np.float64)
-        n = self.lib.afsref_utterance(_ptr(frames), F, hop, seed, fs, _ptr(out))
+        o = (ctypes.c_int * 6)(*option_vector(opt or {}))
+        n = self.lib.afsref_utterance_opt(_ptr(frames), F, hop, seed, fs, _ptr(out), o)
         assert n == out.size
         return out
 

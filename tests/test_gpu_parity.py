@@ -215,3 +215,30 @@ def test_full_second_static_vowels_rms(contexts, oracle, solver):
     # deterministic: a second run is bitwise identical
     y2 = ctx.synthesize(frames, w.hop, seeds=w.seeds)
     assert np.array_equal(y, y2)
+
+
+OPTION_VARIANTS = [
+    {"turbulence_losses": 0}, {"soft_walls": 0}, {"generate_noise_sources": 0},
+    {"radiation_from_skin": 0}, {"piriform_fossa": 1}, {"inner_length_corrections": 0},
+    {"turbulence_losses": 0, "soft_walls": 0, "generate_noise_sources": 0, "radiation_from_skin": 0,
+     "piriform_fossa": 1, "inner_length_corrections": 0},
+]
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_options_vs_oracle(contexts, oracle, solver):
+    """TdsModel::Options variants (afs_options) on the GPU against the oracle (which is
+    pinned to the reference build for the same variants in test_oracle.py)."""
+    sh = default_shapes()
+    f = oracle.af_to_frame(sh["s"])
+    f["velum_opening_cm2"] = 0.6
+    f["glottis"] = DEFAULT_GLOTTIS
+    g = oracle.af_to_frame(sh["(a)b(a):"])
+    g["velum_opening_cm2"] = 0.2
+    g["glottis"] = [140.0, 9000.0, 0.01, 0.02, 0.0, -20.0]
+    frames = np.stack([f, f, g, g, f])
+    for opt in OPTION_VARIANTS:
+        ctx = contexts(22050.0, solver, **opt)
+        y = ctx.synthesize(np.ascontiguousarray(frames[None]), 150, seeds=np.array([3], np.uint32))
+        x = oracle.utterance(frames, 150, 3, 22050.0, opt=opt)
+        assert np.abs(y[0] - x).max() <= GOLD_TOL, (opt, float(np.abs(y[0] - x).max()))

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from areafunctionsynthesis_amd.frames import FRAME_DTYPE
+from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS, FRAME_DTYPE
 from areafunctionsynthesis_amd.params import default_shapes
 
 
@@ -101,3 +101,36 @@ def test_restatement_matches_reference_random_trajectories(oracle):
         x = oracle.utterance(fr, hop, seed, fs)
         y = ref.utterance(fr, hop, seed, fs)
         assert np.array_equal(x, y, equal_nan=True), trial
+
+
+OPTION_VARIANTS = [
+    {"turbulence_losses": 0}, {"soft_walls": 0}, {"generate_noise_sources": 0},
+    {"radiation_from_skin": 0}, {"piriform_fossa": 1}, {"inner_length_corrections": 0},
+    {"turbulence_losses": 0, "soft_walls": 0, "generate_noise_sources": 0, "radiation_from_skin": 0,
+     "piriform_fossa": 1, "inner_length_corrections": 0},
+]
+
+
+@pytest.mark.parametrize("opt", OPTION_VARIANTS, ids=lambda o: "+".join(f"{k}={v}" for k, v in o.items()))
+def test_options_vs_reference(oracle, opt):
+    """TdsModel::Options (TdsModel.h:83-95): every option the restatement implements, flipped
+    one at a time and all together, bit for bit against the reference build."""
+    from oracle_lib import RefLib
+    try:
+        ref = RefLib()
+    except FileNotFoundError:
+        pytest.skip("reference build not available")
+    sh = default_shapes()
+    f = oracle.af_to_frame(sh["s"])
+    f["velum_opening_cm2"] = 0.6
+    f["glottis"] = DEFAULT_GLOTTIS
+    g = oracle.af_to_frame(sh["(a)b(a):"])
+    g["velum_opening_cm2"] = 0.2
+    g["glottis"] = [140.0, 9000.0, 0.01, 0.02, 0.0, -20.0]
+    frames = np.stack([f, f, g, g, f])
+    x = oracle.utterance(frames, 150, 3, 22050.0, opt=opt)
+    y = ref.utterance(frames, 150, 3, 22050.0, opt=opt)
+    assert np.isfinite(x).all() and np.array_equal(x, y)
+    # the option changes the output (it is not silently ignored)
+    base = oracle.utterance(frames, 150, 3, 22050.0)
+    assert not np.array_equal(x, base)
