@@ -24,7 +24,7 @@ EXPORTED = (
     "afs_abi_version", "afs_config_default", "afs_status_string", "afs_create", "afs_destroy",
     "afs_last_error", "afs_set_stream", "afs_synchronize", "afs_synthesize",
     "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_session_destroy",
-    "afs_af_to_frames",
+    "afs_af_to_frames", "afs_to_int16",
 )
 
 
@@ -82,8 +82,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.afs_session_reset.argtypes = [vp, vp]
     lib.afs_session_destroy.argtypes = [vp]
     lib.afs_af_to_frames.argtypes = [vp, vp, ctypes.c_int64, vp]
+    lib.afs_to_int16.argtypes = [vp, vp, ctypes.c_int64, vp]
     for name in ("afs_create", "afs_set_stream", "afs_synchronize", "afs_synthesize",
-                 "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_af_to_frames"):
+                 "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_af_to_frames",
+                 "afs_to_int16"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include "afs_lane.h"
+#include "afs_audio.h"
 #include "afs_model.h"
 #include "afs_tree.h"
 
@@ -418,6 +419,36 @@ afs_status afs_af_to_frames(afs_ctx *c, const double *params, int64_t n, afs_fra
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (tmp_p) (void)hipFree(tmp_p);
   if (tmp_f) (void)hipFree(tmp_f);
+  return AFS_OK;
+}
+
+afs_status afs_to_int16(afs_ctx *c, const double *samples, int64_t n, int16_t *out) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (!samples || !out || n < 0) return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_to_int16: bad args");
+  if (n == 0) return AFS_OK;
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  const bool host_in = !is_device_ptr(samples), host_out = !is_device_ptr(out);
+  struct Staging {  // freed on every return path
+    void *in = nullptr, *out = nullptr;
+    ~Staging() {
+      if (in) (void)hipFree(in);
+      if (out) (void)hipFree(out);
+    }
+  } tmp;
+  const double *din = samples;
+  int16_t *dout = out;
+  if (host_in) {
+    HIP_TRY(c, hipMalloc(&tmp.in, (size_t)n * sizeof(double)));
+    HIP_TRY(c, hipMemcpyAsync(tmp.in, samples, (size_t)n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    din = (const double *)tmp.in;
+  }
+  if (host_out) {
+    HIP_TRY(c, hipMalloc(&tmp.out, (size_t)n * sizeof(int16_t)));
+    dout = (int16_t *)tmp.out;
+  }
+  HIP_TRY(c, afs::launch_to_int16(din, dout, n, c->stream));
+  if (host_out) HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)n * sizeof(int16_t), hipMemcpyDeviceToHost, c->stream));
+  if (host_in || host_out || !(c->cfg.flags & AFS_ASYNC)) HIP_TRY(c, hipStreamSynchronize(c->stream));
   return AFS_OK;
 }
 

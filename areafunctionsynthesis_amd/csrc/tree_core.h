@@ -878,7 +878,7 @@ AFS_HD inline double sec_R1(const double *X, const Consts &C, int s) {
 template <int W>
 AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  const double dt = C.h.dt, idt = C.h.inv_dtTH, idt2 = C.h.inv_dt2TH2;
+  const double idt = C.h.inv_dtTH;
   const afs_options &opt = U.opt;
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
@@ -1028,7 +1028,7 @@ AFS_HD inline void solve_backward(int k, int r, bool carried, double *X, const C
 template <int W>
 AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  const double dt = C.h.dt, c = C.h.noise_lp_c, idt = C.h.inv_dtTH;
+  const double c = C.h.noise_lp_c, idt = C.h.inv_dtTH;
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const int s = slot_section<W>(j, gl);

@@ -132,6 +132,26 @@ class Context:
         return frames
 
 
+    def to_int16(self, samples, out=None):
+        """The reference's int16 audio ring format (Synthesizer.cpp:955-973) on the GPU:
+        short(x * 32767) truncated, clipped outside [-1, 1], NaN -> 0."""
+        if isinstance(samples, np.ndarray):
+            samples = np.ascontiguousarray(samples, dtype=np.float64)
+            n = samples.size
+            if out is None:
+                out = np.zeros(samples.shape, dtype=np.int16)
+        else:
+            n = int(samples.numel())
+            if out is None:
+                import torch
+                out = torch.empty(tuple(samples.shape), dtype=torch.int16, device=samples.device)
+        if _nbytes(out) != n * 2:
+            raise ValueError("out must hold one int16 per sample")
+        st = self._lib.afs_to_int16(self._h, _vp(_addr(samples)), n, _vp(_addr(out)))
+        _native.check(st, self._h, "afs_to_int16")
+        return out
+
+
 class Synthesizer:
     """Batch of ``B`` voices with the reference's incremental synthesis semantics.
 

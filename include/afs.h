@@ -19,6 +19,8 @@
  *   afs_af_to_frames        <- OneDimAreaFunction::calculateOneDimTubeFunction
  *                              (src/Backend/OneDimAreaFunction.cpp:75-138)
  *   afs_options             <- TdsModel::Options (src/Backend/TdsModel.h:83-95)
+ *   afs_to_int16            <- the int16 audio ring of Synthesizer::synthesizeSegment
+ *                              (Synthesizer.cpp:955-973, Signal16 = short, Signal.h:19)
  *
  * Errors: the reference prints and continues (TdsModel.cpp:1832,1849,1898,2267); here every
  * call returns an afs_status and afs_last_error() holds a message.  Inputs are clamped exactly
@@ -137,6 +139,10 @@ void afs_session_destroy(afs_session *s);
 /* Area-function model -> tube frames (pharynx/mouth part, teeth).  params[n][16] in
  * OneDimAreaFunction::ParamIndex order; velum and glottis fields of frames are left unchanged. */
 afs_status afs_af_to_frames(afs_ctx *ctx, const double *params, int64_t n, afs_frame *frames);
+
+/* Output format stage: out[i] = short(x * 32767) truncated towards zero, x > 1 -> 32767,
+ * x < -1 -> -32768, NaN -> 0 (Synthesizer.cpp:955-973).  Host or device pointers. */
+afs_status afs_to_int16(afs_ctx *ctx, const double *samples, int64_t n, int16_t *out);
 
 #ifdef __cplusplus
 }

@@ -1010,3 +1010,17 @@ void ao_af_to_frame(const double *p, ao_frame *f) {
   }
   f->teeth_position_cm = p[P_XIN];
 }
+
+/* Synthesizer.cpp:955-973: audioBuffer->setValue(pos, newSignal[i] * SHRT_MAX) stores into
+ * a Signal16 (signed short), then the two clipping branches overwrite out-of-range values. */
+void ao_to_int16(const double *x, long n, int16_t *out) {
+  for (long i = 0; i < n; ++i) {
+    const double v = x[i];
+    int16_t s;
+    if (v != v) s = 0;
+    else if (v > 1.0) s = 32767;
+    else if (v < -1.0) s = -32768;
+    else s = (int16_t)(int)(v * 32767.0);
+    out[i] = s;
+  }
+}

@@ -98,6 +98,10 @@ double ao_af_area(const double params16[16], double x_cm);
 /* IirFilter::createChebyshev (IirFilter.cpp:286-432): a[0..order], b[0..order]. */
 int ao_chebyshev(double cutoff_ratio, int highpass, int poles, double *a, double *b);
 
+/* Synthesizer::synthesizeSegment's int16 ring (Synthesizer.cpp:955-973): short(x*SHRT_MAX)
+ * (truncation), x > 1 -> SHRT_MAX, x < -1 -> SHRT_MIN; NaN -> 0 (the x86 conversion). */
+void ao_to_int16(const double *x, long n, int16_t *out);
+
 #ifdef __cplusplus
 }
 #endif

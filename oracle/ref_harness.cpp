@@ -175,6 +175,18 @@ int afsref_chebyshev(double ratio, int highpass, int poles, double *a, double *b
   return f.order;
 }
 
+// Synthesizer::synthesizeSegment's output stage (Synthesizer.cpp:955-973) on the reference's
+// own Signal16 ring: the same three statements per sample.
+void afsref_to_int16(const double *x, int n, short *out) {
+  Signal16 buf(n);
+  for (int i = 0; i < n; ++i) {
+    buf.setValue(i, (double)x[i] * SHRT_MAX);
+    if (x[i] > 1.0) buf.setValue(i, SHRT_MAX);
+    if (x[i] < -1.0) buf.setValue(i, SHRT_MIN);
+    out[i] = buf.getValue(i);
+  }
+}
+
 void afsref_glibc_rand(unsigned seed, int n, int *out) {
   srand(seed);
   for (int i = 0; i < n; ++i) out[i] = rand();

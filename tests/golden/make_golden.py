@@ -1,7 +1,8 @@
 """Generate the golden vectors in tests/golden/ from the REFERENCE build.
 
 Run in the build container (needs /root/reference for oracle/_ref):
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py          (all files)
+    python tests/golden/make_golden.py int16    (int16.npz only)
 
 Every expected value comes from oracle/_ref/libafsref.so -- the reference's own
 TdsModel / Tube / TriangularGlottis / IirFilter sources compiled unmodified and driven
@@ -48,7 +49,26 @@ def trajectory(o: Oracle, shapes, names, F, rng, lateral=False):
     return fr
 
 
+def int16_inputs() -> np.ndarray:
+    """Edge cases of the output stage (Synthesizer.cpp:955-973): exact +-1, just past +-1,
+    large magnitudes, signed zeros, NaN, values on and between int16 steps, random audio."""
+    eps = np.finfo(np.float64).eps
+    edge = [0.0, -0.0, 1.0, -1.0, 1.0 + eps, -1.0 - eps, 1.0 - eps / 2, -1.0 + eps / 2, 2.0, -2.0, 1e300,
+            -1e300, np.inf, -np.inf, np.nan, 0.5, -0.5, 1 / 32767, -1 / 32767, 0.99999 / 32767,
+            -0.99999 / 32767, 32766.5 / 32767, -32766.5 / 32767, 1e-320]
+    rng = np.random.default_rng(16)
+    return np.concatenate([np.array(edge), rng.uniform(-1.2, 1.2, 4000), rng.standard_normal(4000) * 0.3])
+
+
+def write_int16(ref: RefLib) -> None:
+    x = int16_inputs()
+    np.savez_compressed(os.path.join(HERE, "int16.npz"), x=x, out=ref.to_int16(x))
+
+
 def main() -> None:
+    if sys.argv[1:] == ["int16"]:
+        write_int16(RefLib())
+        return
     o = Oracle()
     r = RefLib()
     sh = default_shapes()
@@ -118,6 +138,7 @@ def main() -> None:
     np.savez_compressed(os.path.join(HERE, "af_frames.npz"), names=np.array(names), params=P,
                         area=F["area_cm2"], length=F["length_cm"], articulator=F["articulator"],
                         teeth=F["teeth_position_cm"], source=np.array("restatement"))
+    write_int16(r)
     print("golden vectors written to", HERE)
 
 

@@ -79,7 +79,14 @@ class Oracle:
         lib.ao_af_area.restype = ctypes.c_double
         lib.ao_chebyshev.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int, _vp, _vp]
         lib.ao_chebyshev.restype = ctypes.c_int
+        lib.ao_to_int16.argtypes = [_vp, ctypes.c_long, _vp]
         self.lib = lib
+
+    def to_int16(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.zeros(x.size, dtype=np.int16)
+        self.lib.ao_to_int16(_ptr(x), x.size, _ptr(out))
+        return out
 
     def utterance(self, frames: np.ndarray, hop: int, seed: int, fs: float, opt=None) -> np.ndarray:
         """opt: dict of TdsModel options (OPTION_NAMES) overriding the defaults."""
@@ -170,7 +177,14 @@ class RefLib:
         lib.afsref_chebyshev.restype = ctypes.c_int
         lib.afsref_chebyshev.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int, _vp, _vp]
         lib.afsref_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, _vp]
+        lib.afsref_to_int16.argtypes = [_vp, ctypes.c_int, _vp]
         self.lib = lib
+
+    def to_int16(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.zeros(x.size, dtype=np.int16)
+        self.lib.afsref_to_int16(_ptr(x), x.size, _ptr(out))
+        return out
 
     def utterance(self, frames: np.ndarray, hop: int, seed: int, fs: float, opt=None) -> np.ndarray:
         frames = np.ascontiguousarray(frames, dtype=FRAME_DTYPE)

@@ -23,6 +23,12 @@ def _standin(w) -> torch.Tensor:
     return torch.from_numpy(base[:, None] + np.arange(T)[None, :] * 1e-9)
 
 
+def _to_int16(x: torch.Tensor, out: torch.Tensor) -> None:
+    """CPU stand-in for Context.to_int16 (the oracle's restatement of the int16 stage)."""
+    from oracle_lib import Oracle
+    out.copy_(torch.from_numpy(Oracle().to_int16(x.numpy())).reshape(out.shape))
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -37,10 +43,18 @@ def _worker(rank, world, port, q):
     w = workloads.static_vowels(n, seconds=SECONDS, fs=FS, first_utterance=first)
     out = _standin(w)
     got = sharding.gather_to_rank0(out, world, rank, dist)
+    pcm = []
+    pg = sharding.PcmGather(_to_int16, out.shape, world, rank, dist, depth=2)
+    for scale in (0.5, -3.0, 1.0):  # three steps through two rotating buffers
+        slot = pg.submit(torch.sin(out * 1e3) * scale)
+        if slot == 1 or scale == 1.0:
+            pg.drain()
+            if rank == 0:
+                pcm.append(torch.cat(pg.result(slot)).numpy().copy())
     t = torch.tensor([float(out.numel())], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks timing reduction
     if rank == 0:
-        q.put((torch.cat(got).numpy(), w.seeds.copy(), float(t.item())))
+        q.put((torch.cat(got).numpy(), w.seeds.copy(), float(t.item()), pcm))
     else:
         q.put(("seeds", w.seeds.copy()))
     dist.barrier()
@@ -62,14 +76,19 @@ def test_gloo_world2_gather_matches_single_process():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
+    res = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     gathered = next(r for r in res if not isinstance(r[0], str))
-    audio, seeds0, numel = gathered
+    audio, seeds0, numel, pcm = gathered
     seeds1 = next(r[1] for r in res if isinstance(r[0], str))
     full = workloads.static_vowels(world * B, seconds=SECONDS, fs=FS)
     assert np.array_equal(audio, _standin(full).numpy())
     assert np.array_equal(np.concatenate([seeds0, seeds1]), np.arange(1, world * B + 1, dtype=np.uint32))
     assert numel == B * full.samples_per_utterance
+    from oracle_lib import Oracle
+    x = np.sin(_standin(full).numpy() * 1e3)
+    assert len(pcm) == 2
+    assert np.array_equal(pcm[0], Oracle().to_int16(x * -3.0).reshape(x.shape))  # step 2 (slot 1)
+    assert np.array_equal(pcm[1], Oracle().to_int16(x).reshape(x.shape))  # step 3 reused slot 0
