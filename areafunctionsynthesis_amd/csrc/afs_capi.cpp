@@ -424,8 +424,8 @@ afs_status afs_af_to_frames(afs_ctx *c, const double *params, int64_t n, afs_fra
 
 afs_status afs_to_int16(afs_ctx *c, const double *samples, int64_t n, int16_t *out) {
   if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AFS_OK;  // empty views may carry null pointers
   if (!samples || !out || n < 0) return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_to_int16: bad args");
-  if (n == 0) return AFS_OK;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   const bool host_in = !is_device_ptr(samples), host_out = !is_device_ptr(out);
   struct Staging {  // freed on every return path
