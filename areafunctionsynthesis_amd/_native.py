@@ -24,7 +24,8 @@ EXPORTED = (
     "afs_abi_version", "afs_config_default", "afs_status_string", "afs_create", "afs_destroy",
     "afs_last_error", "afs_set_stream", "afs_synchronize", "afs_synthesize",
     "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_session_destroy",
-    "afs_af_to_frames", "afs_to_int16",
+    "afs_af_to_frames", "afs_to_int16", "afs_target_sequence_default", "afs_target_sequence_samples",
+    "afs_play_target_sequences",
 )
 
 
@@ -32,6 +33,12 @@ class AfsOptions(ctypes.Structure):
     _fields_ = [("turbulence_losses", ctypes.c_int32), ("soft_walls", ctypes.c_int32),
                 ("generate_noise_sources", ctypes.c_int32), ("radiation_from_skin", ctypes.c_int32),
                 ("piriform_fossa", ctypes.c_int32), ("inner_length_corrections", ctypes.c_int32)]
+
+
+class AfsTargetSequence(ctypes.Structure):
+    _fields_ = [("stationary_s", ctypes.c_double * 4), ("transition_s", ctypes.c_double * 3),
+                ("f0_hz", ctypes.c_double * 4), ("lung_pressure_dpa", ctypes.c_double),
+                ("glottis", ctypes.c_double * 6)]
 
 
 class AfsConfig(ctypes.Structure):
@@ -83,9 +90,15 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.afs_session_destroy.argtypes = [vp]
     lib.afs_af_to_frames.argtypes = [vp, vp, ctypes.c_int64, vp]
     lib.afs_to_int16.argtypes = [vp, vp, ctypes.c_int64, vp]
+    lib.afs_target_sequence_default.argtypes = [ctypes.POINTER(AfsTargetSequence)]
+    lib.afs_target_sequence_default.restype = None
+    lib.afs_target_sequence_samples.argtypes = [ctypes.POINTER(AfsTargetSequence), ctypes.c_double]
+    lib.afs_target_sequence_samples.restype = ctypes.c_int64
+    lib.afs_play_target_sequences.argtypes = [vp, vp, ctypes.c_int32, vp, ctypes.POINTER(AfsTargetSequence), vp,
+                                              ctypes.c_int32, vp, ctypes.POINTER(AfsReport)]
     for name in ("afs_create", "afs_set_stream", "afs_synchronize", "afs_synthesize",
                  "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_af_to_frames",
-                 "afs_to_int16"):
+                 "afs_to_int16", "afs_play_target_sequences"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib

@@ -1,4 +1,4 @@
-// af_kernels.hip -- the area-function model on the device (BASELINE row f1, kernel K2).
+// af_kernels.hip -- the area-function model on the device.
 //
 // OneDimAreaFunction::calculateArea (OneDimAreaFunction.cpp:23-58) and
 // calculateOneDimTubeFunction (:75-138): 16 parameters -> 40 tube sections.  One lane
@@ -8,7 +8,7 @@
 
 #include <hip/hip_runtime.h>
 
-#include "afs_lane.h"
+#include "afs_af.h"
 #include "afs_model.h"
 
 namespace afs {
@@ -33,13 +33,8 @@ __device__ double af_area(const double *p, double x) {
   return a < 0.0 ? 0.0 : a;
 }
 
-__global__ void af_to_frames_kernel(const double *params, int64_t n, afs_frame *frames) {
-  int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n) return;
-  double p[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) p[i] = params[f * 16 + i];
-  afs_frame *fr = frames + f;
+// calculateOneDimTubeFunction (:75-138) for one parameter vector.
+__device__ void af_frame(const double *p, afs_frame *fr) {
   const double w = p[P_LVT] / 40;
   const double step = w * 0.01;
   double x = 0.0;
@@ -63,11 +58,107 @@ __global__ void af_to_frames_kernel(const double *params, int64_t n, afs_frame *
   fr->teeth_position_cm = p[P_XIN];
 }
 
+__global__ void af_to_frames_kernel(const double *params, int64_t n, afs_frame *frames) {
+  int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n) return;
+  double p[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) p[i] = params[f * 16 + i];
+  af_frame(p, frames + f);
+}
+
+// ---- Synthesizer::playTargetSequence (Synthesizer.cpp:1299-1422) ----------------------------
+
+// OneDimAreaFunction::reset: the schwa init() latches (OneDimAreaFunction.cpp:281-350).
+__constant__ double SCHWA[16] = {2.0, 1.0, 1.0, 3.02, 5.609, 1.0, 5.92, 2.879, 1.0, 8.48, 4.238, 1.0,
+                                 15.31, 0.701, 16.44, 1.65};
+
+// Lung pressure set by the fade-in statements (:1333-1346) at sample i < 0.1 fs.
+__device__ double fade_in(const TargetPlan &t, int64_t i) {
+  if (i < (double)0.05 * (double)t.fs) return 0.0;
+  return t.P / 2 * cos((0.1 * t.fs - i) / (0.05 * t.fs) * PI) + t.P / 2;
+}
+
+// glottisParams[PRESSURE] after sample i's statements: fade-in, then held, then the
+// fade-out of :1399-1403 with its denominator as written.
+__device__ double lung_pressure(const TargetPlan &t, int64_t i) {
+  double v;
+  if (i < (double)0.1 * (double)t.fs) v = fade_in(t, i);
+  else v = t.hold_j >= 0 ? fade_in(t, t.hold_j) : t.P;
+  const double total = t.b[6];
+  if (i > (double)(total - 0.1) * (double)t.fs)
+    v = -t.P / 2 * cos((total * t.fs - i) / (total - 0.1 * t.fs) * PI) + t.P / 2;
+  return v;
+}
+
+// F0 contour (:1348-1361).
+__device__ double f0_contour(const TargetPlan &t, int64_t i) {
+  const double *f = t.f0, *b = t.b, fs = t.fs;
+  if (i < (double)b[1] * fs) return (f[0] + f[1]) / 2 + (f[1] - f[0]) / 2 * cos((b[1] * fs - i) / (b[1] * fs) * PI);
+  if (i < (double)b[3] * fs)
+    return (f[2] + f[1]) / 2 + (f[2] - f[1]) / 2 * cos((b[3] * fs - i) / ((b[3] - b[1]) * fs) * PI);
+  return (f[3] + f[2]) / 2 + (f[3] - f[2]) / 2 * cos((b[6] * fs - i) / ((b[6] - b[3]) * fs) * PI);
+}
+
+// currentParams of sample i (:1364-1397) with interpolateParameters (:1286-1294).
+__device__ void target_params(const double *s, const TargetPlan &t, int64_t i, double *p) {
+  const double fs = t.fs, *b = t.b;
+  int seg;  // 0..6: stationary 0, transition 0, stationary 1, ...
+  if (i <= b[0] * fs) seg = 0;
+  else if (i <= b[1] * fs) seg = 1;
+  else if (i <= b[2] * fs) seg = 2;
+  else if (i <= b[3] * fs) seg = 3;
+  else if (i <= b[4] * fs) seg = 4;
+  else if (i <= b[5] * fs) seg = 5;
+  else seg = 6;
+  const double *s0 = s + 16 * (seg / 2);
+  if ((seg & 1) == 0) {
+    for (int k = 0; k < 16; ++k) p[k] = s0[k];
+  } else {
+    const double *s1 = s0 + 16;
+    const double t0 = b[seg - 1] * fs, t1 = b[seg] * fs;
+    const double c = cos((t1 - i) / (t1 - t0) * PI);
+    for (int k = 0; k < 16; ++k) p[k] = (s1[k] - s0[k]) / 2 * c + (s1[k] + s0[k]) / 2;
+  }
+}
+
+__global__ void target_frames_kernel(const double *seq, int Q, TargetPlan t, int64_t k0, int n, int64_t fstride,
+                                     afs_frame *frames) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)Q * n) return;
+  const int q = (int)(idx / n), k = (int)(idx % n);
+  const int64_t g = k0 + k;
+  afs_frame *fr = frames + (int64_t)q * fstride + k;
+  double p[16], gp[6];
+  if (g == 0) {
+    for (int i = 0; i < 16; ++i) p[i] = SCHWA[i];
+    for (int i = 0; i < 6; ++i) gp[i] = t.glottis[i];
+  } else {
+    const int64_t i = g - 1;
+    target_params(seq + (int64_t)q * 64, t, i, p);
+    gp[0] = f0_contour(t, i);
+    gp[1] = lung_pressure(t, i);
+    for (int j = 2; j < 6; ++j) gp[j] = t.glottis[j];
+  }
+  af_frame(p, fr);
+  fr->velum_opening_cm2 = 0.0;  // the Synthesizer's tube keeps Tube()'s closed velum
+  for (int j = 0; j < 6; ++j) fr->glottis[j] = gp[j];
+}
+
 }  // namespace
 
 hipError_t launch_af_to_frames(const double *params, int64_t n, afs_frame *frames, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(af_to_frames_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, params, n, frames);
+  return hipGetLastError();
+}
+
+hipError_t launch_target_frames(const double *seq, int Q, const TargetPlan &plan, int64_t k0, int n,
+                                int64_t fstride, afs_frame *frames, hipStream_t st) {
+  const int64_t total = (int64_t)Q * n;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(target_frames_kernel, dim3((unsigned)((total + 63) / 64)), dim3(64), 0, st, seq, Q, plan, k0,
+                     n, fstride, frames);
   return hipGetLastError();
 }
 

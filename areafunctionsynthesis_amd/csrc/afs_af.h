@@ -1,0 +1,32 @@
+// afs_af.h -- host interface of the area-function kernels (af_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "afs_model.h"
+
+namespace afs {
+
+// OneDimAreaFunction parameters[n][16] -> the pharynx/mouth part of frames[n] (K2).
+hipError_t launch_af_to_frames(const double *params, int64_t n, afs_frame *frames, hipStream_t st);
+
+// Synthesizer::playTargetSequence's trajectory (Synthesizer.cpp:1299-1422), everything that
+// does not depend on the target shapes, evaluated once on the host.
+struct TargetPlan {
+  double b[7];            // boundary_s (:1318-1326), summed left to right
+  double fs;              // SAMPLING_RATE
+  double f0[4];           // f0_Hz (:1311)
+  double P;               // steadyStateLungPressure
+  double glottis[6];      // init() latch glottis; [2..5] for every sample
+  int64_t hold_j;         // the last sample index below 0.1 fs (its fade-in value is held)
+};
+
+// frames[q * fstride + k] = global frame k0 + k (k < n) of target sequence q, for Q sequences
+// of 4 shapes each (seq[q][4][16]).  Frame 0 is init()'s schwa latch, frame g >= 1 is the tube
+// and glottis controls of sample g - 1 (K4).
+hipError_t launch_target_frames(const double *seq, int Q, const TargetPlan &plan, int64_t k0, int n,
+                                int64_t fstride, afs_frame *frames, hipStream_t st);
+
+}  // namespace afs

@@ -4,13 +4,18 @@
 // There is no CPU fallback: without a usable HIP device afs_create fails with
 // AFS_ERR_NO_DEVICE.
 #include <algorithm>
+#include <array>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
+#include <vector>
 
 #include <hip/hip_runtime.h>
 
+#include "afs_af.h"
 #include "afs_lane.h"
 #include "afs_audio.h"
 #include "afs_model.h"
@@ -37,6 +42,8 @@ struct afs_ctx {
   size_t stage_out_bytes = 0;
   void *stage_seeds = nullptr;
   size_t stage_seeds_bytes = 0;
+  void *tgt = nullptr;  // target sequences: shape rows [Q][4][16] then frame_row [B]
+  size_t tgt_bytes = 0;
   int32_t *dcount = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
@@ -103,17 +110,18 @@ bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE; }
 // Launch the synthesis for frame transitions [k0, k1) in chunks that keep each kernel
 // well below a second (state is carried between launches).
 afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int k0, int k1, int hop,
-                      double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B) {
+                      double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B,
+                      const int32_t *frame_row = nullptr) {
   const int64_t max_samples = tree(c) ? 65536 : 8192;
   int per = (int)std::max<int64_t>(1, max_samples / std::max(1, hop));
   for (int k = k0; k < k1; k += per) {
     int ke = std::min(k1, k + per);
     double *o = out + (int64_t)(k - k0) * hop;
     if (tree(c)) {
-      afs::TreeArgs a{c->dev_tab, frames, fstride, k, ke, hop, o, ostride, lanes, (double *)ws, B, c->host_tab.uni};
+      afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, k, ke, hop, o, ostride, lanes, (double *)ws, B, c->host_tab.uni};
       HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
     } else {
-      afs::LaneArgs a{c->dev_tab, frames, fstride, k, ke, hop, o, ostride, (double *)ws, rng, bp, B};
+      afs::LaneArgs a{c->dev_tab, frames, fstride, frame_row, k, ke, hop, o, ostride, (double *)ws, rng, bp, B};
       HIP_TRY(c, afs::launch_lane_synth(a, c->stream));
     }
   }
@@ -221,6 +229,7 @@ void afs_destroy(afs_ctx *c) {
   if (c->stage_in) (void)hipFree(c->stage_in);
   if (c->stage_out) (void)hipFree(c->stage_out);
   if (c->stage_seeds) (void)hipFree(c->stage_seeds);
+  if (c->tgt) (void)hipFree(c->tgt);
   if (c->dcount) (void)hipFree(c->dcount);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -449,6 +458,139 @@ afs_status afs_to_int16(afs_ctx *c, const double *samples, int64_t n, int16_t *o
   HIP_TRY(c, afs::launch_to_int16(din, dout, n, c->stream));
   if (host_out) HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)n * sizeof(int16_t), hipMemcpyDeviceToHost, c->stream));
   if (host_in || host_out || !(c->cfg.flags & AFS_ASYNC)) HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return AFS_OK;
+}
+
+// ---- Synthesizer::playTargetSequence (Synthesizer.cpp:1299-1422) -------------------------
+
+void afs_target_sequence_default(afs_target_sequence *ts) {
+  if (!ts) return;
+  static const double st[4] = {0.2, 0.05, 0.2, 0.1}, tr[3] = {0.05, 0.05, 0.05}, f0[4] = {100, 115, 105, 80};
+  static const double g[6] = {120.0, 10000.0, 0.01, 0.01, 0.0, -40.0};
+  std::memcpy(ts->stationary_s, st, sizeof st);
+  std::memcpy(ts->transition_s, tr, sizeof tr);
+  std::memcpy(ts->f0_hz, f0, sizeof f0);
+  ts->lung_pressure_dpa = 8000.0;
+  std::memcpy(ts->glottis, g, sizeof g);
+}
+
+static void target_bounds(const afs_target_sequence *ts, double *b) {  // :1318-1326, left to right
+  const double *s = ts->stationary_s, *t = ts->transition_s;
+  b[0] = s[0];
+  b[1] = s[0] + t[0];
+  b[2] = s[0] + t[0] + s[1];
+  b[3] = s[0] + t[0] + s[1] + t[1];
+  b[4] = s[0] + t[0] + s[1] + t[1] + s[2];
+  b[5] = s[0] + t[0] + s[1] + t[1] + s[2] + t[2];
+  b[6] = s[0] + t[0] + s[1] + t[1] + s[2] + t[2] + s[3];
+}
+
+int64_t afs_target_sequence_samples(const afs_target_sequence *ts, double fs) {
+  if (!ts || !(fs > 0.0)) return -1;
+  double b[7];
+  target_bounds(ts, b);
+  const double n = fs * b[6];
+  if (!(n >= 0.0) || n >= 2147483647.0) return -1;
+  return (int64_t)(int)n;  // int numSamples = SAMPLING_RATE * totalTime_s
+}
+
+afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t num_shapes, const int32_t *targets,
+                                     const afs_target_sequence *ts, const uint32_t *seeds, int32_t B, double *out,
+                                     afs_report *rep) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (!shapes || num_shapes <= 0 || !targets || !ts || B <= 0 || !out)
+    return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_play_target_sequences: need shapes, targets, timing, batch>0, out");
+  if (is_device_ptr(shapes) || is_device_ptr(targets))
+    return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_play_target_sequences: shapes and targets are host arrays");
+  const double fs = c->cfg.sampling_rate_hz;
+  const int64_t T = afs_target_sequence_samples(ts, fs);
+  if (T < 0) return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_play_target_sequences: bad timing");
+  for (int64_t k = 0; k < (int64_t)B * 4; ++k)
+    if (targets[k] < 0 || targets[k] >= num_shapes)
+      return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_play_target_sequences: target %lld out of range", (long long)k);
+  if (rep) std::memset(rep, 0, sizeof *rep);
+  if (T == 0) return AFS_OK;
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  // one tube trajectory per distinct sequence of four shapes
+  std::map<std::array<int32_t, 4>, int32_t> uniq;
+  std::vector<int32_t> row((size_t)B);
+  std::vector<double> seq;
+  for (int32_t b = 0; b < B; ++b) {
+    const std::array<int32_t, 4> key{targets[4 * b], targets[4 * b + 1], targets[4 * b + 2], targets[4 * b + 3]};
+    auto it = uniq.find(key);
+    if (it == uniq.end()) {
+      it = uniq.emplace(key, (int32_t)uniq.size()).first;
+      for (int j = 0; j < 4; ++j) seq.insert(seq.end(), shapes + 16 * (int64_t)key[j], shapes + 16 * (int64_t)key[j] + 16);
+    }
+    row[(size_t)b] = it->second;
+  }
+  const int Q = (int)uniq.size();
+  afs::TargetPlan plan{};
+  target_bounds(ts, plan.b);
+  plan.fs = fs;
+  std::memcpy(plan.f0, ts->f0_hz, sizeof plan.f0);
+  plan.P = ts->lung_pressure_dpa;
+  std::memcpy(plan.glottis, ts->glottis, sizeof plan.glottis);
+  {  // the last sample below 0.1 fs: its fade-in value is held until the fade-out
+    int64_t j = (int64_t)std::ceil((double)0.1 * fs);
+    while (j >= 0 && !((double)j < (double)0.1 * fs)) --j;
+    while ((double)(j + 1) < (double)0.1 * fs) ++j;
+    plan.hold_j = j;
+  }
+  afs_status s;
+  const size_t seq_bytes = seq.size() * sizeof(double);
+  if ((s = ensure(c, &c->tgt, &c->tgt_bytes, seq_bytes + (size_t)B * sizeof(int32_t))) != AFS_OK) return s;
+  double *dseq = (double *)c->tgt;
+  int32_t *drow = (int32_t *)((char *)c->tgt + seq_bytes);
+  HIP_TRY(c, hipMemcpyAsync(dseq, seq.data(), seq_bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(drow, row.data(), (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));  // the host vectors die with this call
+  const uint32_t *dseeds = seeds;
+  if (seeds && !is_device_ptr(seeds)) {
+    if ((s = ensure(c, &c->stage_seeds, &c->stage_seeds_bytes, (size_t)B * 4)) != AFS_OK) return s;
+    HIP_TRY(c, hipMemcpyAsync(c->stage_seeds, seeds, (size_t)B * 4, hipMemcpyHostToDevice, c->stream));
+    dseeds = (const uint32_t *)c->stage_seeds;
+  }
+  double *dout = out;
+  const bool host_out = !is_device_ptr(out);
+  if (host_out) {
+    if ((s = ensure(c, &c->stage_out, &c->stage_out_bytes, (size_t)B * T * sizeof(double))) != AFS_OK) return s;
+    dout = (double *)c->stage_out;
+  }
+  const int64_t bp = pad64(B);
+  if ((s = ensure(c, &c->ws, &c->ws_bytes, ws_bytes_for(c, bp))) != AFS_OK) return s;
+  if ((s = ensure(c, (void **)&c->rng, &c->rng_bytes, (size_t)(32 * bp) * sizeof(int32_t))) != AFS_OK) return s;
+  if (tree(c) && (s = ensure(c, &c->tree_lanes, &c->tree_lanes_bytes, lanes_bytes_for(c, bp))) != AFS_OK) return s;
+  if ((s = reset_state(c, c->ws, c->rng, c->tree_lanes, bp, B, dseeds)) != AFS_OK) return s;
+  // time chunks of Tc samples: Tc + 1 frames per sequence (the first repeats the previous
+  // chunk's last), at most 1 GiB of frames
+  const int64_t budget = (int64_t)1 << 30;
+  const int64_t Tc = std::max<int64_t>(1, std::min<int64_t>({T, 65536, budget / ((int64_t)Q * (int64_t)sizeof(afs_frame)) - 1}));
+  if ((s = ensure(c, &c->stage_in, &c->stage_in_bytes, (size_t)Q * (size_t)(Tc + 1) * sizeof(afs_frame))) != AFS_OK)
+    return s;
+  afs_frame *dframes = (afs_frame *)c->stage_in;
+  HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
+  for (int64_t k0 = 0; k0 < T; k0 += Tc) {
+    const int nk = (int)std::min<int64_t>(Tc, T - k0);
+    HIP_TRY(c, afs::launch_target_frames(dseq, Q, plan, k0, nk + 1, Tc + 1, dframes, c->stream));
+    if ((s = run_chunks(c, dframes, Tc + 1, 1, nk + 1, 1, dout + k0, T, c->ws, c->rng, c->tree_lanes, bp, B, drow)) !=
+        AFS_OK)
+      return s;
+  }
+  HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
+  int32_t nonfinite = 0;
+  if ((s = count_nonfinite(c, c->ws, bp, B, &nonfinite)) != AFS_OK) return s;
+  if (host_out) HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)B * T * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  const bool sync = !(c->cfg.flags & AFS_ASYNC) || host_out || rep;
+  if (sync) HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (rep) {
+    float ms = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    rep->device_ms = ms;
+    rep->samples = (int64_t)B * T;
+    rep->nonfinite_utterances = nonfinite;
+    rep->kernel = c->cfg.solver;
+  }
   return AFS_OK;
 }
 

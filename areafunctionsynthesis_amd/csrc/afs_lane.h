@@ -9,8 +9,9 @@ namespace afs {
 
 struct LaneArgs {
   const Tables *tab;         // device copy of the tables
-  const afs_frame *frames;   // frames[u * frame_stride + k]
+  const afs_frame *frames;   // frames[row(u) * frame_stride + k]
   int64_t frame_stride;
+  const int32_t *frame_row;  // row(u) = frame_row[u], or u when null (shared trajectories)
   int k_begin, k_end;        // frame transitions (k-1 -> k) processed by this launch
   int hop;                   // samples per transition
   double *out;               // out[u * out_stride + t], t = 0 .. (k_end-k_begin)*hop-1
@@ -26,8 +27,5 @@ int64_t lane_persist_rows();
 hipError_t launch_lane_reset(double *ws, int32_t *rng, int64_t bp, int B, const uint32_t *seeds, hipStream_t st);
 hipError_t launch_lane_synth(const LaneArgs &a, hipStream_t st);
 hipError_t launch_lane_nonfinite(const double *ws, int64_t bp, int B, int32_t *count, hipStream_t st);
-
-// Area function -> frames (af_kernels.hip).
-hipError_t launch_af_to_frames(const double *params, int64_t n, afs_frame *frames, hipStream_t st);
 
 }  // namespace afs

@@ -9,8 +9,9 @@ namespace afs {
 
 struct TreeArgs {
   const Tables *tab;
-  const afs_frame *frames;  // frames[u * frame_stride + k]
+  const afs_frame *frames;  // frames[row(u) * frame_stride + k]
   int64_t frame_stride;
+  const int32_t *frame_row; // row(u) = frame_row[u], or u when null (shared trajectories)
   int k_begin, k_end, hop;
   double *out;              // out[u * out_stride + t]
   int64_t out_stride;

@@ -607,7 +607,7 @@ __global__ void __launch_bounds__(64) lane_synth_kernel(LaneArgs a) {
   if (u >= a.B) return;
   const Tables &T = *a.tab;
   Lane L{T, a.ws + u, a.bp, a.rng + u};
-  const afs_frame *fu = a.frames + (int64_t)u * a.frame_stride;
+  const afs_frame *fu = a.frames + (int64_t)(a.frame_row ? a.frame_row[u] : u) * a.frame_stride;
   double *o = a.out + (int64_t)u * a.out_stride;
   Col NF = L.q(Q_NONFINITE);
   double bad = NF[0];

@@ -139,6 +139,20 @@ AFS_HD inline double pivot_recip(double d) {
 #endif
 }
 
+// Reciprocal and quotient of positive, normal operands (areas, surfaces, capacitances) without
+// the scaling/fixup steps of IEEE division: v_rcp_f64 + two Newton steps, and for the quotient
+// one residual correction (within 1 ulp of a / b).  Host builds (the CPU emulator) divide.
+AFS_HD inline double fast_rcp(double d) { return pivot_recip(d); }
+AFS_HD inline double fast_div(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double r = pivot_recip(b);
+  const double q = a * r;
+  return fma(r, fma(-b, q, a), q);
+#else
+  return a / b;
+#endif
+}
+
 // Lane registers.
 // Only the persistent state and the frame cache live here; per-sample intermediates
 // go through the LDS block or are recomputed from unchanged state.
@@ -183,7 +197,7 @@ AFS_HD inline int slot_section(int j, int gl) {
 AFS_HD inline double clampA(double a) { return a < AMIN ? AMIN : a; }
 
 AFS_HD inline double glottis_q(double f0) {
-  double q = 1.0 + (f0 - G_NAT_F0) / G_F0_DIV_Q;
+  double q = 1.0 + (f0 - G_NAT_F0) * (1.0 / G_F0_DIV_Q);
   return q < 0.05 ? 0.05 : q;
 }
 
@@ -204,7 +218,7 @@ AFS_HD inline void glottis_open_close(const double *gp, double cord, double rel0
     } else {
       double r = rest[i];
       if (fabs(r) < 0.000000001) r = 0.000000001;
-      double apex = cord * (1.0 + rel[i] / r);
+      double apex = cord * (1.0 + fast_div(rel[i], r));
       if (apex >= 0.0 && apex <= cord) {
         if (back > 0.0) {
           olen[i] = apex; ow[i] = back; clen[i] = cord - apex; cz[i] = 0.5 * (apex + cord);
@@ -224,7 +238,7 @@ AFS_HD inline double junction_l(double A1, double A2) {
   double a, b;
   if (A1 > A2) { a = sqrt(A1 * (1.0 / PI)); b = sqrt(A2 * (1.0 / PI)); }
   else { a = sqrt(A2 * (1.0 / PI)); b = sqrt(A1 * (1.0 / PI)); }
-  const double r = 1.0 / (a * b);
+  const double r = fast_rcp(a * b);
   const double H = 1.0 - (b * b) * r;
   return (8.0 * RHO / (3.0 * PI * PI)) * H * (a * r);
 }
@@ -383,7 +397,7 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, c
     } else if (s >= S_NOSE0) {  // nose sections 65..68: velum taper (Tube.cpp:402-416)
       double open = r1 * X[X_FRAME + 2] + ratio * X[X_FRAME + 3];
       int i = s - S_NOSE0;
-      X[X_AREA + s - DYN0] = clampA(open + ((double)(i * i) * (C.h.nose4_area - open)) / (double)16);
+      X[X_AREA + s - DYN0] = clampA(open + ((double)(i * i) * (C.h.nose4_area - open)) * (1.0 / 16));
     }
   }
   if (gl == 0) {
@@ -400,9 +414,9 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, c
     double chink = gp[4] < 0.0 ? 0.0 : gp[4];
     double q = glottis_q(gp[0]);
     double f = sqrt(q);
-    const double inv_f = 1.0 / f, inv_q = 1.0 / q;
+    const double inv_f = fast_rcp(f), inv_q = fast_rcp(q);
     double cord = G_REST_LEN * f;
-    const double inv_cord = 1.0 / cord;
+    const double inv_cord = fast_rcp(cord);
     double th0 = G_REST_THICK0 * inv_f, th1 = G_REST_THICK1 * inv_f;
     double olen[2], clen[2], ow[2], cz[2];
     glottis_open_close(gp, cord, rel0, rel1, olen, clen, ow, cz);
@@ -433,7 +447,7 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, c
     double Ff = fo1 * Tt * Tt + 2.0 * m1 * rel1 - m1 * X[X_RELX + 3] + rr1 * Tt * rel1 - Tt * Tt * kc1 * al1 * rs1;
     double det = A * Dq - B * Cq;
     if (fabs(det) < 0.000000001) det = 0.000000001;
-    const double inv_det = 1.0 / det;
+    const double inv_det = fast_rcp(det);  // |det| >= 1e-9
     X[X_RELX + 2] = rel0;
     X[X_RELX + 3] = rel1;
     X[X_RELX + 0] = (Ee * Dq - B * Ff) * inv_det;
@@ -478,7 +492,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     // prepareTimeStep's section quantities (TdsModel.cpp:732-834), with the repeated
     // divisions folded into one reciprocal of the area and one of the wall surface.
     const double vol = area * len;
-    const double inv_area = 1.0 / area;
+    const double inv_area = fast_rcp(area);
     double alpha = 0.0, beta = 0.0;
     const double r0 = sqrt(area * (1.0 / PI));
     const double circ = 2.0 * PI * r0;
@@ -487,18 +501,18 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     if (a < rmin) { a = rmin; b = area * (glot ? 1.0 / (PI * 0.8) : 1.0 / (PI * 1.6)); }
     const double L = (RHO * 0.5 * len) * inv_area;
     const double Cc = vol * (1.0 / (RHO * CSND * CSND));
-    const double Rr = ((2.0 * MU * len) * (a * a + b * b)) / (PI * a * a * a * b * b * b);
+    const double Rr = fast_div((2.0 * MU * len) * (a * a + b * b), PI * a * a * a * b * b * b);
     if (opt.soft_walls && !glot) {
       double surf = circ * len;
       if (surf < AMIN) surf = AMIN;
-      const double inv_surf = 1.0 / surf;
+      const double inv_surf = fast_rcp(surf);
       double Rw = C.h.Bw_ph0 * inv_surf, Lw = C.h.Mw_ph0 * inv_surf;
-      alpha = 1.0 / (Lw * idt2 + Rw * idt + C.h.Kw_ph0 * inv_surf);
+      alpha = fast_rcp(Lw * idt2 + Rw * idt + C.h.Kw_ph0 * inv_surf);
       beta = alpha * (R.w[j] * (Lw * idt2 + Rw * idt) +
                       R.wr[j] * (Lw * (TH1 / TH + 1.0) * idt + Rw * (TH1 / TH)) +
                       R.wr2[j] * Lw * (TH1 / TH));
     }
-    const double E = dt * TH / (Cc + alpha);
+    const double E = fast_div(dt * TH, Cc + alpha);
     double R0 = Rr, R1 = Rr;
     // Bernoulli losses between pharynx/mouth sections (TdsModel.cpp:850-877)
     if (opt.turbulence_losses && s >= S_PHARYNX0 && s <= S_LAST_MOUTH) {
@@ -519,7 +533,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
       double sa = C.h.area_last_trachea, ta = area;
       double u = 0.0;
       u += R.u[j];
-      if (u > 0) R0 = R0 + 1.0 * 0.5 * RHO * fabs(u) * (1.0 / (ta * ta) - 1.0 / (sa * sa));
+      if (u > 0) R0 = R0 + 1.0 * 0.5 * RHO * fabs(u) * (fast_rcp(ta * ta) - fast_rcp(sa * sa));
       sa = ta;
       ta = X[X_AREA + 1];
       double bt = (ta < 1.0 * sa) ? 1.0 : 0.0;
@@ -527,7 +541,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
       X[X_GBF] = g;
       u = 0.0;
       u += X[X_U + S_GLOT_UP];
-      if (u > 0) R1 = R1 + g * fabs(u) * 0.5 * RHO * (1.0 / (ta * ta) - 1.0 / (sa * sa));
+      if (u > 0) R1 = R1 + g * fabs(u) * 0.5 * RHO * (fast_rcp(ta * ta) - fast_rcp(sa * sa));
     }
     R.al[j] = alpha;
     R.be[j] = beta;
@@ -598,11 +612,11 @@ AFS_HD inline void dipole_targets(Xc &x, double *X, const Uni &U, const Consts &
   if (M == 0) return;
   const int up = __builtin_ctzll(M);  // the first section that contains the obstacle
   const int dn = (up < NPM - 1) ? up + 1 : DIP_LIPS;
-  double fdn = (c.obst - X[X_POS + up]) / X[X_LEN + up];
+  double fdn = fast_div(c.obst - X[X_POS + up], X[X_LEN + up]);
   double fup = 1.0 - fdn;
   double A = X[X_AREA + c.narrow - DYN0];
   if (A < 0.1) A = 0.1;
-  const double inv_A = 1.0 / A;
+  const double inv_A = fast_rcp(A);
   double flow = 0.0;
   const Topo tn = C.topo[c.narrow];
   const int o0 = tn.out0, o1 = tn.out1;
@@ -845,9 +859,9 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
       double smp = 0.0;
       if ((act >> d) & 1) {
         double xi = (double)(int32_t)R.racc[k];
-        xi /= (double)2147483647;
+        xi *= 1.0 / 2147483647.0;  // constant reciprocals (within 1 ulp of the divisions)
         xi -= 6.0;
-        xi /= C.h.sqrt12;
+        xi *= 0.28867513459481288225;  // 1 / sqrt(12)
         double cut = R.dcut[k];
         double xx = (cut == 2000.0) ? C.h.noise_x_2000 : exp(-2.0 * PI * (cut * C.h.dt));
         double y = (1.0 - xx) * xi;
@@ -936,14 +950,14 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const
       R.rad_un[0] = X[X_UN + C.un_slot[rc]]; R.rad_un[1] = X[X_UN + C.un_slot[lc]];
       const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
       {
-        double Rrad = C.h.rrad_num / (9.0 * PI * PI * AB);
+        double Rrad = fast_div(C.h.rrad_num, 9.0 * PI * PI * AB);
         double F = LA2 * idt + RA2 + Rrad;
         double H = -(LA2 * idt) * (uR + uL) - (LA2 * (TH1 / TH)) * (uRr + uLr) + Sr;
         X[X_DIAG + rc] = -(-EB - F);
         X[X_RHS + rc] = -(H - DB);
       }
       {
-        double Lrad = C.h.lrad_num / (3.0 * PI * sqrt(AB * PI));
+        double Lrad = fast_div(C.h.lrad_num, 3.0 * PI * sqrt(AB * PI));
         double LAB2 = LA2 + Lrad;
         double G = LAB2 * idt + RA2;
         double H = -idt * (LA2 * uR + LAB2 * uL) - (TH1 / TH) * (LA2 * uRr + LAB2 * uLr) + Sr;

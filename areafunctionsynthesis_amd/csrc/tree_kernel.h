@@ -137,7 +137,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   const Consts &C = lds.C;
   GpuExec<PROF> ex{gl, &R};
   if constexpr (PROF) ex.last = __builtin_amdgcn_s_memtime();
-  const afs_frame *fu = a.frames + (int64_t)ue * a.frame_stride;
+  const afs_frame *fu = a.frames + (int64_t)(a.frame_row ? a.frame_row[ue] : ue) * a.frame_stride;
   double *o = a.out + (int64_t)ue * a.out_stride;
   int64_t t = 0;
   for (int k = a.k_begin; k < a.k_end; ++k) {

@@ -6,6 +6,9 @@
   an ``afs_session`` whose state stays on the GPU.
 * :meth:`Context.synthesize` -- whole trajectories (latch frame 0, then ``F-1`` calls of
   ``hop`` samples) for ``B`` utterances in one go.
+* :meth:`Context.play_target_sequences` -- ``Synthesizer::playTargetSequence``
+  (``src/Backend/Synthesizer.cpp:1299-1422``) for ``B`` utterances: four target shapes each,
+  per-sample area-function tubes built on the GPU.
 
 Arrays may be numpy arrays (host) or torch tensors on the GPU (device pointers are
 passed straight to the library).
@@ -132,6 +135,45 @@ class Context:
         return frames
 
 
+    def target_sequence_samples(self, timing: Optional[dict] = None) -> int:
+        """numSamples of playTargetSequence (``SAMPLING_RATE * totalTime_s``, truncated)."""
+        ts = target_sequence(timing)
+        return int(self._lib.afs_target_sequence_samples(ctypes.byref(ts), self.sampling_rate_hz))
+
+    def play_target_sequences(self, shapes, targets, timing: Optional[dict] = None, seeds=None, out=None,
+                              report: bool = False):
+        """``playTargetSequence(targetShape, stationary_s, transition_s)`` for every row of
+        ``targets[B, 4]`` (indices into ``shapes[S, 16]``) -> audio[B, T] float64.
+
+        ``timing`` overrides fields of :func:`target_sequence` (``stationary_s``,
+        ``transition_s``, ``f0_hz``, ``lung_pressure_dpa``, ``glottis``)."""
+        shapes = np.ascontiguousarray(shapes, dtype=np.float64)
+        targets = np.ascontiguousarray(targets, dtype=np.int32)
+        if shapes.ndim != 2 or shapes.shape[1] != 16 or targets.ndim != 2 or targets.shape[1] != 4:
+            raise ValueError("shapes must be [S, 16] and targets [B, 4]")
+        ts = target_sequence(timing)
+        B = targets.shape[0]
+        T = int(self._lib.afs_target_sequence_samples(ctypes.byref(ts), self.sampling_rate_hz))
+        if T < 0:
+            raise ValueError("bad target-sequence timing")
+        if seeds is None:
+            seeds = np.arange(1, B + 1, dtype=np.uint32)
+        if isinstance(seeds, np.ndarray):
+            seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        if out is None:
+            out = np.zeros((B, T), dtype=np.float64)
+        if _nbytes(out) != B * T * 8:
+            raise ValueError("out must hold B*T doubles")
+        rep = _native.AfsReport()
+        st = self._lib.afs_play_target_sequences(self._h, _vp(_addr(shapes)), shapes.shape[0], _vp(_addr(targets)),
+                                                 ctypes.byref(ts), _vp(_addr(seeds)), B, _vp(_addr(out)),
+                                                 ctypes.byref(rep))
+        _native.check(st, self._h, "afs_play_target_sequences")
+        if report:
+            return out, {"device_ms": rep.device_ms, "samples": rep.samples,
+                         "nonfinite_utterances": rep.nonfinite_utterances}
+        return out
+
     def to_int16(self, samples, out=None):
         """The reference's int16 audio ring format (Synthesizer.cpp:955-973) on the GPU:
         short(x * 32767) truncated, clipped outside [-1, 1], NaN -> 0."""
@@ -150,6 +192,26 @@ class Context:
         st = self._lib.afs_to_int16(self._h, _vp(_addr(samples)), n, _vp(_addr(out)))
         _native.check(st, self._h, "afs_to_int16")
         return out
+
+
+def target_sequence(overrides: Optional[dict] = None) -> "_native.AfsTargetSequence":
+    """afs_target_sequence with the reference's constants (afs_target_sequence_default) and
+    the given fields replaced."""
+    ts = _native.AfsTargetSequence()
+    _native.load().afs_target_sequence_default(ctypes.byref(ts))
+    for k, v in (overrides or {}).items():
+        if not hasattr(ts, k):
+            raise TypeError(f"unknown target-sequence field {k}")
+        cur = getattr(ts, k)
+        if isinstance(cur, float):
+            setattr(ts, k, float(v))
+        else:
+            vals = list(v)
+            if len(vals) != len(cur):
+                raise ValueError(f"{k} takes {len(cur)} values")
+            for i, x in enumerate(vals):
+                cur[i] = float(x)
+    return ts
 
 
 class Synthesizer:

@@ -11,6 +11,8 @@ kernel (``Context.af_to_frames``) or any other ``params -> frames`` function.
 * ``vcv``            config 3: V-C-V target sequences timed like
   Synthesizer::playTargetSequence (Synthesizer.cpp:1299-1422) and sampled at 100 Hz
   frames (Synthesizer::FRAME_RATE_HZ, Synthesizer.h:58).
+* ``vcv_targets``    config 3 as the reference actually plays it: four target shapes per
+  utterance for ``Context.play_target_sequences`` (per-sample tubes, hop 1).
 * ``fricatives``     config 5: fricative shapes with the velum open 1.0 cm^2
   (the GUI's default port area, MainPage.cpp:127-131), so the noise sources and the
   nasal side branch are active.
@@ -179,6 +181,24 @@ def vcv(B: int, fs: float = 44100.0, frame_rate: float = 100.0, first_utterance:
             glottis[u, k, 0] = f0
             glottis[u, k, 1] = pr
     return Workload("vcv", params, glottis, np.zeros((B, F)), hop, fs, _seeds(B, first_utterance))
+
+
+VCV_VOWELS = ("a:", "e:", "i:", "o:", "u:")
+VCV_CONSONANTS = ("b", "d", "g")
+
+
+def vcv_targets(B: int, first_utterance: int = 0, seed: int = BUILD_SEED + 3):
+    """Config 3 for Context.play_target_sequences: utterance u plays the targets
+    V, (V)C(V):, V, V (the reference's four-shape playTargetSequence) for V, C drawn per
+    utterance.  Returns (shapes[S, 16], targets[B, 4] int32, seeds[B] uint32)."""
+    sh = default_shapes()
+    names = list(VCV_VOWELS) + [f"({v[0]}){c}({v[0]}):" for v in VCV_VOWELS for c in VCV_CONSONANTS]
+    shapes = np.stack([sh[n] for n in names])
+    pick, _, _ = _rows(seed, first_utterance, B, len(VCV_VOWELS) * len(VCV_CONSONANTS))
+    vi, ci = pick // len(VCV_CONSONANTS), pick % len(VCV_CONSONANTS)
+    cons_row = len(VCV_VOWELS) + vi * len(VCV_CONSONANTS) + ci
+    targets = np.stack([vi, cons_row, vi, vi], axis=1).astype(np.int32)
+    return shapes, targets, _seeds(B, first_utterance)
 
 
 def build_frames(w: Workload, af_to_frames) -> np.ndarray:

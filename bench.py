@@ -39,8 +39,9 @@ def frame_bytes_per_sample(hop: int) -> float:
     return 1072.0 / hop + 8.0
 
 
-def cpu_baseline(frames: np.ndarray, seeds: np.ndarray, hop: int, fs: float, n_utt: int, gpu_out: np.ndarray):
-    """Time the reference build (oracle/_ref) on a bounded sample, one process per core."""
+def cpu_baseline(jobs, fs: float, n_utt: int, gpu_out: np.ndarray, what: str):
+    """Time the reference build (oracle/_ref) on a bounded sample, one process per core.
+    jobs[u] = ("frames", frames, seed, hop) or ("target", shapes4, seed, None)."""
     import multiprocessing as mp
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -48,7 +49,7 @@ def cpu_baseline(frames: np.ndarray, seeds: np.ndarray, hop: int, fs: float, n_u
 
     kind = "reference" if os.path.exists(REF_SO) else "port"
     cores = max(1, min(16, os.cpu_count() or 1, n_utt))
-    jobs = [(kind, frames[u], int(seeds[u]), hop, fs) for u in range(n_utt)]
+    jobs = [(kind,) + tuple(j) + (fs,) for j in jobs]
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
     with ctx.Pool(cores) as pool:
@@ -62,18 +63,19 @@ def cpu_baseline(frames: np.ndarray, seeds: np.ndarray, hop: int, fs: float, n_u
         "unit": "samples/s",
         "cores": cores,
         "kind": kind,
-        "sample": f"{n_utt} utterances x {frames.shape[1] - 1} frames x {hop} samples @ {fs:g} Hz "
-                  f"(first utterances of this shard), {cores} processes",
+        "sample": f"{n_utt} utterances ({what}) @ {fs:g} Hz (first utterances of this shard), {cores} processes",
         "wall_s": wall,
     }, max(errs), max(rmss)
 
 
 def _cpu_job(job):
-    kind, fr, seed, hop, fs = job
+    kind, what, data, seed, hop, fs = job
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import Oracle, RefLib
     lib = RefLib() if kind == "reference" else Oracle()
-    return lib.utterance(fr, hop, seed, fs)
+    if what == "target":  # playTargetSequence: per-sample area function -> tube, then n = 1 calls
+        return lib.utterance(Oracle().target_frames(data, fs), 1, seed, fs)
+    return lib.utterance(data, hop, seed, fs)
 
 
 def main() -> None:
@@ -87,6 +89,9 @@ def main() -> None:
     ap.add_argument("--solver", default=os.environ.get("AFS_SOLVER", "tree"))
     ap.add_argument("--cpu-utterances", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=("static", "vcv"), default="static",
+                    help="static: config-4 shard of static vowels (default); vcv: config-3 VCV "
+                         "utterances through playTargetSequence (per-sample tubes, hop 1)")
     args = ap.parse_args()
 
     import torch
@@ -104,7 +109,7 @@ def main() -> None:
     from areafunctionsynthesis_amd import sharding
     from areafunctionsynthesis_amd.frames import FRAME_DTYPE
     from areafunctionsynthesis_amd.synthesizer import Context
-    from areafunctionsynthesis_amd.workloads import build_frames, static_vowels
+    from areafunctionsynthesis_amd.workloads import build_frames, static_vowels, vcv_targets
 
     B = args.batch
     ctx = Context(args.fs, solver=args.solver, device=local, async_calls=True)
@@ -112,22 +117,33 @@ def main() -> None:
     ctx.set_stream(stream.cuda_stream)
 
     first, _ = sharding.shard_range(rank, world, B)
-    w = static_vowels(B, seconds=args.seconds, fs=args.fs, first_utterance=first)
-    frames = build_frames(w, ctx.af_to_frames)
-    F, hop, T = w.num_frames, w.hop, w.samples_per_utterance
-    frames_dev = torch.from_numpy(frames.view(np.uint8).reshape(B, F, FRAME_DTYPE.itemsize)).to(dev)
-    seeds_dev = torch.from_numpy(w.seeds.astype(np.int32)).to(dev)
-    out_dev = torch.empty((B, T), dtype=torch.float64, device=dev)
-
     max_launch_samples = 65536 if args.solver == "tree" else 8192
-    launches_per_step = -(-(F - 1) // max(1, max_launch_samples // hop))
+    if args.workload == "static":
+        w = static_vowels(B, seconds=args.seconds, fs=args.fs, first_utterance=first)
+        frames = build_frames(w, ctx.af_to_frames)
+        F, hop, T = w.num_frames, w.hop, w.samples_per_utterance
+        seeds = w.seeds
+        frames_dev = torch.from_numpy(frames.view(np.uint8).reshape(B, F, FRAME_DTYPE.itemsize)).to(dev)
+        launches_per_step = -(-(F - 1) // max(1, max_launch_samples // hop))
+
+        def synth():
+            ctx.synthesize(frames_dev, hop, seeds=seeds_dev, out=out_dev)
+    else:
+        shapes, targets, seeds = vcv_targets(B, first_utterance=first)
+        hop, T = 1, ctx.target_sequence_samples()
+        launches_per_step = -(-T // max_launch_samples)
+
+        def synth():
+            ctx.play_target_sequences(shapes, targets, seeds=seeds_dev, out=out_dev)
+    seeds_dev = torch.from_numpy(seeds.astype(np.int32)).to(dev)
+    out_dev = torch.empty((B, T), dtype=torch.float64, device=dev)
 
     # the reference's output format (int16, Synthesizer.cpp:955-973) is produced on the GPU
     # and gathered to rank 0 while the next step synthesizes
     pcm = sharding.PcmGather(lambda x, o: ctx.to_int16(x, out=o), (B, T), world, rank, dist, device=dev)
 
     def step():
-        ctx.synthesize(frames_dev, hop, seeds=seeds_dev, out=out_dev)
+        synth()
         pcm.submit(out_dev)
 
     for _ in range(args.warmup):
@@ -142,7 +158,7 @@ def main() -> None:
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        ctx.synthesize(frames_dev, hop, seeds=seeds_dev, out=out_dev)
+        synth()
         ev[k][1].record(stream)
         pcm.submit(out_dev)
     pcm.drain()
@@ -179,8 +195,11 @@ def main() -> None:
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"BASELINE config 4 shard: {B} static-vowel utterances/GPU x {args.seconds:g} s "
-                            f"@ {args.fs:g} Hz ({B * 8} at 8 GPUs), frames resident in HBM",
+                "workload": (f"BASELINE config 4 shard: {B} static-vowel utterances/GPU x {args.seconds:g} s "
+                             f"@ {args.fs:g} Hz ({B * 8} at 8 GPUs), frames resident in HBM")
+                if args.workload == "static" else
+                (f"BASELINE config 3 (fp64 state): {B} VCV utterances/GPU through playTargetSequence "
+                 f"({T} samples @ {args.fs:g} Hz, per-sample area-function tubes built on the GPU)"),
                 "batch_per_gpu": B,
                 "global_batch": B * world,
                 "samples_per_utterance": T,
@@ -209,7 +228,13 @@ def main() -> None:
         if world == 1 and not args.no_cpu_baseline:
             n = min(args.cpu_utterances, B)
             gpu_out = out_dev[:n].cpu().numpy()
-            cb, max_abs, max_rms = cpu_baseline(frames[:n], w.seeds[:n], hop, args.fs, n, gpu_out)
+            if args.workload == "static":
+                jobs = [("frames", frames[u], int(seeds[u]), hop) for u in range(n)]
+                what = f"{F - 1} frames x {hop} samples"
+            else:
+                jobs = [("target", shapes[targets[u]], int(seeds[u]), None) for u in range(n)]
+                what = f"playTargetSequence, {T} samples, trajectory built per sample on the CPU"
+            cb, max_abs, max_rms = cpu_baseline(jobs, args.fs, n, gpu_out, what)
             cb.pop("wall_s")
             result["cpu_baseline"] = cb
             result["max_abs_err_vs_cpu_ref"] = max_abs

@@ -21,6 +21,8 @@
  *   afs_options             <- TdsModel::Options (src/Backend/TdsModel.h:83-95)
  *   afs_to_int16            <- the int16 audio ring of Synthesizer::synthesizeSegment
  *                              (Synthesizer.cpp:955-973, Signal16 = short, Signal.h:19)
+ *   afs_play_target_sequences <- Synthesizer::playTargetSequence (Synthesizer.cpp:1299-1422)
+ *                              with interpolateParameters (:1286-1294), for B utterances
  *
  * Errors: the reference prints and continues (TdsModel.cpp:1832,1849,1898,2267); here every
  * call returns an afs_status and afs_last_error() holds a message.  Inputs are clamped exactly
@@ -143,6 +145,36 @@ afs_status afs_af_to_frames(afs_ctx *ctx, const double *params, int64_t n, afs_f
 /* Output format stage: out[i] = short(x * 32767) truncated towards zero, x > 1 -> 32767,
  * x < -1 -> -32768, NaN -> 0 (Synthesizer.cpp:955-973).  Host or device pointers. */
 afs_status afs_to_int16(afs_ctx *ctx, const double *samples, int64_t n, int16_t *out);
+
+/* Synthesizer::playTargetSequence(targetShape, stationary_s, transition_s)
+ * (Synthesizer.cpp:1299-1422).  The reference hard-codes f0_hz {100, 115, 105, 80} (:1311), the
+ * 8000 dPa lung pressure of sensorDataToGlottisParams (:903) and takes the other glottis controls
+ * from TriangularGlottis' control parameters after reset() (f0 120 Hz, 10000 dPa, rest
+ * displacements 0.01 cm, arytenoid area 0, aspiration -40 dB; TriangularGlottis.cpp:19-24,
+ * Synthesizer.cpp:244); afs_target_sequence_default() sets those and the SURVEY config-3
+ * timing (stationary 0.2/0.05/0.2/0.1 s, transitions 0.05 s). */
+typedef struct afs_target_sequence {
+  double stationary_s[4];
+  double transition_s[3];
+  double f0_hz[4];
+  double lung_pressure_dpa;
+  double glottis[AFS_NUM_GLOTTIS_PARAMS];  /* init() latch; [2..5] also for every sample */
+} afs_target_sequence;
+
+void afs_target_sequence_default(afs_target_sequence *ts);
+/* int numSamples = SAMPLING_RATE * totalTime_s (:1328), with the context's rate. */
+int64_t afs_target_sequence_samples(const afs_target_sequence *ts, double sampling_rate_hz);
+
+/* B utterances, utterance b playing the four shapes targets[4 b .. 4 b + 3] of the shape
+ * table shapes[num_shapes][16] (host pointers) with one timing for the batch.  Semantics of the
+ * reference per utterance: reset + srand(seeds[b]) (NULL: b + 1), init() latches the schwa
+ * tube, then one synthesizeSignalTds(tube_i, glottis_i, 1) per sample, where tube_i comes from
+ * the area-function model at the cosine-interpolated parameters of sample i (teeth at xin).
+ * out[B][afs_target_sequence_samples()] doubles, host or device.  Tube trajectories are built
+ * on the GPU once per distinct target sequence and streamed in time chunks. */
+afs_status afs_play_target_sequences(afs_ctx *ctx, const double *shapes, int32_t num_shapes,
+                                     const int32_t *targets, const afs_target_sequence *ts,
+                                     const uint32_t *seeds, int32_t B, double *out, afs_report *report);
 
 #ifdef __cplusplus
 }

@@ -1011,6 +1011,115 @@ void ao_af_to_frame(const double *p, ao_frame *f) {
   f->teeth_position_cm = p[P_XIN];
 }
 
+/* ---- Synthesizer::playTargetSequence (Synthesizer.cpp:1299-1422) --------------------- */
+
+/* OneDimAreaFunction::reset, the schwa shape init() latches (OneDimAreaFunction.cpp:281-350). */
+static const double AO_SCHWA[16] = {2.0, 1.0, 1.0, 3.02, 5.609, 1.0, 5.92, 2.879, 1.0, 8.48, 4.238, 1.0,
+                                    15.31, 0.701, 16.44, 1.65};
+
+void ao_target_default(ao_target_cfg *c) {
+  static const double st[4] = {0.2, 0.05, 0.2, 0.1}, tr[3] = {0.05, 0.05, 0.05};
+  static const double f0[4] = {100, 115, 105, 80};               /* Synthesizer.cpp:1311 */
+  static const double g[6] = {120.0, 10000.0, 0.01, 0.01, 0.0, -40.0}; /* controlParam after reset() */
+  memcpy(c->stationary_s, st, sizeof st);
+  memcpy(c->transition_s, tr, sizeof tr);
+  memcpy(c->f0_hz, f0, sizeof f0);
+  c->lung_pressure_dpa = 8000.0;                                   /* sensorDataToGlottisParams :903 */
+  memcpy(c->glottis, g, sizeof g);
+}
+
+/* boundary_s[0..6] of :1318-1326, summed left to right as the reference writes them. */
+static void ao_target_bounds(const ao_target_cfg *c, double *b) {
+  const double *s = c->stationary_s, *t = c->transition_s;
+  b[0] = s[0];
+  b[1] = s[0] + t[0];
+  b[2] = s[0] + t[0] + s[1];
+  b[3] = s[0] + t[0] + s[1] + t[1];
+  b[4] = s[0] + t[0] + s[1] + t[1] + s[2];
+  b[5] = s[0] + t[0] + s[1] + t[1] + s[2] + t[2];
+  b[6] = s[0] + t[0] + s[1] + t[1] + s[2] + t[2] + s[3];
+}
+
+long ao_target_num_samples(const ao_target_cfg *c, double fs) {
+  double b[7];
+  ao_target_bounds(c, b);
+  return (long)(int)(fs * b[6]);  /* int numSamples = SAMPLING_RATE * totalTime_s (:1328) */
+}
+
+/* interpolateParameters (:1286-1294) */
+static void ao_interp(const double *p0, const double *p1, double *px, double t0, double t1, double tx) {
+  for (int i = 0; i < 16; ++i)
+    px[i] = (p1[i] - p0[i]) / 2 * cos((t1 - tx) / (t1 - t0) * M_PI) + (p1[i] + p0[i]) / 2;
+}
+
+/* The lung-pressure statements of :1333-1346 and :1399-1403 for sample i (before the
+ * fade-out check). */
+static double ao_fade_in(double P, double fs, long i) {
+  if (i < (double)0.05 * (double)fs) return 0.0;
+  return P / 2 * cos((0.1 * fs - i) / (0.05 * fs) * M_PI) + P / 2;
+}
+
+static double ao_pressure(const ao_target_cfg *c, double fs, double total, long i) {
+  const double P = c->lung_pressure_dpa;
+  double v;
+  if (i < (double)0.1 * (double)fs) {
+    v = ao_fade_in(P, fs, i);
+  } else {
+    /* held: the value the last sample below 0.1 fs set, or P if none did */
+    long j = (long)ceil((double)0.1 * (double)fs);  /* the largest j with j < 0.1 fs */
+    while (j >= 0 && !(j < (double)0.1 * (double)fs)) --j;
+    while ((double)(j + 1) < (double)0.1 * (double)fs) ++j;
+    v = (j >= 0) ? ao_fade_in(P, fs, j) : P;
+  }
+  if (i > (double)(total - 0.1) * (double)fs)  /* the reference's fade-out, denominator as written */
+    v = -P / 2 * cos((total * fs - i) / (total - 0.1 * fs) * M_PI) + P / 2;
+  return v;
+}
+
+static double ao_f0(const ao_target_cfg *c, const double *b, double fs, long i) {
+  const double *f = c->f0_hz;
+  if (i < (double)b[1] * fs)
+    return (f[0] + f[1]) / 2 + (f[1] - f[0]) / 2 * cos((b[1] * fs - i) / (b[1] * fs) * M_PI);
+  if (i < (double)b[3] * fs)
+    return (f[2] + f[1]) / 2 + (f[2] - f[1]) / 2 * cos((b[3] * fs - i) / ((b[3] - b[1]) * fs) * M_PI);
+  return (f[3] + f[2]) / 2 + (f[3] - f[2]) / 2 * cos((b[6] * fs - i) / ((b[6] - b[3]) * fs) * M_PI);
+}
+
+/* currentParams of sample i (:1364-1397); shapes = 4 x 16 targets. */
+static void ao_target_params(const double *shapes, const double *b, double fs, long i, double *p) {
+  const double *s0 = shapes, *s1 = shapes + 16, *s2 = shapes + 32, *s3 = shapes + 48;
+  if (i <= b[0] * fs) memcpy(p, s0, 16 * sizeof(double));
+  else if (i <= b[1] * fs) ao_interp(s0, s1, p, b[0] * fs, b[1] * fs, i);
+  else if (i <= b[2] * fs) memcpy(p, s1, 16 * sizeof(double));
+  else if (i <= b[3] * fs) ao_interp(s1, s2, p, b[2] * fs, b[3] * fs, i);
+  else if (i <= b[4] * fs) memcpy(p, s2, 16 * sizeof(double));
+  else if (i <= b[5] * fs) ao_interp(s2, s3, p, b[4] * fs, b[5] * fs, i);
+  else memcpy(p, s3, 16 * sizeof(double));  /* i <= b[6] fs for every i < numSamples */
+}
+
+void ao_target_frames(const double *shapes, const ao_target_cfg *c, double fs, long k0, long n, ao_frame *out) {
+  double b[7];
+  ao_target_bounds(c, b);
+  for (long k = 0; k < n; ++k) {
+    const long g = k0 + k;
+    ao_frame *f = out + k;
+    memset(f, 0, sizeof *f);
+    if (g == 0) {  /* init(): the schwa tube and the glottis parameters of reset() */
+      ao_af_to_frame(AO_SCHWA, f);
+      for (int q = 0; q < 6; ++q) f->glottis[q] = c->glottis[q];
+    } else {       /* sample i = g - 1: synthesizeSignalTds(tube_i, glottis_i, 1) */
+      const long i = g - 1;
+      double p[16];
+      ao_target_params(shapes, b, fs, i, p);
+      ao_af_to_frame(p, f);
+      f->glottis[0] = ao_f0(c, b, fs, i);
+      f->glottis[1] = ao_pressure(c, fs, b[6], i);
+      for (int q = 2; q < 6; ++q) f->glottis[q] = c->glottis[q];
+    }
+    f->velum_opening_cm2 = 0.0;  /* the Synthesizer's tube keeps Tube()'s closed velum */
+  }
+}
+
 /* Synthesizer.cpp:955-973: audioBuffer->setValue(pos, newSignal[i] * SHRT_MAX) stores into
  * a Signal16 (signed short), then the two clipping branches overwrite out-of-range values. */
 void ao_to_int16(const double *x, long n, int16_t *out) {

@@ -15,13 +15,16 @@
  *                                             reference calls rand() at
  *                                             src/Backend/TdsModel.cpp:1690-1692)
  *   OneDimAreaFunction (area fn -> tube)      src/Backend/OneDimAreaFunction.cpp:23-138
+ *   Synthesizer::playTargetSequence           src/Backend/Synthesizer.cpp:1286-1422
+ *   int16 output ring                         src/Backend/Synthesizer.cpp:955-973
  *
  * Parity pin: the restatement is checked bit-for-bit against oracle/_ref, a build of
  * the reference's own TdsModel/Tube/TriangularGlottis/IirFilter sources driven by
  * oracle/ref_harness.cpp (tests/test_oracle_vs_ref.py), and against the committed
  * golden vectors in tests/golden/ that the same reference build produced.
- * OneDimAreaFunction is not buildable from the reference (it needs wxWidgets'
- * generated setup.h); that row is pinned by the restatement and its tests only.
+ * OneDimAreaFunction and Synthesizer.cpp are not buildable from the reference (wxWidgets /
+ * portaudio); the area-function and target-sequence rows are pinned by the restatement
+ * and its tests only.
  */
 #ifndef AFS_ORACLE_H
 #define AFS_ORACLE_H
@@ -94,6 +97,22 @@ int32_t ao_rng_next(ao_rng *g);
  * Velum and glottis fields are left untouched. */
 void ao_af_to_frame(const double params16[16], ao_frame *f);
 double ao_af_area(const double params16[16], double x_cm);
+
+/* Synthesizer::playTargetSequence (Synthesizer.cpp:1299-1422) as a hop-1 frame trajectory:
+ * frame 0 is init()'s latch (the schwa of OneDimAreaFunction::reset and reset()'s glottis
+ * parameters), frame k >= 1 holds sample k-1's tube (interpolateParameters, cosine) and
+ * glottis controls (F0 contour, lung-pressure fade-in/hold/fade-out as written).  Sample i
+ * of the utterance is synthesizeSignalTds(frame i+1, ..., 1), i.e. it plays frame i. */
+typedef struct ao_target_cfg {
+  double stationary_s[4];
+  double transition_s[3];
+  double f0_hz[4];
+  double lung_pressure_dpa;
+  double glottis[6];
+} ao_target_cfg;
+void ao_target_default(ao_target_cfg *c);
+long ao_target_num_samples(const ao_target_cfg *c, double fs);
+void ao_target_frames(const double *shapes4x16, const ao_target_cfg *c, double fs, long k0, long n, ao_frame *out);
 
 /* IirFilter::createChebyshev (IirFilter.cpp:286-432): a[0..order], b[0..order]. */
 int ao_chebyshev(double cutoff_ratio, int highpass, int poles, double *a, double *b);

@@ -3,6 +3,7 @@
 Run in the build container (needs /root/reference for oracle/_ref):
     python tests/golden/make_golden.py          (all files)
     python tests/golden/make_golden.py int16    (int16.npz only)
+    python tests/golden/make_golden.py target_seq (target_seq.npz only)
 
 Every expected value comes from oracle/_ref/libafsref.so -- the reference's own
 TdsModel / Tube / TriangularGlottis / IirFilter sources compiled unmodified and driven
@@ -65,9 +66,29 @@ def write_int16(ref: RefLib) -> None:
     np.savez_compressed(os.path.join(HERE, "int16.npz"), x=x, out=ref.to_int16(x))
 
 
+def write_target_seq(o: Oracle, ref: RefLib) -> None:
+    """playTargetSequence (Synthesizer.cpp:1299-1422): the trajectory frames come from the
+    restatement (Synthesizer.cpp is not buildable here), the audio from the reference build
+    playing them with one synthesizeSignalTds(.., 1) call per sample."""
+    sh = default_shapes()
+    names = ["a:", "(a)b(a):", "u:", "(u)g(u):", "i:", "(i)d(i):"]
+    shapes = np.stack([sh[n] for n in names])
+    targets = np.array([[0, 1, 0, 0], [2, 3, 2, 2], [4, 5, 4, 4], [1, 0, 5, 2]], dtype=np.int32)
+    seeds = np.array([1, 2, 3, 11], dtype=np.uint32)
+    st, tr, fs = [0.02, 0.01, 0.02, 0.01], [0.01, 0.01, 0.01], 44100.0
+    timing = {"stationary_s": st, "transition_s": tr}
+    outs = [ref.utterance(o.target_frames(shapes[t], fs, timing), 1, int(s), fs) for t, s in zip(targets, seeds)]
+    np.savez_compressed(os.path.join(HERE, "target_seq.npz"), names=np.array(names), shapes=shapes,
+                        targets=targets, seeds=seeds, stationary_s=np.array(st), transition_s=np.array(tr),
+                        fs=fs, out=np.stack(outs))
+
+
 def main() -> None:
     if sys.argv[1:] == ["int16"]:
         write_int16(RefLib())
+        return
+    if sys.argv[1:] == ["target_seq"]:
+        write_target_seq(Oracle(), RefLib())
         return
     o = Oracle()
     r = RefLib()
@@ -139,6 +160,7 @@ def main() -> None:
                         area=F["area_cm2"], length=F["length_cm"], articulator=F["articulator"],
                         teeth=F["teeth_position_cm"], source=np.array("restatement"))
     write_int16(r)
+    write_target_seq(o, r)
     print("golden vectors written to", HERE)
 
 

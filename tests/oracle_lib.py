@@ -49,6 +49,12 @@ def option_vector(opt: dict):
     return [int(bool(opt.get(n, d))) for n, d in zip(OPTION_NAMES, OPTION_DEFAULTS)]
 
 
+class TargetCfg(ctypes.Structure):
+    _fields_ = [("stationary_s", ctypes.c_double * 4), ("transition_s", ctypes.c_double * 3),
+                ("f0_hz", ctypes.c_double * 4), ("lung_pressure_dpa", ctypes.c_double),
+                ("glottis", ctypes.c_double * 6)]
+
+
 class Oracle:
     """Restatement: one utterance at a time (batch 1), fp64."""
 
@@ -80,7 +86,44 @@ class Oracle:
         lib.ao_chebyshev.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int, _vp, _vp]
         lib.ao_chebyshev.restype = ctypes.c_int
         lib.ao_to_int16.argtypes = [_vp, ctypes.c_long, _vp]
+        lib.ao_target_default.argtypes = [ctypes.POINTER(TargetCfg)]
+        lib.ao_target_default.restype = None
+        lib.ao_target_num_samples.argtypes = [ctypes.POINTER(TargetCfg), ctypes.c_double]
+        lib.ao_target_num_samples.restype = ctypes.c_long
+        lib.ao_target_frames.argtypes = [_vp, ctypes.POINTER(TargetCfg), ctypes.c_double, ctypes.c_long,
+                                         ctypes.c_long, _vp]
+        lib.ao_target_frames.restype = None
         self.lib = lib
+
+    # Synthesizer::playTargetSequence ------------------------------------------
+    def target_cfg(self, timing=None) -> "TargetCfg":
+        c = TargetCfg()
+        self.lib.ao_target_default(ctypes.byref(c))
+        for k, v in (timing or {}).items():
+            cur = getattr(c, k)
+            if isinstance(cur, float):
+                setattr(c, k, float(v))
+            else:
+                for i, x in enumerate(v):
+                    cur[i] = float(x)
+        return c
+
+    def target_num_samples(self, fs: float, timing=None) -> int:
+        return int(self.lib.ao_target_num_samples(ctypes.byref(self.target_cfg(timing)), fs))
+
+    def target_frames(self, shapes4, fs: float, timing=None, k0: int = 0, n=None) -> np.ndarray:
+        """Frames k0 .. k0+n-1 of the hop-1 trajectory (frame 0 = init() latch)."""
+        c = self.target_cfg(timing)
+        if n is None:
+            n = int(self.lib.ao_target_num_samples(ctypes.byref(c), fs)) + 1 - k0
+        s = np.ascontiguousarray(shapes4, dtype=np.float64).reshape(64)
+        out = np.zeros(n, dtype=FRAME_DTYPE)
+        self.lib.ao_target_frames(_ptr(s), ctypes.byref(c), fs, k0, n, _ptr(out))
+        return out
+
+    def target_sequence(self, shapes4, seed: int, fs: float, timing=None) -> np.ndarray:
+        """playTargetSequence's audio: the trajectory frames played with hop 1."""
+        return self.utterance(self.target_frames(shapes4, fs, timing), 1, seed, fs)
 
     def to_int16(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float64)

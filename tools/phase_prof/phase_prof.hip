@@ -51,7 +51,7 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   CK(hipMalloc(&dlanes, (size_t)B * TW * tree_lane_bytes()));
   CK(hipMalloc(&dprof, sizeof(uint64_t) * waves * PH_COUNT));
   CK(launch_tree_reset(dlanes, dlds, B, ds, nullptr));
-  TreeArgs a{dt, df, F, 1, F, hop, dout, (int64_t)(F - 1) * hop, dlanes, dlds, B, ht->uni};
+  TreeArgs a{dt, df, F, nullptr, 1, F, hop, dout, (int64_t)(F - 1) * hop, dlanes, dlds, B, ht->uni};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
