@@ -178,6 +178,7 @@ typedef struct topo {
   int cin[NS], cout0[NS], cout1[NS];
   int env_n[NC], env[NC][ENV_MAX];
   int col_n[NC], col[NC][COL_MAX];
+  int row_n[NC], row[NC][16];  /* filledRowIndex (TdsModel.cpp:340-357): ascending, <= 16 */
 } topo;
 
 static const int SINUS_COUPLE[4] = {8, 9, 11, 12}; /* Tube.cpp:35-38 */
@@ -212,6 +213,9 @@ static void topo_build(topo *t) {
       if (t->cout0[s] != -1) nz[c][t->cout0[s]] = 1;
       if (t->cout1[s] != -1) nz[c][t->cout1[s]] = 1;
     }
+    t->row_n[c] = 0;
+    for (int j = 0; j < NC; ++j)
+      if (nz[c][j] && j != c && t->row_n[c] < 16) t->row[c][t->row_n[c]++] = j;
     t->env_n[c] = 0;
     int inside = 0;
     for (int j = 0; j < c; ++j) {
@@ -268,9 +272,12 @@ struct ao_synth {
   double teeth_tds, asp_tds;
   int position;
   iir tone;            /* glottalToneFilter */
+  iir tglot;           /* transglottalPressureFilter (VARIABLE_ENTRANCE_LOSS) */
+  iir tvel1, tvel2;    /* transvelarCouplingFilter1/2 */
   iir outf;            /* Synthesizer::outputPressureFilter */
   double flow_ring[256];
   double sol[NC], flowv[NC];
+  int sor_iterations;
   double fac[NC][NC];
   double mat[NC][NC];
 };
@@ -282,6 +289,25 @@ void ao_default_options(ao_options *o) {
   o->radiation_from_skin = 1;
   o->piriform_fossa = 0;
   o->inner_length_corrections = 1;
+  o->transvelar_coupling = 0;
+  o->glottis_loss = 0;
+  o->solver = 0;
+  o->flow_separation_area_ratio = 1.0;
+}
+
+/* getGlottalEntranceLossCoeffFlucher2011(pressure, d), TdsModel.cpp:1048-1092. */
+double ao_fulcher_kent(double pressure_dPa, double d_cm) {
+  double pc = pressure_dPa / 979.7;
+  double D = d_cm;
+  if (pc < 0.001) pc = 0.001;
+  if (D < 0.001) D = 0.001;
+  double logD = log10(D);
+  double a = pow(10, 0.7953 * logD * logD + 1.4741 * logD + 0.6529);
+  double b = -0.7427 * logD * logD + -1.6209 * logD + -0.875;
+  double k = a * pow(pc, b);
+  if (k < 0.6) k = 0.6;
+  if (k > 18.0) k = 18.0;
+  return k;
 }
 
 /* Static parts of the tube: Tube.cpp:79-260 (trachea, nose, sinuses, fossa) and
@@ -677,22 +703,35 @@ static void tds_prepare(ao_synth *s) {
   if (!s->opt.piriform_fossa)
     s->R0[S_FOSSA0] = 8.0 * MU * s->len[S_FOSSA0] * M_PI / (AMIN * AMIN);
 
+  /* glottal entrance loss, TdsModel.cpp:898-911 (+ :1019-1039 for the variable option) */
   double kent = 1.0;
+  if (s->opt.glottis_loss == 1) kent = 1.375;
+  else if (s->opt.glottis_loss == 2) {
+    double tp = s->p[S_LAST_TRACHEA] - s->p[S_PHARYNX0];
+    double ftp = iir_run(&s->tglot, tp);
+    kent = ao_fulcher_kent(ftp, s->area[S_GLOT_LO] / 1.25);
+  }
   double sa = s->area[S_LAST_TRACHEA], ta = s->area[S_GLOT_LO];
   double u = cur_in(s, S_GLOT_LO);
   if (u > 0) s->R0[S_GLOT_LO] += kent * 0.5 * RHO * fabs(u) * (1.0 / (ta * ta) - 1.0 / (sa * sa));
   sa = s->area[S_GLOT_LO];
   ta = s->area[S_GLOT_UP];
   double bt = 0.0;
-  if (ta < 1.0 * sa) bt = 1.0;
+  if (ta < s->opt.flow_separation_area_ratio * sa) bt = 1.0;
   s->gbf = 0.8 * s->gbf + (1.0 - 0.8) * bt;
   u = cur_out(s, S_GLOT_LO);
   if (u > 0) s->R1[S_GLOT_LO] += s->gbf * fabs(u) * 0.5 * RHO * (1.0 / (ta * ta) - 1.0 / (sa * sa));
 
   if (s->opt.generate_noise_sources) noise_sources(s);
 
+  /* transvelar coupling, TdsModel.cpp:966-980 */
+  double tvflow = 0.0;
+  if (s->opt.transvelar_coupling)
+    tvflow = iir_run(&s->tvel1, s->p[S_MOUTH0 + 2]) + iir_run(&s->tvel2, s->p[S_NOSE0 + 2]);
+
   for (int i = 0; i < NS; ++i) {
-    double src = 0.0; /* monopole sample; transvelar / flow source disabled */
+    double src = 0.0; /* monopole sample (never active); flow source disabled */
+    if (i == S_NOSE0 + 2) src += tvflow;
     double d = dt * TH / (s->C[i] + s->alpha[i]);
     s->E[i] = d;
     s->D[i] = s->p[i] + dt * TH1 * s->pr[i] - d * (s->beta[i] - src);
@@ -820,6 +859,43 @@ static void tds_cholesky(ao_synth *s, double M[NC][NC]) {
   }
 }
 
+/* solveEquationsSor, TdsModel.cpp:2105-2180: SOR with OMEGA 1.25 from a zero start vector,
+ * at most 100 sweeps while the residual norm exceeds 0.1; rows swept from the last to the
+ * first, each row's off-diagonal terms from the highest column down; currents of closed
+ * sections (area <= 1.01 MIN_AREA) are not computed. */
+static void tds_sor(ao_synth *s, double M[NC][NC]) {
+  const topo *t = &s->T;
+  int active[NC];
+  for (int i = 0; i < NC; ++i) active[i] = 1;
+  for (int i = 0; i < NS; ++i) {
+    if (s->area[i] <= 1.01 * AMIN) {
+      if (t->cin[i] != -1) active[t->cin[i]] = 0;
+      if (t->cout0[i] != -1) active[t->cout0[i]] = 0;
+      if (t->cout1[i] != -1) active[t->cout1[i]] = 0;
+    }
+  }
+  double *x = s->flowv;
+  for (int i = 0; i < NC; ++i) x[i] = 0.0;
+  int it = 0;
+  double res;
+  do {
+    res = 0.0;
+    for (int i = NC - 1; i >= 0; --i) {
+      if (!active[i]) continue;
+      double sum = M[i][i] * x[i];
+      for (int k = t->row_n[i] - 1; k >= 0; --k) {
+        int j = t->row[i][k];
+        sum += x[j] * M[i][j];
+      }
+      double d = s->sol[i] - sum;
+      res += d * d;
+      x[i] += 1.25 * d / M[i][i];
+    }
+    it++;
+  } while (it < 100 && res > 0.1 * 0.1);
+  s->sor_iterations = it;
+}
+
 /* updateVariables, TdsModel.cpp:2046-2098. */
 static void tds_update(ao_synth *s) {
   const double dt = s->dt;
@@ -847,7 +923,8 @@ static double tds_step(ao_synth *s) {
   tds_prepare(s);
   memset(s->mat, 0, sizeof s->mat);
   tds_matrix(s, s->mat, s->sol);
-  tds_cholesky(s, s->mat);
+  if (s->opt.solver == 1) tds_sor(s, s->mat);
+  else tds_cholesky(s, s->mat);
   tds_update(s);
   double f = 0.0;
   int t0 = S_LAST_MOUTH, t1 = S_LAST_NOSE;
@@ -881,6 +958,22 @@ ao_synth *ao_create(double fs_hz, uint32_t seed, const ao_options *opt) {
   s->tone.order = 4;
   for (int i = 0; i <= 4; ++i) { s->tone.a[i] = TA[i]; s->tone.b[i] = TB[i]; }
   iir_reset(&s->tone);
+  /* transglottalPressureFilter (TdsModel.cpp:474, 50 Hz Chebyshev at the simulation rate) and
+   * the transvelar coupling filters H1, H2 (:488-533) */
+  iir_clear(&s->tglot);
+  chebyshev_design(50.0 / fs_hz, 0, 4, s->tglot.a, s->tglot.b, &s->tglot.order);
+  iir_reset(&s->tglot);
+  static const double VA2[5] = {6.589309727087047e-004, -0.001972281980771, 0.001968000742164,
+                                -6.546497341015677e-004, 0.0};
+  iir_clear(&s->tvel1);
+  iir_clear(&s->tvel2);
+  s->tvel1.order = s->tvel2.order = 4;
+  for (int i = 0; i <= 4; ++i) {
+    s->tvel1.a[i] = TA[i]; s->tvel1.b[i] = TB[i];
+    s->tvel2.a[i] = VA2[i]; s->tvel2.b[i] = TB[i];
+  }
+  iir_reset(&s->tvel1);
+  iir_reset(&s->tvel2);
   iir_clear(&s->outf);
   chebyshev_design(7000.0 / fs_hz, 0, 8, s->outf.a, s->outf.b, &s->outf.order);
   iir_reset(&s->outf);

@@ -60,7 +60,14 @@ typedef struct ao_options {
   int radiation_from_skin;      /* 1 */
   int piriform_fossa;           /* 0 */
   int inner_length_corrections; /* 1 */
+  int transvelar_coupling;      /* 0 */
+  int glottis_loss;             /* 0 STANDARD, 1 VAN_DEN_BERG, 2 VARIABLE (Fulcher 2011) */
+  int solver;                   /* 0 CHOLESKY_FACTORIZATION, 1 SOR_GAUSS_SEIDEL */
+  double flow_separation_area_ratio; /* 1.0 */
 } ao_options;
+
+/* getGlottalEntranceLossCoeffFlucher2011(pressure_dPa, d_cm) (TdsModel.cpp:1048-1092). */
+double ao_fulcher_kent(double pressure_dPa, double d_cm);
 
 void ao_default_options(ao_options *o);
 

@@ -17,7 +17,10 @@
 #include <climits>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+
+#include <unistd.h>
 
 #include "IirFilter.h"
 #include "TdsModel.h"
@@ -53,6 +56,11 @@ struct RefVoice {
     tds.timeStep = 1.0 / fs_hz;
     outputPressureFilter.createChebyshev(7000.0 / fs_hz, false, 8);
     tds.resetMotion();        // Synthesizer::reset, Synthesizer.cpp:231-250
+    // resetMotion designs the transglottal-pressure low-pass at 50 Hz / TDS_SAMPLING_RATE
+    // (TdsModel.cpp:474); at a run-time rate it is redesigned for that rate, as the
+    // reference compiled with SAMPLING_RATE = fs would (identical at 22050 Hz).
+    tds.transglottalPressureFilter.createChebyshev(50.0 / fs_hz, false, 4);
+    tds.transglottalPressureFilter.resetBuffers();
     glottis.resetMotion();
     outputPressureFilter.resetBuffers();
     srand(seed);
@@ -138,19 +146,24 @@ void afsref_currents(void *v, double *u) {
 long afsref_rand_calls(void) { return g_rand_calls; }
 
 // One utterance end to end: latch frames[0], then (F-1) calls of hop samples.
-// opt6 (optional): turbulence losses, soft walls, noise sources, radiation from skin,
-// piriform fossa, inner length corrections -- TdsModel::Options (TdsModel.h:83-95).
+// opt (optional): every field of TdsModel::Options (TdsModel.h:83-95), in ao_options layout.
 long afsref_utterance_opt(const ao_frame *frames, int F, int hop, unsigned seed, double fs, double *out,
-                          const int *opt6) {
+                          const ao_options *opt) {
   RefVoice *v = new RefVoice(fs, seed);
-  if (opt6) {
+  if (opt) {
     TdsModel::Options &o = v->tds.options;
-    o.turbulenceLosses = opt6[0] != 0;
-    o.softWalls = opt6[1] != 0;
-    o.generateNoiseSources = opt6[2] != 0;
-    o.radiationFromSkin = opt6[3] != 0;
-    o.piriformFossa = opt6[4] != 0;
-    o.innerLengthCorrections = opt6[5] != 0;
+    o.turbulenceLosses = opt->turbulence_losses != 0;
+    o.softWalls = opt->soft_walls != 0;
+    o.generateNoiseSources = opt->generate_noise_sources != 0;
+    o.radiationFromSkin = opt->radiation_from_skin != 0;
+    o.piriformFossa = opt->piriform_fossa != 0;
+    o.innerLengthCorrections = opt->inner_length_corrections != 0;
+    o.transvelarCoupling = opt->transvelar_coupling != 0;
+    o.glottisLossOption = opt->glottis_loss == 1   ? TdsModel::ENTRANCE_LOSS_VAN_DEN_BERG
+                          : opt->glottis_loss == 2 ? TdsModel::VARIABLE_ENTRANCE_LOSS
+                                                   : TdsModel::STANDARD_ENTRANCE_LOSS;
+    o.flowSeparationAreaRatio = opt->flow_separation_area_ratio;
+    o.solverType = opt->solver == 1 ? TdsModel::SOR_GAUSS_SEIDEL : TdsModel::CHOLESKY_FACTORIZATION;
   }
   long n = 0;
   v->call(&frames[0], hop, nullptr);
@@ -165,6 +178,28 @@ long afsref_utterance(const ao_frame *frames, int F, int hop, unsigned seed, dou
   v->call(&frames[0], hop, nullptr);
   for (int k = 1; k < F; ++k) n += v->call(&frames[k], hop, out + n);
   delete v;
+  return n;
+}
+
+// The reference's own Fulcher et al. (2011) Table I printout
+// (TdsModel::checkGlottalEntranceLossCoeffFlucher2011, TdsModel.cpp:1100-1181), captured from
+// stdout into buf.  Returns the number of bytes.
+int afsref_fulcher_table(char *buf, int cap) {
+  TdsModel tds;
+  fflush(stdout);
+  int fds[2];
+  if (pipe(fds) != 0) return -1;
+  int saved = dup(1);
+  dup2(fds[1], 1);
+  tds.checkGlottalEntranceLossCoeffFlucher2011();
+  fflush(stdout);
+  dup2(saved, 1);
+  close(saved);
+  close(fds[1]);
+  int n = 0, r;
+  while (n < cap - 1 && (r = (int)read(fds[0], buf + n, (size_t)(cap - 1 - n))) > 0) n += r;
+  close(fds[0]);
+  buf[n] = 0;
   return n;
 }
 

@@ -83,7 +83,17 @@ def write_target_seq(o: Oracle, ref: RefLib) -> None:
                         fs=fs, out=np.stack(outs))
 
 
+def write_fulcher(ref: RefLib) -> None:
+    """The reference's own printout of Fulcher et al. (2011) Table I
+    (TdsModel::checkGlottalEntranceLossCoeffFlucher2011, TdsModel.cpp:1100-1181)."""
+    with open(os.path.join(HERE, "fulcher_table.txt"), "w") as fh:
+        fh.write(ref.fulcher_table())
+
+
 def main() -> None:
+    if sys.argv[1:] == ["fulcher"]:
+        write_fulcher(RefLib())
+        return
     if sys.argv[1:] == ["int16"]:
         write_int16(RefLib())
         return
@@ -160,6 +170,7 @@ def main() -> None:
                         area=F["area_cm2"], length=F["length_cm"], articulator=F["articulator"],
                         teeth=F["teeth_position_cm"], source=np.array("restatement"))
     write_int16(r)
+    write_fulcher(r)
     write_target_seq(o, r)
     print("golden vectors written to", HERE)
 

@@ -37,16 +37,30 @@ def build_oracle() -> None:
 
 
 # TdsModel::Options (TdsModel.h:83-95) in afs_options / ao_options order, with defaults
-OPTION_NAMES = ("turbulence_losses", "soft_walls", "generate_noise_sources", "radiation_from_skin",
-                "piriform_fossa", "inner_length_corrections")
-OPTION_DEFAULTS = (1, 1, 1, 1, 0, 1)
+class AoOptions(ctypes.Structure):
+    """ao_options (oracle/afs_oracle.h) = TdsModel::Options (TdsModel.h:83-95)."""
+    _fields_ = [("turbulence_losses", ctypes.c_int), ("soft_walls", ctypes.c_int),
+                ("generate_noise_sources", ctypes.c_int), ("radiation_from_skin", ctypes.c_int),
+                ("piriform_fossa", ctypes.c_int), ("inner_length_corrections", ctypes.c_int),
+                ("transvelar_coupling", ctypes.c_int), ("glottis_loss", ctypes.c_int), ("solver", ctypes.c_int),
+                ("flow_separation_area_ratio", ctypes.c_double)]
 
 
-def option_vector(opt: dict):
+OPTION_DEFAULTS = {"turbulence_losses": 1, "soft_walls": 1, "generate_noise_sources": 1, "radiation_from_skin": 1,
+                   "piriform_fossa": 0, "inner_length_corrections": 1, "transvelar_coupling": 0, "glottis_loss": 0,
+                   "solver": 0, "flow_separation_area_ratio": 1.0}
+OPTION_NAMES = tuple(OPTION_DEFAULTS)
+
+
+def options_struct(opt: dict) -> AoOptions:
     unknown = set(opt) - set(OPTION_NAMES)
     if unknown:
         raise KeyError(f"unknown options {sorted(unknown)}")
-    return [int(bool(opt.get(n, d))) for n, d in zip(OPTION_NAMES, OPTION_DEFAULTS)]
+    o = AoOptions()
+    for k, d in OPTION_DEFAULTS.items():
+        v = opt.get(k, d)
+        setattr(o, k, float(v) if k == "flow_separation_area_ratio" else int(v))
+    return o
 
 
 class TargetCfg(ctypes.Structure):
@@ -69,7 +83,9 @@ class Oracle:
         lib.ao_synthesize_call.argtypes = [_vp, _vp, ctypes.c_int, _vp]
         lib.ao_synthesize_utterance.restype = ctypes.c_long
         lib.ao_synthesize_utterance.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
-                                                ctypes.c_double, _vp, _vp]
+                                                ctypes.c_double, ctypes.POINTER(AoOptions), _vp]
+        lib.ao_fulcher_kent.restype = ctypes.c_double
+        lib.ao_fulcher_kent.argtypes = [ctypes.c_double, ctypes.c_double]
         lib.ao_get_pressures.argtypes = [_vp, _vp]
         lib.ao_get_currents.argtypes = [_vp, _vp]
         lib.ao_get_state.argtypes = [_vp, _vp, ctypes.POINTER(ctypes.c_int)]
@@ -96,6 +112,9 @@ class Oracle:
         self.lib = lib
 
     # Synthesizer::playTargetSequence ------------------------------------------
+    def fulcher_kent(self, pressure_dpa: float, d_cm: float) -> float:
+        return float(self.lib.ao_fulcher_kent(pressure_dpa, d_cm))
+
     def target_cfg(self, timing=None) -> "TargetCfg":
         c = TargetCfg()
         self.lib.ao_target_default(ctypes.byref(c))
@@ -136,10 +155,7 @@ class Oracle:
         frames = np.ascontiguousarray(frames, dtype=FRAME_DTYPE)
         F = frames.shape[0]
         out = np.zeros((F - 1) * hop, dtype=np.float64)
-        o = None
-        if opt:
-            vals = option_vector(opt)
-            o = (ctypes.c_int * 6)(*vals)
+        o = ctypes.byref(options_struct(opt)) if opt else None
         n = self.lib.ao_synthesize_utterance(_ptr(frames), F, hop, seed, fs, o, _ptr(out))
         assert n == out.size
         return out
@@ -216,12 +232,21 @@ class RefLib:
                                          ctypes.c_double, _vp]
         lib.afsref_utterance_opt.restype = ctypes.c_long
         lib.afsref_utterance_opt.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint,
-                                             ctypes.c_double, _vp, _vp]
+                                             ctypes.c_double, _vp, ctypes.POINTER(AoOptions)]
+        lib.afsref_fulcher_table.restype = ctypes.c_int
+        lib.afsref_fulcher_table.argtypes = [ctypes.c_char_p, ctypes.c_int]
         lib.afsref_chebyshev.restype = ctypes.c_int
         lib.afsref_chebyshev.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_int, _vp, _vp]
         lib.afsref_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, _vp]
         lib.afsref_to_int16.argtypes = [_vp, ctypes.c_int, _vp]
         self.lib = lib
+
+    def fulcher_table(self) -> str:
+        """stdout of TdsModel::checkGlottalEntranceLossCoeffFlucher2011 (Fulcher 2011 Table I)."""
+        buf = ctypes.create_string_buffer(8192)
+        n = self.lib.afsref_fulcher_table(buf, 8192)
+        assert n > 0
+        return buf.value.decode()
 
     def to_int16(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float64)
@@ -233,7 +258,7 @@ class RefLib:
         frames = np.ascontiguousarray(frames, dtype=FRAME_DTYPE)
         F = frames.shape[0]
         out = np.zeros((F - 1) * hop, dtype=np.float64)
-        o = (ctypes.c_int * 6)(*option_vector(opt or {}))
+        o = ctypes.byref(options_struct(opt or {}))
         n = self.lib.afsref_utterance_opt(_ptr(frames), F, hop, seed, fs, _ptr(out), o)
         assert n == out.size
         return out

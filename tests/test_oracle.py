@@ -108,6 +108,8 @@ OPTION_VARIANTS = [
     {"radiation_from_skin": 0}, {"piriform_fossa": 1}, {"inner_length_corrections": 0},
     {"turbulence_losses": 0, "soft_walls": 0, "generate_noise_sources": 0, "radiation_from_skin": 0,
      "piriform_fossa": 1, "inner_length_corrections": 0},
+    {"transvelar_coupling": 1}, {"glottis_loss": 1}, {"glottis_loss": 2}, {"flow_separation_area_ratio": 1.2},
+    {"solver": 1}, {"solver": 1, "glottis_loss": 2, "transvelar_coupling": 1, "piriform_fossa": 1},
 ]
 
 
@@ -134,3 +136,36 @@ def test_options_vs_reference(oracle, opt):
     # the option changes the output (it is not silently ignored)
     base = oracle.utterance(frames, 150, 3, 22050.0)
     assert not np.array_equal(x, base)
+
+
+def test_fulcher_table_known_answer(oracle, golden_dir):
+    """VARIABLE_ENTRANCE_LOSS: k_ent of Fulcher et al. (2011) Table I as the reference prints
+    it (tests/golden/fulcher_table.txt, captured from the reference build)."""
+    with open(os.path.join(golden_dir, "fulcher_table.txt")) as fh:
+        want = [ln for ln in fh.read().splitlines() if ln.startswith("d=")]
+    cm = 97.97
+    got = ["d=%f cm: " % d + "  ".join("%4.3f" % oracle.fulcher_kent(p * cm, d) for p in (3, 5, 10, 15, 25))
+           for d in (0.005, 0.0075, 0.01, 0.02, 0.04, 0.08, 0.16, 0.32)]
+    assert got == want
+
+
+@pytest.mark.parametrize("opt", [{"glottis_loss": 2}, {"solver": 1}, {"transvelar_coupling": 1}],
+                         ids=["variable_loss", "sor", "transvelar"])
+def test_options_vs_reference_44k(oracle, opt):
+    """Rate-dependent option state (the transglottal 50 Hz low-pass) at 44.1 kHz."""
+    from oracle_lib import RefLib
+    try:
+        ref = RefLib()
+    except FileNotFoundError:
+        pytest.skip("reference build not available")
+    sh = default_shapes()
+    f = oracle.af_to_frame(sh["a:"])
+    f["velum_opening_cm2"] = 0.5
+    f["glottis"] = DEFAULT_GLOTTIS
+    g = oracle.af_to_frame(sh["z"])
+    g["velum_opening_cm2"] = 0.5
+    g["glottis"] = [110.0, 8000.0, 0.02, 0.01, 0.0, -30.0]
+    frames = np.stack([f, g, g, f])
+    x = oracle.utterance(frames, 441, 5, 44100.0, opt=opt)
+    y = ref.utterance(frames, 441, 5, 44100.0, opt=opt)
+    assert np.isfinite(x).all() and np.array_equal(x, y)
