@@ -16,6 +16,7 @@ STATUS = {0: "ok", 1: "invalid argument", 2: "no HIP device", 3: "HIP runtime er
           4: "out of device memory", 5: "unsupported configuration"}
 AFS_SOLVER_CHOLESKY = 0
 AFS_SOLVER_TREE = 1
+AFS_SOLVER_SOR = 2
 AFS_FP64 = 0
 AFS_ASYNC = 0x1
 
@@ -32,7 +33,9 @@ EXPORTED = (
 class AfsOptions(ctypes.Structure):
     _fields_ = [("turbulence_losses", ctypes.c_int32), ("soft_walls", ctypes.c_int32),
                 ("generate_noise_sources", ctypes.c_int32), ("radiation_from_skin", ctypes.c_int32),
-                ("piriform_fossa", ctypes.c_int32), ("inner_length_corrections", ctypes.c_int32)]
+                ("piriform_fossa", ctypes.c_int32), ("inner_length_corrections", ctypes.c_int32),
+                ("transvelar_coupling", ctypes.c_int32), ("glottis_loss", ctypes.c_int32),
+                ("flow_separation_area_ratio", ctypes.c_double)]
 
 
 class AfsTargetSequence(ctypes.Structure):

@@ -103,7 +103,7 @@ afs_status ensure(afs_ctx *c, void **buf, size_t *cap, size_t bytes) {
 
 int64_t pad64(int64_t b) { return (b + 63) / 64 * 64; }
 
-bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_TREE; }
+bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_TREE || s == AFS_SOLVER_SOR; }
 
 bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE; }
 
@@ -121,7 +121,8 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, k, ke, hop, o, ostride, lanes, (double *)ws, B, c->host_tab.uni};
       HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
     } else {
-      afs::LaneArgs a{c->dev_tab, frames, fstride, frame_row, k, ke, hop, o, ostride, (double *)ws, rng, bp, B};
+      afs::LaneArgs a{c->dev_tab, frames, fstride, frame_row, k, ke, hop, o, ostride, (double *)ws, rng, bp, B,
+                      c->cfg.solver == AFS_SOLVER_SOR ? 1 : 0};
       HIP_TRY(c, afs::launch_lane_synth(a, c->stream));
     }
   }
@@ -169,12 +170,7 @@ void afs_config_default(afs_config *cfg) {
   cfg->solver = AFS_SOLVER_TREE;
   cfg->device = 0;
   cfg->flags = 0;
-  cfg->options.turbulence_losses = 1;
-  cfg->options.soft_walls = 1;
-  cfg->options.generate_noise_sources = 1;
-  cfg->options.radiation_from_skin = 1;
-  cfg->options.piriform_fossa = 0;
-  cfg->options.inner_length_corrections = 1;
+  cfg->options = afs::default_options();
 }
 
 const char *afs_status_string(afs_status s) {

@@ -20,6 +20,7 @@ struct LaneArgs {
   int32_t *rng;              // 32 rows of bp ints (glibc TYPE_3 state + index)
   int64_t bp;                // padded batch (row pitch)
   int B;
+  int sor;                   // 1: SOR (TdsModel::SOR_GAUSS_SEIDEL) instead of the Cholesky
 };
 
 int64_t lane_ws_rows(const Tables &t);

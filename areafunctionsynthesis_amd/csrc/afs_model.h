@@ -28,7 +28,7 @@ constexpr int NS = 93;   // Tube::NUM_SECTIONS
 constexpr int NC = 97;   // TdsModel::NUM_BRANCH_CURRENTS
 constexpr int NPM = 40;  // pharynx + mouth sections
 constexpr int S_LAST_TRACHEA = 22, S_GLOT_LO = 23, S_GLOT_UP = 24;
-constexpr int S_PHARYNX0 = 25, S_LAST_PHARYNX = 40, S_LAST_MOUTH = 64;
+constexpr int S_PHARYNX0 = 25, S_LAST_PHARYNX = 40, S_MOUTH0 = 41, S_LAST_MOUTH = 64;
 constexpr int S_NOSE0 = 65, S_LAST_NOSE = 83, S_FOSSA0 = 84, S_LAST_FOSSA = 88;
 constexpr int S_SINUS0 = 89, S_LAST_SINUS = 92;
 constexpr int NDIP = 41;  // dipole sources of sections 25..64, then the lips source
@@ -105,6 +105,8 @@ struct Hot {
   double Tt;                    // glottis time step 1 / fs
   double inv_dt;                // 1 / dt
   double g_smk0, g_smk1;        // sqrt(mass * stiffness) of the two glottis masses (q-free)
+  double tglot_a[5], tglot_b[5];  // transglottal-pressure Chebyshev, 50 Hz (TdsModel.cpp:474)
+  double tvel2_a[5];              // transvelar coupling H2 numerator (H1 = tone_a; b = tone_b)
 };
 // Values that steer branches in the time loop: kernel arguments on the device, so the
 // compiler keeps them in scalar registers and branches on them uniformly.
@@ -134,6 +136,8 @@ struct Tables {
   double rrad_num, lrad_num; // 128 rho c, 8 rho                     (TdsModel.cpp:1874, 1889)
   double tone_a[5], tone_b[5];  // glottalToneFilter (TdsModel.cpp:494-510)
   double out_a[9], out_b[9];    // Chebyshev(7000/fs, 8 poles)     (Synthesizer.cpp:52)
+  double tglot_a[5], tglot_b[5];  // Chebyshev(50/fs, 4 poles)      (TdsModel.cpp:474)
+  double tvel2_a[5];            // transvelar coupling filter 2     (TdsModel.cpp:511-524)
 
   // per-section geometry and walls (static sections: final values; dynamic: walls only)
   double area[NS], len[NS], vol[NS], Mw[NS], Bw[NS], Kw[NS];
@@ -146,6 +150,8 @@ struct Tables {
   int16_t env_start[NC], env_n[NC], env_off[NC];
   int16_t col_n[NC], col[NC][ENV_COLS];
   int32_t env_total;
+  // SOR rows: filledRowIndex (TdsModel.cpp:340-357), ascending columns, at most 16
+  int16_t row_n[NC], row[NC][16];
 
   // tree solver
   int16_t edge[NS][3];
@@ -159,6 +165,21 @@ struct Tables {
 
   afs_options opt;
 };
+
+// TdsModel's default options (TdsModel.cpp:35-44).
+inline afs_options default_options() {
+  afs_options o{};
+  o.turbulence_losses = 1;
+  o.soft_walls = 1;
+  o.generate_noise_sources = 1;
+  o.radiation_from_skin = 1;
+  o.piriform_fossa = 0;
+  o.inner_length_corrections = 1;
+  o.transvelar_coupling = 0;
+  o.glottis_loss = AFS_ENTRANCE_LOSS_STANDARD;
+  o.flow_separation_area_ratio = 1.0;
+  return o;
+}
 
 // Host: build the tables for a sampling rate and option set (afs_tables.cpp).
 void build_tables(Tables *t, double fs_hz, const afs_options &opt);

@@ -124,6 +124,9 @@ void topology(Tables *t) {
       if (t->cout0[s] != -1) nz[c][t->cout0[s]] = 1;
       if (t->cout1[s] != -1) nz[c][t->cout1[s]] = 1;
     }
+    t->row_n[c] = 0;
+    for (int j = 0; j < NC; ++j)
+      if (nz[c][j] && j != c && t->row_n[c] < 16) t->row[c][t->row_n[c]++] = (int16_t)j;
     int first = c;
     for (int j = 0; j < c; ++j)
       if (nz[c][j]) { first = j; break; }
@@ -377,6 +380,10 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   static const double TB[5] = {0.0, 3.986308869708467, -5.959669638387298, 3.960408461107104, -0.987047716233603};
   for (int i = 0; i < 5; ++i) { t->tone_a[i] = TA[i]; t->tone_b[i] = TB[i]; }
   chebyshev(7000.0 / fs_hz, false, 8, t->out_a, t->out_b);
+  chebyshev(50.0 / fs_hz, false, 4, t->tglot_a, t->tglot_b);
+  static const double VA2[5] = {6.589309727087047e-004, -0.001972281980771, 0.001968000742164,
+                                -6.546497341015677e-004, 0.0};
+  for (int i = 0; i < 5; ++i) t->tvel2_a[i] = VA2[i];
   static_geometry(t);
   static_network(t);
   t->fossa_R0 = 8.0 * MU * t->len[S_FOSSA0] * PI / (AMIN * AMIN);
@@ -390,6 +397,7 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   h.rrad_num = t->rrad_num; h.lrad_num = t->lrad_num;
   for (int i = 0; i < 5; ++i) { h.tone_a[i] = t->tone_a[i]; h.tone_b[i] = t->tone_b[i]; }
   for (int i = 0; i < 9; ++i) { h.out_a[i] = t->out_a[i]; h.out_b[i] = t->out_b[i]; }
+  for (int i = 0; i < 5; ++i) { h.tglot_a[i] = t->tglot_a[i]; h.tglot_b[i] = t->tglot_b[i]; h.tvel2_a[i] = t->tvel2_a[i]; }
   h.len_nose0 = t->len[S_NOSE0]; h.Bw_ph0 = t->Bw[S_PHARYNX0]; h.Mw_ph0 = t->Mw[S_PHARYNX0];
   h.Kw_ph0 = t->Kw[S_PHARYNX0]; h.area_last_trachea = t->area[S_LAST_TRACHEA]; h.area_last_nose = t->area[S_LAST_NOSE];
   h.inv_dtTH = 1.0 / (t->dt * TH);

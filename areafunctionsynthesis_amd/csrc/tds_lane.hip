@@ -33,6 +33,7 @@ struct Lane {
   double *base;
   int64_t bp;
   int32_t *rng;
+  bool sor;  // solveEquationsSor instead of solveEquationsCholesky
   __device__ Col q(int off) const { return Col{base + (int64_t)off * bp, bp}; }
 
   __device__ int32_t rand_next() const {
@@ -117,7 +118,8 @@ enum : int {
   Q_DAMP = Q_UN + NC, Q_DOUT = Q_DAMP + NDIP, Q_DCUT = Q_DOUT + NDIP,
   Q_GBF = Q_DCUT + NDIP, Q_TONE = Q_GBF + 1, Q_OUTF = Q_TONE + 8, Q_PREVFLOW = Q_OUTF + 16,
   Q_RELX = Q_PREVFLOW + 1, Q_NONFINITE = Q_RELX + 4,
-  Q_PERSIST = Q_NONFINITE + 1,
+  Q_TGLOT = Q_NONFINITE + 1, Q_TVEL1 = Q_TGLOT + 8, Q_TVEL2 = Q_TVEL1 + 8,  // option filters
+  Q_PERSIST = Q_TVEL2 + 8,
   Q_AREA = Q_PERSIST, Q_LEN = Q_AREA + NS, Q_VOL = Q_LEN + NS, Q_POS = Q_VOL + NS,
   Q_LAT = Q_POS + NS, Q_ART = Q_LAT + NS,
   Q_L = Q_ART + NS, Q_C = Q_L + NS, Q_R0 = Q_C + NS, Q_R1 = Q_R0 + NS, Q_AL = Q_R1 + NS,
@@ -259,6 +261,60 @@ __device__ __forceinline__ double junction_l(double A1, double A2) {
   else { a = sqrt(A2 / PI); b = sqrt(A1 / PI); }
   double H = 1.0 - b / a;
   return 8.0 * RHO * H / (3.0 * PI * PI * b);
+}
+
+// getGlottalEntranceLossCoeffFlucher2011(pressure, d) (TdsModel.cpp:1048-1092)
+__device__ double fulcher_kent(double pressure_dPa, double d_cm) {
+  double pc = pressure_dPa / 979.7;
+  double D = d_cm;
+  if (pc < 0.001) pc = 0.001;
+  if (D < 0.001) D = 0.001;
+  double logD = log10(D);
+  double a = pow(10.0, 0.7953 * logD * logD + 1.4741 * logD + 0.6529);
+  double b = -0.7427 * logD * logD + -1.6209 * logD + -0.875;
+  double k = a * pow(pc, b);
+  if (k < 0.6) k = 0.6;
+  if (k > 18.0) k = 18.0;
+  return k;
+}
+
+// solveEquationsSor (TdsModel.cpp:2105-2180) on the negated envelope storage of calcMatrix
+// (negating A and b leaves every SOR iterate bit-identical).  Entry (i, j > i) is read from
+// row j's envelope: calcMatrix writes the two halves with identical values.
+__device__ void sor_solve(const Lane &Ln, const Col &AREA, const Col &FD, const Col &FE, const Col &SOL,
+                          const Col &FLOW) {
+  const Tables &T = Ln.T;
+  uint64_t act0 = ~0ull, act1 = ~0ull;  // isActive bit per current (97 bits)
+  auto off = [&](int c) {
+    if (c < 0) return;
+    if (c < 64) act0 &= ~(1ull << c); else act1 &= ~(1ull << (c - 64));
+  };
+  for (int i = 0; i < NS; ++i) {
+    const double a = is_static_section(i) ? T.area[i] : AREA[i];
+    if (a <= 1.01 * AMIN) { off(T.cin[i]); off(T.cout0[i]); off(T.cout1[i]); }
+  }
+  for (int i = 0; i < NC; ++i) FLOW[i] = 0.0;
+  auto m = [&](int i, int j) -> double {
+    return j < i ? FE[T.env_off[i] + j - T.env_start[i]] : FE[T.env_off[j] + i - T.env_start[j]];
+  };
+  int it = 0;
+  double res;
+  do {
+    res = 0.0;
+    for (int i = NC - 1; i >= 0; --i) {
+      const bool active = i < 64 ? ((act0 >> i) & 1) : ((act1 >> (i - 64)) & 1);
+      if (!active) continue;
+      double sum = FD[i] * FLOW[i];
+      for (int k = T.row_n[i] - 1; k >= 0; --k) {
+        const int j = T.row[i][k];
+        sum += FLOW[j] * m(i, j);
+      }
+      const double d = SOL[i] - sum;
+      res += d * d;
+      FLOW[i] = FLOW[i] + 1.25 * d / FD[i];
+    }
+    ++it;
+  } while (it < 100 && res > 0.1 * 0.1);
 }
 
 __device__ double iir_step(const Col &st, int order, const double *a, const double *b, double x) {
@@ -410,13 +466,21 @@ __device__ double sample_step(const Lane &Ln, const afs_frame *fl, const afs_fra
   if (!opt.piriform_fossa) R0[S_FOSSA0] = T.fossa_R0;
   {
     Col GBF = Ln.q(Q_GBF);
+    double kent = 1.0;  // glottal entrance loss (TdsModel.cpp:898-911, 1019-1092)
+    if (opt.glottis_loss == AFS_ENTRANCE_LOSS_VAN_DEN_BERG) {
+      kent = 1.375;
+    } else if (opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE) {
+      double tp = P[S_LAST_TRACHEA] - P[S_PHARYNX0];
+      double ftp = iir_step(Ln.q(Q_TGLOT), 4, T.tglot_a, T.tglot_b, tp);
+      kent = fulcher_kent(ftp, AREA[S_GLOT_LO] / 1.25);
+    }
     double sa = T.area[S_LAST_TRACHEA], ta = AREA[S_GLOT_LO];
     double u = 0.0;
     u += U[S_GLOT_LO];
-    if (u > 0) R0[S_GLOT_LO] = R0[S_GLOT_LO] + 1.0 * 0.5 * RHO * fabs(u) * (1.0 / (ta * ta) - 1.0 / (sa * sa));
+    if (u > 0) R0[S_GLOT_LO] = R0[S_GLOT_LO] + kent * 0.5 * RHO * fabs(u) * (1.0 / (ta * ta) - 1.0 / (sa * sa));
     sa = AREA[S_GLOT_LO];
     ta = AREA[S_GLOT_UP];
-    double bt = (ta < 1.0 * sa) ? 1.0 : 0.0;
+    double bt = (ta < opt.flow_separation_area_ratio * sa) ? 1.0 : 0.0;
     double g = 0.8 * GBF[0] + (1.0 - 0.8) * bt;
     GBF[0] = g;
     u = 0.0;
@@ -425,10 +489,16 @@ __device__ double sample_step(const Lane &Ln, const afs_frame *fl, const afs_fra
   }
   if (opt.generate_noise_sources) noise_sources(Ln, teeth, gp[5]);
   else for (int d = 0; d < NDIP; ++d) SMP[d] = 0.0;
+  double tvflow = 0.0;  // transvelar coupling (TdsModel.cpp:966-980)
+  if (opt.transvelar_coupling)
+    tvflow = iir_step(Ln.q(Q_TVEL1), 4, T.tone_a, T.tone_b, P[S_MOUTH0 + 2]) +
+             iir_step(Ln.q(Q_TVEL2), 4, T.tvel2_a, T.tone_b, P[S_NOSE0 + 2]);
   for (int i = 0; i < NS; ++i) {
     double d = is_static_section(i) ? T.E[i] : dt * TH / (Cc[i] + AL[i]);
+    double src = 0.0;
+    if (i == S_NOSE0 + 2) src += tvflow;
     E[i] = d;
-    D[i] = P[i] + T.dtTH1 * PR[i] - d * (BE[i] - 0.0);
+    D[i] = P[i] + T.dtTH1 * PR[i] - d * (BE[i] - src);
   }
 
   // ---- calcMatrix (TdsModel.cpp:1785-2039) into the negated envelope storage ----
@@ -508,6 +578,9 @@ __device__ double sample_step(const Lane &Ln, const afs_frame *fl, const afs_fra
     SOL[i] = -rhs;
   }
 
+  if (Ln.sor) {
+    sor_solve(Ln, AREA, FD, FE, SOL, FLOW);
+  } else {
   // ---- solveEquationsCholesky (TdsModel.cpp:2259-2313) ----
   for (int k = 0; k < NC; ++k) {
     const int esk = T.env_start[k], eok = T.env_off[k];
@@ -543,6 +616,7 @@ __device__ double sample_step(const Lane &Ln, const afs_frame *fl, const afs_fra
     }
     SOL[k] = y;
     FLOW[k] = y / FD[k];
+  }
   }
 
   // ---- updateVariables (TdsModel.cpp:2046-2098) ----
@@ -606,7 +680,7 @@ __global__ void __launch_bounds__(64) lane_synth_kernel(LaneArgs a) {
   int u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= a.B) return;
   const Tables &T = *a.tab;
-  Lane L{T, a.ws + u, a.bp, a.rng + u};
+  Lane L{T, a.ws + u, a.bp, a.rng + u, a.sor != 0};
   const afs_frame *fu = a.frames + (int64_t)(a.frame_row ? a.frame_row[u] : u) * a.frame_stride;
   double *o = a.out + (int64_t)u * a.out_stride;
   Col NF = L.q(Q_NONFINITE);

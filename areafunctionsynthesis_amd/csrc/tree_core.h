@@ -28,6 +28,7 @@
 #include <cmath>
 using std::exp;
 using std::fabs;
+using std::log10;
 using std::isfinite;
 using std::pow;
 using std::sqrt;
@@ -85,7 +86,10 @@ enum : int {
   X_ART = X_NONFIN + 1,        // 40 articulator bytes
   X_RNG = X_ART + 5,           // rand(): value ring, prefix-sum ring (64 u32 each), head, pending (65 doubles)
   X_GP = X_RNG + 65,           // interpolated glottis controls (6) and teeth position (lane 0)
-  X_TOTAL = X_GP + 8
+  X_TGLOT = X_GP + 8,          // transglottal-pressure filter x1..x4, y1..y4 (variable entrance loss)
+  X_TVEL = X_TGLOT + 8,        // transvelar coupling filters H1, H2: x1..x4, y1..y4 each
+  X_TVP = X_TVEL + 16,         // p[43], p[67] after the last update (transvelar filter inputs)
+  X_TOTAL = X_TVP + 2
 };
 
 // Phase ids for Exec::mark (cycle accounting in tools/phase_prof; a no-op otherwise).
@@ -228,6 +232,21 @@ AFS_HD inline void glottis_open_close(const double *gp, double cord, double rel0
       }
     }
   }
+}
+
+// getGlottalEntranceLossCoeffFlucher2011(pressure, d) (TdsModel.cpp:1048-1092)
+AFS_HD inline double fulcher_kent(double pressure_dPa, double d_cm) {
+  double pc = pressure_dPa / 979.7;
+  double D = d_cm;
+  if (pc < 0.001) pc = 0.001;
+  if (D < 0.001) D = 0.001;
+  const double logD = log10(D);
+  const double a = pow(10.0, 0.7953 * logD * logD + 1.4741 * logD + 0.6529);
+  const double b = -0.7427 * logD * logD + -1.6209 * logD + -0.875;
+  double k = a * pow(pc, b);
+  if (k < 0.6) k = 0.6;
+  if (k > 18.0) k = 18.0;
+  return k;
 }
 
 // getJunctionInductance (TdsModel.cpp:1745-1778)
@@ -529,14 +548,21 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
         if ((area < Aa && u > 0) || (area > Aa && u < 0)) R0 = R0 + u * (0.5 * RHO) * (inv_area * inv_area);
       }
     }
-    if (s == S_GLOT_LO) {  // glottal entrance and transition (TdsModel.cpp:912-950)
+    if (s == S_GLOT_LO) {  // glottal entrance and transition (TdsModel.cpp:898-950)
+      double kent = 1.0;
+      if (opt.glottis_loss == AFS_ENTRANCE_LOSS_VAN_DEN_BERG) {
+        kent = 1.375;
+      } else if (opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE) {  // :1019-1039
+        const double tp = X[X_P4 + 0] - X[X_P4 + 3];
+        kent = fulcher_kent(iir_run<4>(X + X_TGLOT, C.h.tglot_a, C.h.tglot_b, tp), area / 1.25);
+      }
       double sa = C.h.area_last_trachea, ta = area;
       double u = 0.0;
       u += R.u[j];
-      if (u > 0) R0 = R0 + 1.0 * 0.5 * RHO * fabs(u) * (fast_rcp(ta * ta) - fast_rcp(sa * sa));
+      if (u > 0) R0 = R0 + kent * 0.5 * RHO * fabs(u) * (fast_rcp(ta * ta) - fast_rcp(sa * sa));
       sa = ta;
       ta = X[X_AREA + 1];
-      double bt = (ta < 1.0 * sa) ? 1.0 : 0.0;
+      double bt = (ta < opt.flow_separation_area_ratio * sa) ? 1.0 : 0.0;
       double g = 0.8 * X[X_GBF] + (1.0 - 0.8) * bt;
       X[X_GBF] = g;
       u = 0.0;
@@ -546,7 +572,11 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     R.al[j] = alpha;
     R.be[j] = beta;
     X[X_E + s - DYN0] = E;
-    X[X_D + s] = R.p[j] + C.h.dtTH1 * R.pr[j] - E * (beta - 0.0);
+    double src = 0.0;
+    if (opt.transvelar_coupling && s == S_NOSE0 + 2)  // flow through the velum (:966-980, 996)
+      src += iir_run<4>(X + X_TVEL, C.h.tone_a, C.h.tone_b, X[X_TVP]) +
+             iir_run<4>(X + X_TVEL + 8, C.h.tvel2_a, C.h.tone_b, X[X_TVP + 1]);
+    X[X_D + s] = R.p[j] + C.h.dtTH1 * R.pr[j] - E * (beta - src);
     X[X_L + s - DYN0] = L;
     X[X_R0 + s - DYN0] = R0;
     X[X_R1 + s - DYN0] = R1;
@@ -1077,6 +1107,10 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
     R.wr[j] = wr;
     R.wr2[j] = (wr - owr) * idt - R.wr2[j] * (TH1 / TH);
     if (s >= S_LAST_TRACHEA && s <= S_PHARYNX0) X[X_P4 + s - S_LAST_TRACHEA] = p;
+    if (U.opt.transvelar_coupling) {
+      if (s == S_MOUTH0 + 2) X[X_TVP] = p;
+      if (s == S_NOSE0 + 2) X[X_TVP + 1] = p;
+    }
     if (s == S_LAST_MOUTH || s == S_LAST_NOSE) {  // the two radiation currents of this section
       for (int q = 0; q < 2; ++q) {
         const int rc = q == 0 ? o0 : o1;

@@ -25,7 +25,7 @@ from .frames import FRAME_DTYPE
 
 _vp = ctypes.c_void_p
 
-SOLVERS = {"cholesky": _native.AFS_SOLVER_CHOLESKY, "tree": _native.AFS_SOLVER_TREE}
+SOLVERS = {"cholesky": _native.AFS_SOLVER_CHOLESKY, "tree": _native.AFS_SOLVER_TREE, "sor": _native.AFS_SOLVER_SOR}
 
 
 def _addr(x) -> int:
@@ -61,7 +61,12 @@ class Context:
         for k, v in options.items():
             if not hasattr(cfg.options, k):
                 raise TypeError(f"unknown option {k}")
-            setattr(cfg.options, k, int(bool(v)))
+            if k == "flow_separation_area_ratio":
+                setattr(cfg.options, k, float(v))
+            elif k == "glottis_loss":
+                setattr(cfg.options, k, int(v))
+            else:
+                setattr(cfg.options, k, int(bool(v)))
         h = _vp()
         _native.check(lib.afs_create(ctypes.byref(h), ctypes.byref(cfg)), None, "afs_create")
         self._lib = lib

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define AFS_ABI_VERSION 1
+#define AFS_ABI_VERSION 2
 #define AFS_NUM_TUBE_SECTIONS 40   /* Tube::NUM_PHARYNX_MOUTH_SECTIONS (Tube.h:56-58) */
 #define AFS_NUM_GLOTTIS_PARAMS 6   /* TriangularGlottis::NUM_CONTROL_PARAMS (TriangularGlottis.h:26-35) */
 #define AFS_NUM_AF_PARAMS 16       /* OneDimAreaFunction::NUM_AF_PARAMS (OneDimAreaFunction.h:34-43) */
@@ -62,8 +62,16 @@ typedef enum afs_status {
 /* Linear solver for the per-sample 97x97 SPD system. */
 typedef enum afs_solver {
   AFS_SOLVER_CHOLESKY = 0, /* TdsModel::CHOLESKY_FACTORIZATION, same operation order (TdsModel.cpp:2231-2314) */
-  AFS_SOLVER_TREE = 1      /* fill-free leaf-first LDL^T on the tube tree (same system, fewer flops) */
+  AFS_SOLVER_TREE = 1,     /* nested-dissection LDL^T on the tube tree (same system, fewer flops) */
+  AFS_SOLVER_SOR = 2       /* TdsModel::SOR_GAUSS_SEIDEL, same sweep order (TdsModel.cpp:2105-2180) */
 } afs_solver;
+
+/* TdsModel::GlottisLossOptions (TdsModel.h:75-81). */
+typedef enum afs_glottis_loss {
+  AFS_ENTRANCE_LOSS_STANDARD = 0,     /* k_ent = 1 */
+  AFS_ENTRANCE_LOSS_VAN_DEN_BERG = 1, /* k_ent = 1.375 */
+  AFS_ENTRANCE_LOSS_VARIABLE = 2      /* Fulcher et al. 2011 (TdsModel.cpp:1019-1092) */
+} afs_glottis_loss;
 
 typedef enum afs_precision { AFS_FP64 = 0 } afs_precision;
 
@@ -75,6 +83,9 @@ typedef struct afs_options {
   int32_t radiation_from_skin;      /* 1 */
   int32_t piriform_fossa;           /* 0 */
   int32_t inner_length_corrections; /* 1 */
+  int32_t transvelar_coupling;      /* 0 */
+  int32_t glottis_loss;             /* afs_glottis_loss, 0 */
+  double flow_separation_area_ratio; /* 1.0 */
 } afs_options;
 
 #define AFS_ASYNC 0x1u

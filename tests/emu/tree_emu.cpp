@@ -87,7 +87,7 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
 
 extern "C" long emu_tree_utterance(const afs_frame *frames, int F, int hop, unsigned seed, double fs, int W,
                                    double *out, double *dump_p, double *dump_u, int ndump) {
-  afs_options opt{1, 1, 1, 1, 0, 1};
+  afs_options opt = afs::default_options();
   switch (W) {
     case 16: return run<16>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
     case 32: return run<32>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
@@ -96,9 +96,26 @@ extern "C" long emu_tree_utterance(const afs_frame *frames, int F, int hop, unsi
   return -2;
 }
 
+// options: turbulence, soft walls, noise, skin radiation, fossa, inner length corrections,
+// transvelar coupling, glottis loss (ints) and the flow-separation area ratio.
+extern "C" long emu_tree_utterance_opt(const afs_frame *frames, int F, int hop, unsigned seed, double fs,
+                                       const int *iopt, double ratio, double *out) {
+  afs_options opt = afs::default_options();
+  opt.turbulence_losses = iopt[0];
+  opt.soft_walls = iopt[1];
+  opt.generate_noise_sources = iopt[2];
+  opt.radiation_from_skin = iopt[3];
+  opt.piriform_fossa = iopt[4];
+  opt.inner_length_corrections = iopt[5];
+  opt.transvelar_coupling = iopt[6];
+  opt.glottis_loss = iopt[7];
+  opt.flow_separation_area_ratio = ratio;
+  return run<16>(frames, F, hop, seed, fs, opt, out, nullptr, nullptr, 0);
+}
+
 extern "C" int emu_tree_rounds(double fs) {
   static Tables T;
-  afs_options opt{1, 1, 1, 1, 0, 1};
+  afs_options opt = afs::default_options();
   build_tables(&T, fs, opt);
   return T.n_rounds;
 }

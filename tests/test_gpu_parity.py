@@ -222,6 +222,8 @@ OPTION_VARIANTS = [
     {"radiation_from_skin": 0}, {"piriform_fossa": 1}, {"inner_length_corrections": 0},
     {"turbulence_losses": 0, "soft_walls": 0, "generate_noise_sources": 0, "radiation_from_skin": 0,
      "piriform_fossa": 1, "inner_length_corrections": 0},
+    {"transvelar_coupling": 1}, {"glottis_loss": 1}, {"glottis_loss": 2}, {"flow_separation_area_ratio": 1.2},
+    {"transvelar_coupling": 1, "glottis_loss": 2, "piriform_fossa": 1},
 ]
 
 
@@ -242,3 +244,27 @@ def test_options_vs_oracle(contexts, oracle, solver):
         y = ctx.synthesize(np.ascontiguousarray(frames[None]), 150, seeds=np.array([3], np.uint32))
         x = oracle.utterance(frames, 150, 3, 22050.0, opt=opt)
         assert np.abs(y[0] - x).max() <= GOLD_TOL, (opt, float(np.abs(y[0] - x).max()))
+
+
+@pytest.mark.parametrize("opt", [{}, {"glottis_loss": 2, "transvelar_coupling": 1}, {"piriform_fossa": 1}],
+                         ids=["default", "variable_loss+transvelar", "fossa"])
+def test_sor_solver_vs_oracle(contexts, oracle, opt):
+    """TdsModel::SOR_GAUSS_SEIDEL (afs_solver AFS_SOLVER_SOR, lane kernel) against the oracle's
+    SOR, which test_oracle.py pins bit-exactly to the reference build."""
+    sh = default_shapes()
+    f = oracle.af_to_frame(sh["a:"])
+    f["velum_opening_cm2"] = 0.3
+    f["glottis"] = DEFAULT_GLOTTIS
+    g = oracle.af_to_frame(sh["s"])
+    g["velum_opening_cm2"] = 0.3
+    g["glottis"] = [130.0, 9000.0, 0.01, 0.02, 0.0, -25.0]
+    frames = np.stack([f, g, g, f, f])
+    for fs, hop in ((22050.0, 150), (44100.0, 441)):
+        ctx = contexts(fs, "sor", **opt)
+        y = ctx.synthesize(np.ascontiguousarray(frames[None]), hop, seeds=np.array([9], np.uint32))
+        x = oracle.utterance(frames, hop, 9, fs, opt=dict(opt, solver=1))
+        assert np.abs(y[0, :2048] - x[:2048]).max() <= GOLD_TOL, (fs, float(np.abs(y[0] - x).max()))
+        assert float(np.sqrt(np.mean((y[0] - x) ** 2))) < RMS_TOL
+        # SOR's coarse residual bound makes it a different solution from the Cholesky's
+        z = oracle.utterance(frames, hop, 9, fs, opt=opt)
+        assert not np.array_equal(x, z)

@@ -33,7 +33,24 @@ def emu():
                                    dummy.ctypes.data, dummy.ctypes.data, 0)
         assert n == out.size
         return out
+    lib.emu_tree_utterance_opt.restype = ctypes.c_long
+    lib.emu_tree_utterance_opt.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_double, vp,
+                                           ctypes.c_double, vp]
+
+    def run_opt(fr, hop, seed, fs, opt):
+        from oracle_lib import OPTION_DEFAULTS
+        o = dict(OPTION_DEFAULTS, **opt)
+        iopt = np.array([o[k] for k in ("turbulence_losses", "soft_walls", "generate_noise_sources",
+                                        "radiation_from_skin", "piriform_fossa", "inner_length_corrections",
+                                        "transvelar_coupling", "glottis_loss")], dtype=np.int32)
+        fr = np.ascontiguousarray(fr, dtype=FRAME_DTYPE)
+        out = np.zeros((fr.size - 1) * hop)
+        n = lib.emu_tree_utterance_opt(fr.ctypes.data, fr.size, hop, seed, fs, iopt.ctypes.data,
+                                       float(o["flow_separation_area_ratio"]), out.ctypes.data)
+        assert n == out.size
+        return out
     run.lib = lib
+    run.opt = run_opt
     return run
 
 
@@ -62,3 +79,26 @@ def test_lane_width_invariance(emu, golden_dir, W):
         fr = frames[i, : g["num_frames"][i]]
         args = (int(g["hop"][i]), int(g["seed"][i]), float(g["fs"][i]))
         assert np.array_equal(emu(fr, *args, W=W), emu(fr, *args, W=16))
+
+
+@pytest.mark.parametrize("opt", [{"transvelar_coupling": 1}, {"glottis_loss": 1}, {"glottis_loss": 2},
+                                 {"flow_separation_area_ratio": 1.2}, {"piriform_fossa": 1, "soft_walls": 0},
+                                 {"transvelar_coupling": 1, "glottis_loss": 2, "generate_noise_sources": 0}],
+                         ids=lambda o: "+".join(f"{k}={v}" for k, v in o.items()))
+def test_options_vs_oracle(emu, oracle, opt):
+    """The tree decomposition of every TdsModel option (the SOR solver runs in the lane kernel)."""
+    from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS
+    from areafunctionsynthesis_amd.params import default_shapes
+    sh = default_shapes()
+    f = oracle.af_to_frame(sh["a:"])
+    f["velum_opening_cm2"] = 0.5
+    f["glottis"] = DEFAULT_GLOTTIS
+    g = oracle.af_to_frame(sh["z"])
+    g["velum_opening_cm2"] = 0.5
+    g["glottis"] = [110.0, 8000.0, 0.02, 0.01, 0.0, -30.0]
+    frames = np.stack([f, g, g, f])
+    for fs, hop in ((22050.0, 300), (44100.0, 441)):
+        x = emu.opt(frames, hop, 5, fs, opt)
+        y = oracle.utterance(frames, hop, 5, fs, opt=opt)
+        assert np.abs(x[:2048] - y[:2048]).max() <= TOL, fs
+        assert np.sqrt(np.mean((x - y) ** 2)) < 1e-8, fs

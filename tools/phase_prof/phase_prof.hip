@@ -31,7 +31,7 @@ extern "C" int pp_phase_count() { return PH_COUNT; }
 extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int F, int hop, double fs,
                       uint64_t *cycles, double *ms) {
   Tables *ht = new Tables();
-  afs_options opt{1, 1, 1, 1, 0, 1};
+  afs_options opt = afs::default_options();
   build_tables(ht, fs, opt);
   Tables *dt;
   afs_frame *df;
