@@ -292,6 +292,7 @@ void ao_default_options(ao_options *o) {
   o->transvelar_coupling = 0;
   o->glottis_loss = 0;
   o->solver = 0;
+  o->glottis_model = 0;
   o->flow_separation_area_ratio = 1.0;
 }
 
@@ -485,6 +486,113 @@ static void glottis_step(ao_synth *s, double T, const double pr[4]) {
               T * T * kc[0] * al[0] * rs[0];
   double Ff = fo[1] * T * T + 2.0 * m[1] * rel[1] - m[1] * prev[1] + r[1] * T * rel[1] -
               T * T * kc[1] * al[1] * rs[1];
+  double det = A * Dd - B * Cc;
+  if (fabs(det) < 0.000000001) det = 0.000000001;
+  s->relx[0][(s->gpos + 1) & 3] = (Ee * Dd - B * Ff) / det;
+  s->relx[1][(s->gpos + 1) & 3] = (A * Ff - Ee * Cc) / det;
+  s->gpos++;
+}
+
+/* ---------------------------------------------------------------------------
+ * TwoMassModel (TwoMassModel.cpp, static parameters :36-58, control parameters :17-24): the classical two-mass model
+ * with cubic springs; control parameters f0, lung pressure, rest displacements, extra
+ * arytenoid area, damping factor.  Part of the reference's sources but not of its
+ * executable (CMakeLists.txt:9); selected here with ao_options.glottis_model = 1.
+ * ------------------------------------------------------------------------- */
+static const double TM_REST_LEN = 1.3, TM_REST_THICK0 = 0.25, TM_REST_THICK1 = 0.05;
+static const double TM_MASS0 = 0.125, TM_MASS1 = 0.025, TM_DAMP0 = 0.1, TM_DAMP1 = 0.6;
+static const double TM_K0 = 80000.0, TM_K1 = 8000.0, TM_ETA0 = 100.0, TM_ETA1 = 100.0;
+static const double TM_KC0 = 240000.0, TM_KC1 = 24000.0, TM_CETA0 = 500.0, TM_CETA1 = 500.0;
+static const double TM_KCOUPLE = 25000.0, TM_CRIT_WIDTH = 0.0, TM_NAT_F0 = 158.0, TM_F0_DIV_Q = 100.0;
+static const double TM_CHINK_LEN = 0.2;
+
+/* getTensionParameter, :467-485 */
+static double tm_q(double f0) {
+  double dq = TM_F0_DIV_Q;
+  if (dq < 0.000001) dq = 0.000001;
+  double q = 1.0 + (f0 - TM_NAT_F0) / dq;
+  return q < 0.05 ? 0.05 : q;
+}
+
+/* getLengthAndThickness, :491-497 */
+static void tm_len_thick(double q, double *len, double th[2]) {
+  double f = sqrt(q);
+  *len = TM_REST_LEN * f;
+  th[0] = TM_REST_THICK0 / f;
+  th[1] = TM_REST_THICK1 / f;
+}
+
+/* calcGeometry + getTubeData, :359-440 */
+static void tm_geometry(const ao_synth *s, double thick[2], double area[2]) {
+  double rest[2] = {s->gp[2], s->gp[3]};
+  double rel[2] = {s->relx[0][s->gpos & 3], s->relx[1][s->gpos & 3]};
+  double ab[2];
+  for (int i = 0; i < 2; ++i) {
+    ab[i] = rest[i] + rel[i];
+    if (ab[i] < 0.0) ab[i] = 0.0;
+  }
+  double passive = 2.0 * s->gp[3];
+  if (passive < 0.0) passive = 0.0;
+  double chink = passive * TM_CHINK_LEN + s->gp[4];
+  if (chink < 0.0) chink = 0.0;
+  double len;
+  tm_len_thick(tm_q(s->gp[0]), &len, thick);
+  area[0] = 2.0 * len * ab[0] + chink;
+  area[1] = 2.0 * len * ab[1] + chink;
+}
+
+/* incTime, :157-349 */
+static void tm_step(ao_synth *s, double T, const double pr[4]) {
+  double Q = tm_q(s->gp[0]);
+  double critX = 0.5 * TM_CRIT_WIDTH;
+  double rel[2] = {s->relx[0][s->gpos & 3], s->relx[1][s->gpos & 3]};
+  double rest[2] = {s->gp[2], s->gp[3]};
+  double ab[2] = {rest[0] + rel[0], rest[1] + rel[1]};
+  double minRel[2] = {critX - rest[0], critX - rest[1]};
+  double prev[2] = {s->relx[0][(s->gpos - 1) & 3], s->relx[1][(s->gpos - 1) & 3]};
+  double len, th[2];
+  tm_len_thick(Q, &len, th);
+  double m[2] = {TM_MASS0 / Q, TM_MASS1 / Q};
+  double k[2] = {TM_K0 * Q, TM_K1 * Q};
+  double eta[2] = {TM_ETA0, TM_ETA1};
+  double ck[2] = {TM_KC0 * Q, TM_KC1 * Q};
+  double ceta[2] = {TM_CETA0, TM_CETA1};
+  double kc = TM_KCOUPLE * Q * Q;
+  double df = s->gp[5];
+  double dr[2] = {TM_DAMP0, TM_DAMP1};
+  if (ab[0] <= critX) dr[0] += 1.0;
+  if (ab[1] <= critX) dr[1] += 1.0;
+  double r[2];
+  r[0] = 2.0 * dr[0] * sqrt(m[0] * k[0]) * df * df;
+  r[1] = 2.0 * dr[1] * sqrt(m[1] * k[1]) * df * df;
+  double fo[2];
+  if ((ab[0] > TM_CRIT_WIDTH) && (ab[1] > TM_CRIT_WIDTH)) {
+    fo[0] = pr[1] * len * th[0];
+    fo[1] = pr[2] * len * th[1];
+  } else if ((ab[0] <= TM_CRIT_WIDTH) && (ab[1] > TM_CRIT_WIDTH)) {
+    fo[0] = pr[0] * len * th[0];
+    fo[1] = pr[2] * len * th[1];
+  } else if ((ab[0] > TM_CRIT_WIDTH) && (ab[1] <= TM_CRIT_WIDTH)) {
+    fo[0] = pr[1] * len * th[0];
+    fo[1] = pr[1] * len * th[1];
+  } else {
+    fo[0] = pr[0] * len * th[0];
+    fo[1] = pr[3] * len * th[1];
+  }
+  double nl[2];
+  for (int i = 0; i < 2; ++i) {
+    if (rel[i] > minRel[i]) { ck[i] = 0.0; ceta[i] = 0.0; }
+    double dx = rel[i] - minRel[i];
+    nl[i] = k[i] * eta[i] * rel[i] * rel[i] * rel[i] + ck[i] * ceta[i] * dx * dx * dx;
+  }
+  double A = m[0] + r[0] * T + T * T * (k[0] + ck[0]) + kc * T * T;
+  double B = -kc * T * T;
+  double Cc = -kc * T * T;
+  double Dd = m[1] + r[1] * T + T * T * (k[1] + ck[1]) + kc * T * T;
+  double Ee = fo[0] * T * T + 2.0 * m[0] * rel[0] - m[0] * prev[0] + r[0] * T * rel[0] +
+              T * T * ck[0] * minRel[0] - nl[0] * T * T;
+  double Ff = fo[1] * T * T + 2.0 * m[1] * rel[1] - m[1] * prev[1] + r[1] * T * rel[1] +
+              T * T * ck[1] * minRel[1] - nl[1] * T * T;
   double det = A * Dd - B * Cc;
   if (fabs(det) < 0.000000001) det = 0.000000001;
   s->relx[0][(s->gpos + 1) & 3] = (Ee * Dd - B * Ff) / det;
@@ -996,20 +1104,24 @@ int ao_synthesize_call(ao_synth *s, const ao_frame *fr, int n, double *out) {
     tube_interpolate(s, &s->prev, fr, ratio);
     for (int k = 0; k < 6; ++k) s->gp[k] = r1 * s->prev.glottis[k] + ratio * fr->glottis[k];
     double gl[2], ga[2];
-    glottis_geometry(s, gl, ga);
+    if (s->opt.glottis_model == 1) tm_geometry(s, gl, ga);
+    else glottis_geometry(s, gl, ga);
     for (int k = 0; k < 2; ++k) {
       int sec = S_GLOT_LO + k;
       s->len[sec] = gl[k];
       s->area[sec] = clamp_amin(ga[k]);
       s->vol[sec] = s->area[sec] * s->len[sec];
     }
-    s->aspiration_db = s->gp[5];
+    /* TriangularGlottis::getAspirationStrength_dB = control 5; the two-mass model keeps the
+     * base class default (Glottis.cpp:11-16) */
+    s->aspiration_db = (s->opt.glottis_model == 1) ? -40.0 : s->gp[5];
     /* setTube (TdsModel.cpp:552-584) copies the tube; our TDS arrays alias it. */
     s->teeth_tds = s->teeth;
     s->asp_tds = s->aspiration_db;
     s->p_amp = s->gp[1];
     double pg[4] = {s->p[S_LAST_TRACHEA], s->p[S_GLOT_LO], s->p[S_GLOT_UP], s->p[S_PHARYNX0]};
-    glottis_step(s, 1.0 / s->fs, pg);
+    if (s->opt.glottis_model == 1) tm_step(s, 1.0 / s->fs, pg);
+    else glottis_step(s, 1.0 / s->fs, pg);
     double flow = tds_step(s);
     int k = s->position & 255;
     s->flow_ring[k] = flow;

@@ -14,6 +14,7 @@
  *   glibc random_r TYPE_3 (rand()/srand())    glibc 2.35 stdlib/random_r.c (the
  *                                             reference calls rand() at
  *                                             src/Backend/TdsModel.cpp:1690-1692)
+ *   TwoMassModel (alternative glottis)        src/Backend/TwoMassModel.cpp:1-497
  *   OneDimAreaFunction (area fn -> tube)      src/Backend/OneDimAreaFunction.cpp:23-138
  *   Synthesizer::playTargetSequence           src/Backend/Synthesizer.cpp:1286-1422
  *   int16 output ring                         src/Backend/Synthesizer.cpp:955-973
@@ -63,6 +64,7 @@ typedef struct ao_options {
   int transvelar_coupling;      /* 0 */
   int glottis_loss;             /* 0 STANDARD, 1 VAN_DEN_BERG, 2 VARIABLE (Fulcher 2011) */
   int solver;                   /* 0 CHOLESKY_FACTORIZATION, 1 SOR_GAUSS_SEIDEL */
+  int glottis_model;            /* 0 TriangularGlottis (the Synthesizer's), 1 TwoMassModel */
   double flow_separation_area_ratio; /* 1.0 */
 } ao_options;
 

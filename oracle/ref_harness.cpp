@@ -26,6 +26,7 @@
 #include "TdsModel.h"
 #include "TriangularGlottis.h"
 #include "Tube.h"
+#include "TwoMassModel.h"
 
 extern "C" {
 #include "afs_oracle.h"  // only for the ao_frame record layout
@@ -42,7 +43,9 @@ namespace {
 
 struct RefVoice {
   TdsModel tds;
-  TriangularGlottis glottis;
+  TriangularGlottis triangular;
+  TwoMassModel twoMass;  // TwoMassModel.cpp: in the reference's sources, not in its executable
+  Glottis *glottis = &triangular;
   Tube tube;       // Synthesizer::tube
   Tube prevTube;   // Synthesizer::prevTube
   Tube newTube;    // the caller-owned frame tube
@@ -52,7 +55,8 @@ struct RefVoice {
   double outputFlow[256] = {0};  // zero-initialised (Synthesizer.cpp:617 reads [0] first)
   double fs = 22050.0;
 
-  RefVoice(double fs_hz, unsigned seed) : fs(fs_hz) {
+  RefVoice(double fs_hz, unsigned seed, int glottis_model = 0) : fs(fs_hz) {
+    if (glottis_model == 1) glottis = &twoMass;
     tds.timeStep = 1.0 / fs_hz;
     outputPressureFilter.createChebyshev(7000.0 / fs_hz, false, 8);
     tds.resetMotion();        // Synthesizer::reset, Synthesizer.cpp:231-250
@@ -61,7 +65,7 @@ struct RefVoice {
     // reference compiled with SAMPLING_RATE = fs would (identical at 22050 Hz).
     tds.transglottalPressureFilter.createChebyshev(50.0 / fs_hz, false, 4);
     tds.transglottalPressureFilter.resetBuffers();
-    glottis.resetMotion();
+    glottis->resetMotion();
     outputPressureFilter.resetBuffers();
     srand(seed);
   }
@@ -84,7 +88,7 @@ struct RefVoice {
   int call(const ao_frame *f, int n, double *out) {
     loadFrame(f);
     const double *g = f->glottis;
-    const int ng = (int)glottis.controlParam.size();
+    const int ng = (int)glottis->controlParam.size();
     if (!latched) {
       prevTube = newTube;
       for (int i = 0; i < ng; ++i) prevGlottis[i] = g[i];
@@ -96,20 +100,20 @@ struct RefVoice {
       double ratio = (double)i / (double)n;
       double ratio1 = 1.0 - ratio;
       tube.interpolate(&prevTube, &newTube, ratio);
-      for (int k = 0; k < ng; ++k) glottis.controlParam[k].x = ratio1 * prevGlottis[k] + ratio * g[k];
-      glottis.calcGeometry();
+      for (int k = 0; k < ng; ++k) glottis->controlParam[k].x = ratio1 * prevGlottis[k] + ratio * g[k];
+      glottis->calcGeometry();
       double l[2], a[2];
-      glottis.getTubeData(l, a);
+      glottis->getTubeData(l, a);
       tube.setGlottisGeometry(l, a);
-      tube.setAspirationStrength(glottis.getAspirationStrength_dB());
+      tube.setAspirationStrength(glottis->getAspirationStrength_dB());
       tds.setTube(&tube, tds.getSampleIndex() != 0);
       tds.setFlowSource(0.0, -1);
-      tds.setPressureSource(glottis.controlParam[Glottis::PRESSURE].x, Tube::FIRST_TRACHEA_SECTION);
+      tds.setPressureSource(glottis->controlParam[Glottis::PRESSURE].x, Tube::FIRST_TRACHEA_SECTION);
       double p[4] = {tds.getSectionPressure(Tube::LAST_TRACHEA_SECTION),
                      tds.getSectionPressure(Tube::LOWER_GLOTTIS_SECTION),
                      tds.getSectionPressure(Tube::UPPER_GLOTTIS_SECTION),
                      tds.getSectionPressure(Tube::FIRST_PHARYNX_SECTION)};
-      glottis.incTime(1.0 / fs, p);
+      glottis->incTime(1.0 / fs, p);
       double flow = tds.proceedTimeStep();
       int pos = tds.getSampleIndex();
       int k = pos & 255;
@@ -149,7 +153,7 @@ long afsref_rand_calls(void) { return g_rand_calls; }
 // opt (optional): every field of TdsModel::Options (TdsModel.h:83-95), in ao_options layout.
 long afsref_utterance_opt(const ao_frame *frames, int F, int hop, unsigned seed, double fs, double *out,
                           const ao_options *opt) {
-  RefVoice *v = new RefVoice(fs, seed);
+  RefVoice *v = new RefVoice(fs, seed, opt ? opt->glottis_model : 0);
   if (opt) {
     TdsModel::Options &o = v->tds.options;
     o.turbulenceLosses = opt->turbulence_losses != 0;

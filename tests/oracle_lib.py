@@ -43,12 +43,12 @@ class AoOptions(ctypes.Structure):
                 ("generate_noise_sources", ctypes.c_int), ("radiation_from_skin", ctypes.c_int),
                 ("piriform_fossa", ctypes.c_int), ("inner_length_corrections", ctypes.c_int),
                 ("transvelar_coupling", ctypes.c_int), ("glottis_loss", ctypes.c_int), ("solver", ctypes.c_int),
-                ("flow_separation_area_ratio", ctypes.c_double)]
+                ("glottis_model", ctypes.c_int), ("flow_separation_area_ratio", ctypes.c_double)]
 
 
 OPTION_DEFAULTS = {"turbulence_losses": 1, "soft_walls": 1, "generate_noise_sources": 1, "radiation_from_skin": 1,
                    "piriform_fossa": 0, "inner_length_corrections": 1, "transvelar_coupling": 0, "glottis_loss": 0,
-                   "solver": 0, "flow_separation_area_ratio": 1.0}
+                   "solver": 0, "glottis_model": 0, "flow_separation_area_ratio": 1.0}
 OPTION_NAMES = tuple(OPTION_DEFAULTS)
 
 

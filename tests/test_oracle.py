@@ -169,3 +169,31 @@ def test_options_vs_reference_44k(oracle, opt):
     x = oracle.utterance(frames, 441, 5, 44100.0, opt=opt)
     y = ref.utterance(frames, 441, 5, 44100.0, opt=opt)
     assert np.isfinite(x).all() and np.array_equal(x, y)
+
+
+TWO_MASS_GLOTTIS = [120.0, 8000.0, 0.01, 0.01, 0.0, 1.0]  # TwoMassModel controls (TwoMassModel.cpp:17-24)
+
+
+@pytest.mark.parametrize("opt", [{"glottis_model": 1}, {"glottis_model": 1, "solver": 1},
+                                 {"glottis_model": 1, "glottis_loss": 2, "transvelar_coupling": 1}],
+                         ids=["two_mass", "two_mass+sor", "two_mass+variable_loss+transvelar"])
+@pytest.mark.parametrize("fs,hop", [(22050.0, 220), (44100.0, 441)])
+def test_two_mass_vs_reference(oracle, opt, fs, hop):
+    """TwoMassModel in place of TriangularGlottis (control 5 = damping factor, aspiration at
+    the Glottis default) against the reference's own TwoMassModel.cpp, bit for bit."""
+    from oracle_lib import RefLib
+    try:
+        ref = RefLib()
+    except FileNotFoundError:
+        pytest.skip("reference build not available")
+    sh = default_shapes()
+    f = oracle.af_to_frame(sh["a:"])
+    f["glottis"] = TWO_MASS_GLOTTIS
+    g = oracle.af_to_frame(sh["i:"])
+    g["velum_opening_cm2"] = 0.3
+    g["glottis"] = [160.0, 9000.0, 0.02, -0.01, 0.02, 1.5]
+    frames = np.stack([f, f, g, g, f])
+    x = oracle.utterance(frames, hop, 4, fs, opt=opt)
+    y = ref.utterance(frames, hop, 4, fs, opt=opt)
+    assert np.isfinite(x).all() and np.abs(x).max() > 1e-4
+    assert np.array_equal(x, y)
