@@ -35,7 +35,7 @@ class AfsOptions(ctypes.Structure):
                 ("generate_noise_sources", ctypes.c_int32), ("radiation_from_skin", ctypes.c_int32),
                 ("piriform_fossa", ctypes.c_int32), ("inner_length_corrections", ctypes.c_int32),
                 ("transvelar_coupling", ctypes.c_int32), ("glottis_loss", ctypes.c_int32),
-                ("flow_separation_area_ratio", ctypes.c_double)]
+                ("glottis_model", ctypes.c_int32), ("flow_separation_area_ratio", ctypes.c_double)]
 
 
 class AfsTargetSequence(ctypes.Structure):

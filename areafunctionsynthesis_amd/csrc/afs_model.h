@@ -52,6 +52,14 @@ constexpr double G_MASS0 = 0.12, G_MASS1 = 0.03, G_DAMP0 = 0.1, G_DAMP1 = 0.6;
 constexpr double G_K0 = 80000.0, G_K1 = 8000.0, G_KC0 = 240000.0, G_KC1 = 24000.0;
 constexpr double G_KCOUPLE = 25000.0, G_INLET = 0.05, G_OUTLET = 0.01;
 constexpr double G_NAT_F0 = 129.0, G_F0_DIV_Q = 125.51;
+// TwoMassModel static parameters (TwoMassModel.cpp:36-58).
+constexpr double TM_REST_LEN = 1.3, TM_REST_THICK0 = 0.25, TM_REST_THICK1 = 0.05;
+constexpr double TM_MASS0 = 0.125, TM_MASS1 = 0.025, TM_DAMP0 = 0.1, TM_DAMP1 = 0.6;
+constexpr double TM_K0 = 80000.0, TM_K1 = 8000.0, TM_ETA0 = 100.0, TM_ETA1 = 100.0;
+constexpr double TM_KC0 = 240000.0, TM_KC1 = 24000.0, TM_CETA0 = 500.0, TM_CETA1 = 500.0;
+constexpr double TM_KCOUPLE = 25000.0, TM_CRIT_WIDTH = 0.0, TM_NAT_F0 = 158.0, TM_F0_DIV_Q = 100.0;
+constexpr double TM_CHINK_LEN = 0.2;
+constexpr double GLOTTIS_DEFAULT_ASPIRATION_DB = -40.0;  // Glottis.cpp:5
 
 // A section is "static" when nothing about its geometry changes during synthesis:
 // trachea, nose beyond the velum taper (nose[4..18]), fossa, sinuses.
@@ -177,6 +185,7 @@ inline afs_options default_options() {
   o.inner_length_corrections = 1;
   o.transvelar_coupling = 0;
   o.glottis_loss = AFS_ENTRANCE_LOSS_STANDARD;
+  o.glottis_model = AFS_GLOTTIS_TRIANGULAR;
   o.flow_separation_area_ratio = 1.0;
   return o;
 }

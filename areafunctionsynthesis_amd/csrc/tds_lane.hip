@@ -74,6 +74,77 @@ __device__ void seed_rng(int32_t *rng, int64_t bp, uint32_t seed) {
 // ---------------------------------------------------------------------------
 // TriangularGlottis (TriangularGlottis.cpp:154-576).  relx: cur0, cur1, prev0, prev1.
 // ---------------------------------------------------------------------------
+// TwoMassModel (TwoMassModel.cpp): calcGeometry/getTubeData (:359-440), then incTime
+// (:157-349), in the reference's operand order.
+__device__ void two_mass_glottis(const double gp[6], const Col &RELX, const Col &P, const Col &AREA,
+                                 const Col &LEN, const Col &VOL, double T) {
+  double Q = 1.0 + (gp[0] - TM_NAT_F0) / TM_F0_DIV_Q;
+  if (Q < 0.05) Q = 0.05;
+  const double f = sqrt(Q);
+  const double len = TM_REST_LEN * f, th0 = TM_REST_THICK0 / f, th1 = TM_REST_THICK1 / f;
+  const double rel[2] = {RELX[0], RELX[1]}, prev[2] = {RELX[2], RELX[3]};
+  const double rest[2] = {gp[2], gp[3]};
+  {
+    double ab[2];
+    for (int i = 0; i < 2; ++i) {
+      ab[i] = rest[i] + rel[i];
+      if (ab[i] < 0.0) ab[i] = 0.0;
+    }
+    double passive = 2.0 * gp[3];
+    if (passive < 0.0) passive = 0.0;
+    double chink = passive * TM_CHINK_LEN + gp[4];
+    if (chink < 0.0) chink = 0.0;
+    const double a0 = clampA(2.0 * len * ab[0] + chink), a1 = clampA(2.0 * len * ab[1] + chink);
+    AREA[S_GLOT_LO] = a0; LEN[S_GLOT_LO] = th0; VOL[S_GLOT_LO] = a0 * th0;
+    AREA[S_GLOT_UP] = a1; LEN[S_GLOT_UP] = th1; VOL[S_GLOT_UP] = a1 * th1;
+  }
+  const double pr[4] = {P[S_LAST_TRACHEA], P[S_GLOT_LO], P[S_GLOT_UP], P[S_PHARYNX0]};
+  const double critX = 0.5 * TM_CRIT_WIDTH;
+  const double ab[2] = {rest[0] + rel[0], rest[1] + rel[1]};
+  const double minRel[2] = {critX - rest[0], critX - rest[1]};
+  const double m[2] = {TM_MASS0 / Q, TM_MASS1 / Q};
+  const double k[2] = {TM_K0 * Q, TM_K1 * Q};
+  const double eta[2] = {TM_ETA0, TM_ETA1};
+  double ck[2] = {TM_KC0 * Q, TM_KC1 * Q};
+  double ceta[2] = {TM_CETA0, TM_CETA1};
+  const double kc = TM_KCOUPLE * Q * Q;
+  const double df = gp[5];
+  double dr[2] = {TM_DAMP0, TM_DAMP1};
+  if (ab[0] <= critX) dr[0] += 1.0;
+  if (ab[1] <= critX) dr[1] += 1.0;
+  const double r[2] = {2.0 * dr[0] * sqrt(m[0] * k[0]) * df * df, 2.0 * dr[1] * sqrt(m[1] * k[1]) * df * df};
+  double fo[2];
+  if ((ab[0] > TM_CRIT_WIDTH) && (ab[1] > TM_CRIT_WIDTH)) {
+    fo[0] = pr[1] * len * th0; fo[1] = pr[2] * len * th1;
+  } else if ((ab[0] <= TM_CRIT_WIDTH) && (ab[1] > TM_CRIT_WIDTH)) {
+    fo[0] = pr[0] * len * th0; fo[1] = pr[2] * len * th1;
+  } else if ((ab[0] > TM_CRIT_WIDTH) && (ab[1] <= TM_CRIT_WIDTH)) {
+    fo[0] = pr[1] * len * th0; fo[1] = pr[1] * len * th1;
+  } else {
+    fo[0] = pr[0] * len * th0; fo[1] = pr[3] * len * th1;
+  }
+  double nl[2];
+  for (int i = 0; i < 2; ++i) {
+    if (rel[i] > minRel[i]) { ck[i] = 0.0; ceta[i] = 0.0; }
+    const double dx = rel[i] - minRel[i];
+    nl[i] = k[i] * eta[i] * rel[i] * rel[i] * rel[i] + ck[i] * ceta[i] * dx * dx * dx;
+  }
+  const double A = m[0] + r[0] * T + T * T * (k[0] + ck[0]) + kc * T * T;
+  const double B = -kc * T * T;
+  const double Cq = -kc * T * T;
+  const double D = m[1] + r[1] * T + T * T * (k[1] + ck[1]) + kc * T * T;
+  const double E = fo[0] * T * T + 2.0 * m[0] * rel[0] - m[0] * prev[0] + r[0] * T * rel[0] +
+                   T * T * ck[0] * minRel[0] - nl[0] * T * T;
+  const double F = fo[1] * T * T + 2.0 * m[1] * rel[1] - m[1] * prev[1] + r[1] * T * rel[1] +
+                   T * T * ck[1] * minRel[1] - nl[1] * T * T;
+  double det = A * D - B * Cq;
+  if (fabs(det) < 0.000000001) det = 0.000000001;
+  RELX[2] = rel[0];
+  RELX[3] = rel[1];
+  RELX[0] = (E * D - B * F) / det;
+  RELX[1] = (A * F - E * Cq) / det;
+}
+
 __device__ __forceinline__ double glottis_q(double f0) {
   double q = 1.0 + (f0 - G_NAT_F0) / G_F0_DIV_Q;
   return q < 0.05 ? 0.05 : q;
@@ -373,6 +444,10 @@ __device__ double sample_step(const Lane &Ln, const afs_frame *fl, const afs_fra
   double gp[6];
   for (int k = 0; k < 6; ++k) gp[k] = r1 * fl->glottis[k] + ratio * fr->glottis[k];
   const double rel0 = RELX[0], rel1 = RELX[1];
+  const bool two_mass = opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
+  if (two_mass) {
+    two_mass_glottis(gp, RELX, P, AREA, LEN, VOL, 1.0 / T.fs);
+  } else {
   {
     double chink = gp[4] < 0.0 ? 0.0 : gp[4];
     double f = sqrt(glottis_q(gp[0]));
@@ -417,6 +492,7 @@ __device__ double sample_step(const Lane &Ln, const afs_frame *fl, const afs_fra
     RELX[3] = rel1;
     RELX[0] = (Ee * Dq - B * Ff) / det;
     RELX[1] = (A * Ff - Ee * Cq) / det;
+  }
   }
 
   // ---- TdsModel::prepareTimeStep (TdsModel.cpp:718-1010) ----
@@ -487,7 +563,7 @@ __device__ double sample_step(const Lane &Ln, const afs_frame *fl, const afs_fra
     u += U[S_GLOT_UP];
     if (u > 0) R1[S_GLOT_LO] = R1[S_GLOT_LO] + g * fabs(u) * 0.5 * RHO * (1.0 / (ta * ta) - 1.0 / (sa * sa));
   }
-  if (opt.generate_noise_sources) noise_sources(Ln, teeth, gp[5]);
+  if (opt.generate_noise_sources) noise_sources(Ln, teeth, two_mass ? GLOTTIS_DEFAULT_ASPIRATION_DB : gp[5]);
   else for (int d = 0; d < NDIP; ++d) SMP[d] = 0.0;
   double tvflow = 0.0;  // transvelar coupling (TdsModel.cpp:966-980)
   if (opt.transvelar_coupling)

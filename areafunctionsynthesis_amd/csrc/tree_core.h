@@ -234,6 +234,67 @@ AFS_HD inline void glottis_open_close(const double *gp, double cord, double rel0
   }
 }
 
+// TwoMassModel::calcGeometry / getTubeData (TwoMassModel.cpp:359-440) and incTime (:157-349)
+// on lane 0, with the previous sample's pressures X_P4; relative displacements in X_RELX
+// (current 0/1, previous 2/3) as for the triangular glottis.
+AFS_HD inline void two_mass_glottis(double *X, const Consts &C, const double *gp) {
+  double Q = 1.0 + (gp[0] - TM_NAT_F0) * (1.0 / TM_F0_DIV_Q);  // getTensionParameter (:467-485)
+  if (Q < 0.05) Q = 0.05;
+  const double f = sqrt(Q), inv_f = fast_rcp(f), inv_q = fast_rcp(Q);
+  const double len = TM_REST_LEN * f, th0 = TM_REST_THICK0 * inv_f, th1 = TM_REST_THICK1 * inv_f;
+  const double rel0 = X[X_RELX + 0], rel1 = X[X_RELX + 1];
+  const double rest0 = gp[2], rest1 = gp[3];
+  // geometry
+  double a0 = rest0 + rel0, a1 = rest1 + rel1;
+  const double ab0 = a0, ab1 = a1;  // incTime's absolute displacements are not clipped
+  if (a0 < 0.0) a0 = 0.0;
+  if (a1 < 0.0) a1 = 0.0;
+  double passive = 2.0 * rest1;
+  if (passive < 0.0) passive = 0.0;
+  double chink = passive * TM_CHINK_LEN + gp[4];
+  if (chink < 0.0) chink = 0.0;
+  X[X_AREA + 0] = clampA(2.0 * len * a0 + chink);
+  X[X_AREA + 1] = clampA(2.0 * len * a1 + chink);
+  X[X_GLEN + 0] = th0;
+  X[X_GLEN + 1] = th1;
+  // incTime
+  const double crit = 0.5 * TM_CRIT_WIDTH;
+  const double min0 = crit - rest0, min1 = crit - rest1;
+  const double m0 = TM_MASS0 * inv_q, m1 = TM_MASS1 * inv_q;
+  const double k0 = TM_K0 * Q, k1 = TM_K1 * Q;
+  double ck0 = TM_KC0 * Q, ck1 = TM_KC1 * Q, ce0 = TM_CETA0, ce1 = TM_CETA1;
+  const double kc = TM_KCOUPLE * Q * Q;
+  const double df = gp[5];
+  double dr0 = TM_DAMP0, dr1 = TM_DAMP1;
+  if (ab0 <= crit) dr0 += 1.0;
+  if (ab1 <= crit) dr1 += 1.0;
+  const double r0 = 2.0 * dr0 * sqrt(m0 * k0) * df * df, r1 = 2.0 * dr1 * sqrt(m1 * k1) * df * df;
+  const double p0 = X[X_P4 + 0], p1 = X[X_P4 + 1], p2 = X[X_P4 + 2], p3 = X[X_P4 + 3];
+  const bool open0 = ab0 > TM_CRIT_WIDTH, open1 = ab1 > TM_CRIT_WIDTH;
+  const double fp0 = open0 ? p1 : p0;
+  const double fp1 = open1 ? p2 : (open0 ? p1 : p3);
+  const double fo0 = fp0 * len * th0, fo1 = fp1 * len * th1;
+  if (rel0 > min0) { ck0 = 0.0; ce0 = 0.0; }
+  if (rel1 > min1) { ck1 = 0.0; ce1 = 0.0; }
+  const double d0 = rel0 - min0, d1 = rel1 - min1;
+  const double nl0 = k0 * TM_ETA0 * rel0 * rel0 * rel0 + ck0 * ce0 * d0 * d0 * d0;
+  const double nl1 = k1 * TM_ETA1 * rel1 * rel1 * rel1 + ck1 * ce1 * d1 * d1 * d1;
+  const double T = C.h.Tt;
+  const double A = m0 + r0 * T + T * T * (k0 + ck0) + kc * T * T;
+  const double B = -kc * T * T;
+  const double Cq = -kc * T * T;
+  const double D = m1 + r1 * T + T * T * (k1 + ck1) + kc * T * T;
+  const double E = fo0 * T * T + 2.0 * m0 * rel0 - m0 * X[X_RELX + 2] + r0 * T * rel0 + T * T * ck0 * min0 - nl0 * T * T;
+  const double F = fo1 * T * T + 2.0 * m1 * rel1 - m1 * X[X_RELX + 3] + r1 * T * rel1 + T * T * ck1 * min1 - nl1 * T * T;
+  double det = A * D - B * Cq;
+  if (fabs(det) < 0.000000001) det = 0.000000001;
+  const double inv_det = fast_rcp(det);
+  X[X_RELX + 2] = rel0;
+  X[X_RELX + 3] = rel1;
+  X[X_RELX + 0] = (E * D - B * F) * inv_det;
+  X[X_RELX + 1] = (A * F - E * Cq) * inv_det;
+}
+
 // getGlottalEntranceLossCoeffFlucher2011(pressure, d) (TdsModel.cpp:1048-1092)
 AFS_HD inline double fulcher_kent(double pressure_dPa, double d_cm) {
   double pc = pressure_dPa / 979.7;
@@ -419,7 +480,16 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, c
       X[X_AREA + s - DYN0] = clampA(open + ((double)(i * i) * (C.h.nose4_area - open)) * (1.0 / 16));
     }
   }
-  if (gl == 0) {
+  if (gl == 0 && U.opt.glottis_model == AFS_GLOTTIS_TWO_MASS) {
+    double gp[6];
+    for (int k = 0; k < 6; ++k) {
+      gp[k] = r1 * X[X_FRAME + 4 + k] + ratio * X[X_FRAME + 10 + k];
+      X[X_GP + k] = gp[k];
+    }
+    X[X_GP + 5] = GLOTTIS_DEFAULT_ASPIRATION_DB;  // X_GP + 5 is read as the aspiration strength
+    X[X_GP + 6] = r1 * X[X_FRAME + 0] + ratio * X[X_FRAME + 1];
+    two_mass_glottis(X, C, gp);
+  } else if (gl == 0) {
     double gp[6];
     for (int k = 0; k < 6; ++k) {
       gp[k] = r1 * X[X_FRAME + 4 + k] + ratio * X[X_FRAME + 10 + k];

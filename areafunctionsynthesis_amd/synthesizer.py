@@ -63,7 +63,7 @@ class Context:
                 raise TypeError(f"unknown option {k}")
             if k == "flow_separation_area_ratio":
                 setattr(cfg.options, k, float(v))
-            elif k == "glottis_loss":
+            elif k in ("glottis_loss", "glottis_model"):
                 setattr(cfg.options, k, int(v))
             else:
                 setattr(cfg.options, k, int(bool(v)))

@@ -66,6 +66,16 @@ typedef enum afs_solver {
   AFS_SOLVER_SOR = 2       /* TdsModel::SOR_GAUSS_SEIDEL, same sweep order (TdsModel.cpp:2105-2180) */
 } afs_solver;
 
+/* Glottis model driven by the synthesizer: the reference's Synthesizer uses TriangularGlottis
+ * (Synthesizer.h:212-213); TwoMassModel (TwoMassModel.cpp) is the other Glottis subclass in its
+ * sources.  Its six controls are f0, lung pressure, rest displacements 1/2, extra arytenoid
+ * area and damping factor (afs_frame.glottis[5] is the damping factor; aspiration stays at
+ * Glottis::DEFAULT_ASPIRATION_STRENGTH_DB = -40 dB). */
+typedef enum afs_glottis_model {
+  AFS_GLOTTIS_TRIANGULAR = 0,
+  AFS_GLOTTIS_TWO_MASS = 1
+} afs_glottis_model;
+
 /* TdsModel::GlottisLossOptions (TdsModel.h:75-81). */
 typedef enum afs_glottis_loss {
   AFS_ENTRANCE_LOSS_STANDARD = 0,     /* k_ent = 1 */
@@ -85,6 +95,7 @@ typedef struct afs_options {
   int32_t inner_length_corrections; /* 1 */
   int32_t transvelar_coupling;      /* 0 */
   int32_t glottis_loss;             /* afs_glottis_loss, 0 */
+  int32_t glottis_model;            /* afs_glottis_model, 0 (not a TdsModel option: the synthesizer's glottis) */
   double flow_separation_area_ratio; /* 1.0 */
 } afs_options;
 

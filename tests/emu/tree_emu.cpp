@@ -109,6 +109,7 @@ extern "C" long emu_tree_utterance_opt(const afs_frame *frames, int F, int hop, 
   opt.inner_length_corrections = iopt[5];
   opt.transvelar_coupling = iopt[6];
   opt.glottis_loss = iopt[7];
+  opt.glottis_model = iopt[8];
   opt.flow_separation_area_ratio = ratio;
   return run<16>(frames, F, hop, seed, fs, opt, out, nullptr, nullptr, 0);
 }

@@ -268,3 +268,24 @@ def test_sor_solver_vs_oracle(contexts, oracle, opt):
         # SOR's coarse residual bound makes it a different solution from the Cholesky's
         z = oracle.utterance(frames, hop, 9, fs, opt=opt)
         assert not np.array_equal(x, z)
+
+
+@pytest.mark.parametrize("solver", SOLVERS + ("sor",))
+def test_two_mass_glottis_vs_oracle(contexts, oracle, solver):
+    """afs_options.glottis_model = AFS_GLOTTIS_TWO_MASS (TwoMassModel.cpp; control 5 is the
+    damping factor) against the oracle, which test_oracle.py pins to the reference's own
+    TwoMassModel bit for bit."""
+    sh = default_shapes()
+    f = oracle.af_to_frame(sh["a:"])
+    f["glottis"] = [120.0, 8000.0, 0.01, 0.01, 0.0, 1.0]
+    g = oracle.af_to_frame(sh["i:"])
+    g["velum_opening_cm2"] = 0.3
+    g["glottis"] = [160.0, 9000.0, 0.02, -0.01, 0.02, 1.5]
+    frames = np.stack([f, f, g, g, f])
+    for fs, hop in ((22050.0, 220), (44100.0, 441)):
+        ctx = contexts(fs, solver, glottis_model=1)
+        y = ctx.synthesize(np.ascontiguousarray(frames[None]), hop, seeds=np.array([4], np.uint32))
+        x = oracle.utterance(frames, hop, 4, fs, opt={"glottis_model": 1, "solver": int(solver == "sor")})
+        assert np.abs(x).max() > 1e-4
+        assert np.abs(y[0, :2048] - x[:2048]).max() <= GOLD_TOL, (fs, float(np.abs(y[0] - x).max()))
+        assert float(np.sqrt(np.mean((y[0] - x) ** 2))) < RMS_TOL

@@ -42,7 +42,7 @@ def emu():
         o = dict(OPTION_DEFAULTS, **opt)
         iopt = np.array([o[k] for k in ("turbulence_losses", "soft_walls", "generate_noise_sources",
                                         "radiation_from_skin", "piriform_fossa", "inner_length_corrections",
-                                        "transvelar_coupling", "glottis_loss")], dtype=np.int32)
+                                        "transvelar_coupling", "glottis_loss", "glottis_model")], dtype=np.int32)
         fr = np.ascontiguousarray(fr, dtype=FRAME_DTYPE)
         out = np.zeros((fr.size - 1) * hop)
         n = lib.emu_tree_utterance_opt(fr.ctypes.data, fr.size, hop, seed, fs, iopt.ctypes.data,
@@ -83,7 +83,8 @@ def test_lane_width_invariance(emu, golden_dir, W):
 
 @pytest.mark.parametrize("opt", [{"transvelar_coupling": 1}, {"glottis_loss": 1}, {"glottis_loss": 2},
                                  {"flow_separation_area_ratio": 1.2}, {"piriform_fossa": 1, "soft_walls": 0},
-                                 {"transvelar_coupling": 1, "glottis_loss": 2, "generate_noise_sources": 0}],
+                                 {"transvelar_coupling": 1, "glottis_loss": 2, "generate_noise_sources": 0},
+                                 {"glottis_model": 1}],
                          ids=lambda o: "+".join(f"{k}={v}" for k, v in o.items()))
 def test_options_vs_oracle(emu, oracle, opt):
     """The tree decomposition of every TdsModel option (the SOR solver runs in the lane kernel)."""
@@ -96,6 +97,8 @@ def test_options_vs_oracle(emu, oracle, opt):
     g = oracle.af_to_frame(sh["z"])
     g["velum_opening_cm2"] = 0.5
     g["glottis"] = [110.0, 8000.0, 0.02, 0.01, 0.0, -30.0]
+    if opt.get("glottis_model"):  # control 5 is the two-mass model's damping factor
+        f["glottis"][5], g["glottis"][5] = 1.0, 1.5
     frames = np.stack([f, g, g, f])
     for fs, hop in ((22050.0, 300), (44100.0, 441)):
         x = emu.opt(frames, hop, 5, fs, opt)
