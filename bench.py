@@ -34,6 +34,17 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (spec)
 FLOPS_PER_SAMPLE = 1068.0
 
 
+def pmc_traffic(kernel: str, workload: str, batch: int, samples: int, hop: int):
+    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/pmc_traffic.json,
+    written by tools/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE runs of this same
+    command), or None when no pass covers this configuration."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    e = json.load(open(path)).get(f"{kernel}|{workload}|B={batch}|T={samples}|hop={hop}")
+    return (e["traffic_bytes_per_launch"], e["tag"]) if e else (None, None)
+
+
 def frame_bytes_per_sample(hop: int) -> float:
     # SURVEY.md 8(d): one 1072-B frame per hop samples + one 8-B fp64 output sample
     return 1072.0 / hop + 8.0
@@ -181,6 +192,10 @@ def main() -> None:
         alg_bytes = samples_per_launch * frame_bytes_per_sample(hop)
         achieved_gbs = alg_bytes / avg_launch_s / 1e9
         flops = samples_per_launch * FLOPS_PER_SAMPLE
+        kname = "lane_synth_kernel" if args.solver == "cholesky" else "tree_synth_kernel"
+        traffic, traffic_tag = (None, None)
+        if launches_per_step == 1:
+            traffic, traffic_tag = pmc_traffic(kname, args.workload, B, T, hop)
         result = {
             "metric": "audio samples/s (whole node) on 64k-utterance batch; max-abs err vs CPU ref",
             "value": value,
@@ -216,8 +231,11 @@ def main() -> None:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
-                "traffic": None,
-                "kernel": "lane_synth_kernel" if args.solver == "cholesky" else "tree_synth_kernel",
+                "traffic": traffic,
+                "traffic_unit": "bytes per launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
+                "traffic_source": f"profiles/pmc_traffic.json [{traffic_tag}]" if traffic else None,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "kernel": kname,
                 "avg_launch_ms": avg_launch_s * 1e3,
                 "launches_per_step": launches_per_step,
                 "bytes_per_sample": frame_bytes_per_sample(hop),

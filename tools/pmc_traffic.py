@@ -1,0 +1,64 @@
+"""Summarise the FETCH_SIZE / WRITE_SIZE passes of tools/gpu_session.sh (step `pmc`) into the
+per-launch HBM traffic that bench.py reports as roofline.traffic.
+
+usage: python tools/pmc_traffic.py --tag r01_v2j [--batch 8192 --seconds 1 --fs 44100 --hop 441]
+
+Corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a coalesced streaming read,
+so it is doubled; WRITE_SIZE is taken as is.  The result is merged into profiles/pmc_traffic.json
+under a key that names the workload, so bench.py only uses it for the same configuration.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def key(kernel: str, workload: str, batch: int, samples: int, hop: int) -> str:
+    return f"{kernel}|{workload}|B={batch}|T={samples}|hop={hop}"
+
+
+def per_launch(path: str, kernel: str) -> list[float]:
+    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    return [float(r["Counter_Value"]) for r in rows]
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--dir", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--kernel", default="tree_synth_kernel")
+    ap.add_argument("--workload", default="static")
+    ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--samples", type=int, default=44100)
+    ap.add_argument("--hop", type=int, default=441)
+    a = ap.parse_args()
+    fetch = per_launch(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"), a.kernel)
+    write = per_launch(os.path.join(a.dir, "pmc_write", "run_counter_collection.csv"), a.kernel)
+    if not fetch or not write:
+        raise SystemExit("no launches of the kernel in the PMC passes")
+    kib = 1024.0
+    fetch_b = 2.0 * kib * sum(fetch) / len(fetch)   # gfx950: FETCH_SIZE = half the read bytes
+    write_b = kib * sum(write) / len(write)
+    entry = {
+        "tag": a.tag,
+        "fetch_size_kib": fetch, "write_size_kib": write,
+        "read_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+        "traffic_bytes_per_launch": fetch_b + write_b,
+        "correction": "read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE; KiB -> bytes",
+    }
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    db = json.load(open(path)) if os.path.exists(path) else {}
+    db[key(a.kernel, a.workload, a.batch, a.samples, a.hop)] = entry
+    with open(path, "w") as f:
+        json.dump(db, f, indent=1, sort_keys=True)
+        f.write("\n")
+    print(json.dumps(entry))
+
+
+if __name__ == "__main__":
+    main()
