@@ -104,6 +104,25 @@ enum : int { ST_E, ST_ALPHA, ST_WC1, ST_WC2, ST_LW, ST_L, ST_R, ST_N };
 struct alignas(8) Topo {
   int8_t src, br, urbr, out0, out1, e0, e1, e2;
 };
+// Per section s (index NS: an absent slot), the LDS doubles of the utterance block that the
+// matrix row of its in-current and its state update touch besides its own section, as
+// indices into the block (tree_core.h layout).  Absent neighbours point at the zero slot
+// (reads) or the sink slot (writes), so the phases load one record per slot and branch only
+// on the row kind.
+//   row:    x_la/x_ra/x_ea = L, R1, E of the source section when it is dynamic (X_L, X_R1,
+//           X_E), c_la/c_ra/c_ea the same constants when it is static (else 0.0); x_da = its
+//           D; x_ub/x_urb = flow and d/dt of the bifurcation partner; x_sx = the source term
+//           (dipole sample, lung pressure); x_e0..x_e2 = the section's edges (X_OFF).
+//   update: x_o0/x_o1 = flows of the output currents; x_ur/x_un/x_p4 = where d/dt and the
+//           noise-smoothed value of the in-current and the pressure are published.
+enum : uint16_t { SR_BIF = 1, SR_JUNCTION = 2, SR_RADIATION = 4 };
+struct alignas(16) SecRec {
+  double c_la, c_ra, c_ea;
+  int16_t x_la, x_ra, x_ea, x_da, x_ub, x_urb, x_sx, x_e0, x_e1, x_e2;
+  int16_t x_o0, x_o1, x_ur, x_un, x_p4;
+  uint16_t flags;
+};
+static_assert(sizeof(SecRec) == 64, "SecRec: four 16-byte loads");
 // Scalars of the time loop (copies of Tables fields; see build_tables).
 struct Hot {
   double fs, dt, dtTH1, noise_amp_F, noise_lp_c, noise_x_2000, sqrt12, nose4_area, fossa_R0;
@@ -130,6 +149,7 @@ struct Consts {
   int8_t un_slot[NC];  // X_UN slot of a current, -1: none
   Topo topo[NS];
   double stat[NSTATIC][ST_N];
+  SecRec sec[NS + 1];
 };
 
 struct Tables {

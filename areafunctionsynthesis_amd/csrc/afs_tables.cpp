@@ -465,6 +465,43 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
     q.e1 = (int8_t)t->edge[s][1];
     q.e2 = (int8_t)t->edge[s][2];
   }
+  // per-section records of the row and update phases (afs_model.h SecRec)
+  const int16_t zero = (int16_t)(X_U + U_ZERO), sink = (int16_t)(X_U + U_SINK);
+  auto dyn = [](int s) { return s >= tree::DYN0 && s < tree::DYN0 + tree::NDYNS; };
+  for (int s = 0; s <= NS; ++s) {
+    SecRec &q = c.sec[s];
+    std::memset(&q, 0, sizeof q);
+    const bool real = s < NS;
+    const int a = real ? t->src[s] : -1;
+    int br = -1;
+    if (a >= 0) br = (t->cout0[a] == s) ? t->cout1[a] : t->cout0[a];
+    const bool da = a >= 0 && dyn(a), sa = a >= 0 && !dyn(a);
+    q.x_la = da ? (int16_t)(X_L + a - tree::DYN0) : zero;
+    q.x_ra = da ? (int16_t)(X_R1 + a - tree::DYN0) : zero;
+    q.x_ea = da ? (int16_t)(X_E + a - tree::DYN0) : zero;
+    q.c_la = sa ? t->L[a] : 0.0;
+    q.c_ra = sa ? t->R[a] : 0.0;
+    q.c_ea = sa ? t->E[a] : 0.0;
+    q.x_da = a >= 0 ? (int16_t)(X_D + a) : zero;
+    q.x_ub = br >= 0 ? (int16_t)(X_U + br) : zero;
+    q.x_urb = br >= 0 && c.ur_slot[br] >= 0 ? (int16_t)(X_UR + c.ur_slot[br]) : zero;
+    q.x_sx = (s >= S_PHARYNX0 && s <= S_LAST_MOUTH) ? (int16_t)(X_SMP + s - S_PHARYNX0)
+             : (real && s == 0)                    ? (int16_t)(X_GP + 1)
+                                                   : zero;
+    const int16_t esink = (int16_t)(X_OFF + EDGE_SINK);
+    q.x_e0 = real && t->edge[s][0] >= 0 ? (int16_t)(X_OFF + t->edge[s][0]) : esink;
+    q.x_e1 = real && t->edge[s][1] >= 0 ? (int16_t)(X_OFF + t->edge[s][1]) : esink;
+    q.x_e2 = real && t->edge[s][1] >= 0 && t->edge[s][2] >= 0 ? (int16_t)(X_OFF + t->edge[s][2]) : esink;
+    const int o0 = real ? t->cout0[s] : -1, o1 = real ? t->cout1[s] : -1;
+    q.x_o0 = (int16_t)(X_U + (o0 >= 0 ? o0 : U_ZERO));
+    q.x_o1 = (int16_t)(X_U + (o1 >= 0 ? o1 : U_ZERO));
+    q.x_ur = real && c.ur_slot[s] >= 0 ? (int16_t)(X_UR + c.ur_slot[s]) : sink;
+    q.x_un = real && c.un_slot[s] >= 0 ? (int16_t)(X_UN + c.un_slot[s]) : sink;
+    q.x_p4 = (s >= S_LAST_TRACHEA && s <= S_PHARYNX0) ? (int16_t)(X_P4 + s - S_LAST_TRACHEA) : sink;
+    q.flags = (uint16_t)((br >= 0 ? SR_BIF : 0) |
+                         (real && a >= S_PHARYNX0 && s <= S_LAST_MOUTH ? SR_JUNCTION : 0) |
+                         (s == S_LAST_MOUTH || s == S_LAST_NOSE ? SR_RADIATION : 0));
+  }
   for (int k = 0; k < NSTATIC; ++k) {
     int s = k < 23 ? k : k + 46;
     c.stat[k][ST_E] = t->E[s];

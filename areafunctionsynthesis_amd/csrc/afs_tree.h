@@ -25,7 +25,7 @@ struct TreeArgs {
 #define AFS_TREE_W 16
 #endif
 #ifndef AFS_TREE_WPB
-#define AFS_TREE_WPB 1
+#define AFS_TREE_WPB 4
 #endif
 #ifndef AFS_TREE_MIN_WAVES
 #define AFS_TREE_MIN_WAVES 1  // waves per SIMD the register allocation must allow

@@ -989,81 +989,106 @@ AFS_HD inline double sec_R1(const double *X, const Consts &C, int s) {
   return (s >= DYN0 && s < DYN0 + NDYNS) ? X[X_R1 + s - DYN0] : C.stat[static_index(s)][ST_R];
 }
 
+// The section records of this lane's slots (absent slots read the record of index NS).
 template <int W>
-AFS_HD inline void phase_rows(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
+AFS_HD inline void load_sec_recs(int gl, const Consts &C, SecRec *rec) {
+#pragma unroll
+  for (int j = 0; j < Shape<W>::NSL; ++j) {
+    const int s = slot_section<W>(j, gl);
+    rec[j] = C.sec[s < 0 ? NS : s];
+  }
+}
+
+template <int W>
+AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, double *__restrict__ Xw,
+                              const Uni &U, const Consts &C) {
+  // X (reads) and Xw (writes) are the same utterance block; the phase writes only the
+  // solver arrays (X_DIAG, X_RHS, X_OFF), which it never reads.  The slot loop is one
+  // branch-free block: both row forms are evaluated and selected per lane, an absent slot
+  // writes into the sink slots; the radiation rows follow.
   using S = Shape<W>;
   const double idt = C.h.inv_dtTH;
   const afs_options &opt = U.opt;
+  SecRec rec[S::NSL];
+  load_sec_recs<W>(gl, C, rec);
+  if (gl == 0) Xw[X_OFF + EDGE_ZERO] = 0.0;  // the solver's zero edge (union slot)
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
-    const int s = slot_section<W>(j, gl);
-    if (s < 0) continue;
     const bool dyn = j < S::ND;
-    const int i = s;  // current i flows into section s
+    const int s0 = slot_section<W>(j, gl);
+    const int s = s0 < 0 ? (dyn ? DYN0 : 0) : s0;
+    const int i = s0 < 0 ? NODE_SINK : s;  // current i flows into section s
+    const SecRec &q = rec[j];
     const double *ks = C.stat[static_index(s)];
     const double LB = dyn ? X[X_L + s - DYN0] : ks[ST_L];
     const double RB = dyn ? X[X_R0 + s - DYN0] : ((s == S_FOSSA0 && !opt.piriform_fossa) ? C.h.fossa_R0 : ks[ST_R]);
     const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
-    const double AB = dyn ? X[X_AREA + s - DYN0] : C.h.area_last_nose;  // static: only used by s = 83
-    const double EB = sec_E(X, C, s), DB = X[X_D + s];
-    const Topo tp = C.topo[s];
-    const int a = tp.src;
-    double LA = 0.0, RA = 0.0, EA = 0.0, DA = 0.0;
-    if (a != -1) { LA = sec_L(X, C, a); RA = sec_R1(X, C, a); EA = sec_E(X, C, a); DA = X[X_D + a]; }
-    double LAB = LA + LB, RAB = RA + RB;
-    const int br = tp.br;  // the other output of the source section (bifurcations)
+    const double EB = dyn ? X[X_E + s - DYN0] : ks[ST_E], DB = X[X_D + s];
+    // source section a: a static source's constants come from the record, a dynamic one's
+    // from X (the other term is an exact 0.0; no source: both are)
+    const double LA = q.c_la + X[q.x_la], RA = q.c_ra + X[q.x_ra], EA = q.c_ea + X[q.x_ea];
+    const double DA = X[q.x_da];
+    const double LAB0 = LA + LB, RAB = RA + RB;
     double Sx = 0.0;
-    if (s >= S_PHARYNX0 && s <= S_LAST_MOUTH) Sx -= X[X_SMP + s - S_PHARYNX0];
-    if (s == 0) Sx -= X[X_GP + 1];  // lung pressure source at section 0
-    double m, rhs;
-    if (br != -1) {
-      double uB = R.u[j], uBr = R.ur[j], uD = X[X_U + br], uDr = X[X_UR + tp.urbr];
-      double F = LAB * idt + RAB;
-      double H = -idt * (LAB * uB + LA * uD) - (TH1 / TH) * (LAB * uBr + LA * uDr) + Sx;
-      m = -EB - EA - F;
-      rhs = H + DB - DA;
-    } else {
-      double uu = R.u[j], uur = R.ur[j];
-      if (opt.inner_length_corrections && a >= S_PHARYNX0 && s <= S_LAST_MOUTH)
-        LAB += junction_l(X[X_AREA + a - DYN0], AB);
-      double G = LAB * idt + RAB;
-      double H = -uur * LAB * (TH1 / TH) - (LAB * uu) * idt + Sx;
-      m = -EB - G;
-      if (a != -1) m -= EA;
-      rhs = H + DB;
-      if (a != -1) rhs -= DA;
+    Sx -= X[q.x_sx];  // dipole sample (pharynx/mouth) or the lung pressure (section 0)
+    const double uu = R.u[j], uur = R.ur[j];
+    // the source section bifurcates: its other output is current br
+    const double uD = X[q.x_ub], uDr = X[q.x_urb];
+    const double Fb = LAB0 * idt + RAB;
+    const double Hb = -idt * (LAB0 * uu + LA * uD) - (TH1 / TH) * (LAB0 * uur + LA * uDr) + Sx;
+    const double mb = -EB - EA - Fb;
+    const double rb = Hb + DB - DA;
+    // simple junction, with Sondhi's inner length correction between pharynx/mouth sections
+    double LAB = LAB0;
+    if (dyn) {
+      const double jl = junction_l(X[q.x_la + (X_AREA - X_L)], X[X_AREA + s - DYN0]);
+      if (opt.inner_length_corrections && (q.flags & SR_JUNCTION)) LAB += jl;
     }
-    X[X_DIAG + i] = -m;
-    X[X_RHS + i] = -rhs;
+    const double G = LAB * idt + RAB;
+    const double H = -uur * LAB * (TH1 / TH) - (LAB * uu) * idt + Sx;
+    double m = -EB - G;
+    m -= EA;    // 0.0 without a source
+    double rhs = H + DB;
+    rhs -= DA;  // 0.0 without a source
+    const bool bif = (q.flags & SR_BIF) != 0;
+    Xw[X_DIAG + i] = -(bif ? mb : m);
+    Xw[X_RHS + i] = -(bif ? rb : rhs);
     // edges of section s: (in, out0) = -E, (in, out1) = -E, (out0, out1) = E + L/(dt th) + R1
-    const int e0 = tp.e0, e1 = tp.e1, e2 = tp.e2;
-    if (gl == 0 && j == 0) X[X_OFF + EDGE_ZERO] = 0.0;  // the solver's zero edge (union slot)
-    if (e0 >= 0) X[X_OFF + e0] = -EB;
-    if (e1 >= 0) {
-      X[X_OFF + e1] = -EB;
-      X[X_OFF + e2] = -(-EB - (LB * idt + R1B));
+    Xw[q.x_e0] = -EB;
+    Xw[q.x_e1] = -EB;
+    Xw[q.x_e2] = -(-EB - (LB * idt + R1B));
+  }
+#pragma unroll
+  for (int j = 0; j < S::NSL; ++j) {
+    if (!(rec[j].flags & SR_RADIATION)) continue;
+    // radiation rows of s = 64 / 83 (TdsModel.cpp:1841-1911)
+    const bool dyn = j < S::ND;
+    const int s = slot_section<W>(j, gl);
+    const double *ks = C.stat[static_index(s)];
+    const double LB = dyn ? X[X_L + s - DYN0] : ks[ST_L];
+    const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
+    const double AB = dyn ? X[X_AREA + s - DYN0] : C.h.area_last_nose;
+    const double EB = dyn ? X[X_E + s - DYN0] : ks[ST_E], DB = X[X_D + s];
+    const Topo tp = C.topo[s];
+    const int rc = tp.out0, lc = tp.out1;
+    double uR = X[X_U + rc], uL = X[X_U + lc], uRr = X[X_UR + C.ur_slot[rc]], uLr = X[X_UR + C.ur_slot[lc]];
+    R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
+    R.rad_un[0] = X[X_UN + C.un_slot[rc]]; R.rad_un[1] = X[X_UN + C.un_slot[lc]];
+    const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
+    {
+      double Rrad = fast_div(C.h.rrad_num, 9.0 * PI * PI * AB);
+      double F = LA2 * idt + RA2 + Rrad;
+      double H = -(LA2 * idt) * (uR + uL) - (LA2 * (TH1 / TH)) * (uRr + uLr) + Sr;
+      Xw[X_DIAG + rc] = -(-EB - F);
+      Xw[X_RHS + rc] = -(H - DB);
     }
-    if (s == S_LAST_MOUTH || s == S_LAST_NOSE) {  // radiation rows (TdsModel.cpp:1841-1911)
-      const int rc = tp.out0, lc = tp.out1;
-      double uR = X[X_U + rc], uL = X[X_U + lc], uRr = X[X_UR + C.ur_slot[rc]], uLr = X[X_UR + C.ur_slot[lc]];
-      R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
-      R.rad_un[0] = X[X_UN + C.un_slot[rc]]; R.rad_un[1] = X[X_UN + C.un_slot[lc]];
-      const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
-      {
-        double Rrad = fast_div(C.h.rrad_num, 9.0 * PI * PI * AB);
-        double F = LA2 * idt + RA2 + Rrad;
-        double H = -(LA2 * idt) * (uR + uL) - (LA2 * (TH1 / TH)) * (uRr + uLr) + Sr;
-        X[X_DIAG + rc] = -(-EB - F);
-        X[X_RHS + rc] = -(H - DB);
-      }
-      {
-        double Lrad = fast_div(C.h.lrad_num, 3.0 * PI * sqrt(AB * PI));
-        double LAB2 = LA2 + Lrad;
-        double G = LAB2 * idt + RA2;
-        double H = -idt * (LA2 * uR + LAB2 * uL) - (TH1 / TH) * (LA2 * uRr + LAB2 * uLr) + Sr;
-        X[X_DIAG + lc] = -(-EB - G);
-        X[X_RHS + lc] = -(H - DB);
-      }
+    {
+      double Lrad = fast_div(C.h.lrad_num, 3.0 * PI * sqrt(AB * PI));
+      double LAB2 = LA2 + Lrad;
+      double G = LAB2 * idt + RA2;
+      double H = -idt * (LA2 * uR + LAB2 * uL) - (TH1 / TH) * (LA2 * uRr + LAB2 * uLr) + Sr;
+      Xw[X_DIAG + lc] = -(-EB - G);
+      Xw[X_RHS + lc] = -(H - DB);
     }
   }
 }
@@ -1140,13 +1165,21 @@ AFS_HD inline void solve_backward(int k, int r, bool carried, double *X, const C
 // Phase U: updateVariables (TdsModel.cpp:2046-2098).
 // ---------------------------------------------------------------------------
 template <int W>
-AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
+AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X, double *__restrict__ Xw,
+                                const Uni &U, const Consts &C) {
+  // X (reads) and Xw (writes) are the same utterance block; the phase publishes into X_UR,
+  // X_UN, X_P4, X_TVP and the sink slot, none of which it reads.  The slot loop is one
+  // branch-free block (an absent slot updates a copy of section 0 and publishes into the
+  // sink), so the scheduler can batch the loads of all slots; the per-section extras follow.
   using S = Shape<W>;
   const double c = C.h.noise_lp_c, idt = C.h.inv_dtTH;
+  SecRec rec[S::NSL];
+  load_sec_recs<W>(gl, C, rec);
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
-    const int s = slot_section<W>(j, gl);
-    if (s < 0) continue;
+    const int s0 = slot_section<W>(j, gl);
+    const int s = s0 < 0 ? (j < S::ND ? DYN0 : 0) : s0;
+    const SecRec &q = rec[j];
     double alpha, beta;
     if (j < S::ND) { alpha = R.al[j]; beta = R.be[j]; }
     else { alpha = C.stat[static_index(s)][ST_ALPHA]; beta = static_beta<W>(R, j, U, C, s); }  // same values as phase_network
@@ -1155,18 +1188,14 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
     R.u[j] = unew;
     R.ur[j] = (unew - uold) * idt - (TH1 / TH) * R.ur[j];
     R.un[j] = (1.0 - c) * unew + c * R.un[j];
-    if (C.ur_slot[s] >= 0) X[X_UR + C.ur_slot[s]] = R.ur[j];
-    if (C.un_slot[s] >= 0) X[X_UN + C.un_slot[s]] = R.un[j];
     double cin = 0.0;
     cin += unew;
     double cout = 0.0;
-    const Topo tu = C.topo[s];
-    const int o0 = tu.out0, o1 = tu.out1;
-    if (o0 != -1) cout += X[X_U + o0];
-    if (o1 != -1) cout += X[X_U + o1];
+    cout += X[q.x_o0];  // 0.0 for an absent output
+    cout += X[q.x_o1];
     double net = cin - cout;
     double old = R.p[j];
-    double p = X[X_D + s] + sec_E(X, C, s) * net;
+    double p = X[X_D + s] + (j < S::ND ? X[X_E + s - DYN0] : C.stat[static_index(s)][ST_E]) * net;
     R.p[j] = p;
     double prr = (p - old) * idt - R.pr[j] * (TH1 / TH);
     R.pr[j] = prr;
@@ -1176,18 +1205,30 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, double *X, const Uni &U, con
     double wr = (w - ow) * idt - owr * (TH1 / TH);
     R.wr[j] = wr;
     R.wr2[j] = (wr - owr) * idt - R.wr2[j] * (TH1 / TH);
-    if (s >= S_LAST_TRACHEA && s <= S_PHARYNX0) X[X_P4 + s - S_LAST_TRACHEA] = p;
+  }
+  // publish (all stores after all loads: the scheduler may batch the loads of every slot)
+#pragma unroll
+  for (int j = 0; j < S::NSL; ++j) {
+    Xw[rec[j].x_ur] = R.ur[j];  // for the bifurcation partner (or the sink)
+    Xw[rec[j].x_un] = R.un[j];  // for the noise sources (or the sink)
+    Xw[rec[j].x_p4] = R.p[j];   // p[22..25] for the glottis (or the sink)
+  }
+#pragma unroll
+  for (int j = 0; j < S::NSL; ++j) {
+    const int s = slot_section<W>(j, gl);
     if (U.opt.transvelar_coupling) {
-      if (s == S_MOUTH0 + 2) X[X_TVP] = p;
-      if (s == S_NOSE0 + 2) X[X_TVP + 1] = p;
+      if (s == S_MOUTH0 + 2) Xw[X_TVP] = R.p[j];
+      if (s == S_NOSE0 + 2) Xw[X_TVP + 1] = R.p[j];
     }
-    if (s == S_LAST_MOUTH || s == S_LAST_NOSE) {  // the two radiation currents of this section
-      for (int q = 0; q < 2; ++q) {
-        const int rc = q == 0 ? o0 : o1;
+    if (rec[j].flags & SR_RADIATION) {  // the two radiation currents of s = 64 / 83
+      const Topo tu = C.topo[s];
+      const int o0 = tu.out0, o1 = tu.out1;
+      for (int k = 0; k < 2; ++k) {
+        const int rc = k == 0 ? o0 : o1;
         double un = X[X_U + rc];
-        double ur = (un - R.rad_u[q]) * idt - (TH1 / TH) * R.rad_ur[q];
-        X[X_UR + C.ur_slot[rc]] = ur;
-        X[X_UN + C.un_slot[rc]] = (1.0 - c) * un + c * R.rad_un[q];
+        double ur = (un - R.rad_u[k]) * idt - (TH1 / TH) * R.rad_ur[k];
+        Xw[X_UR + C.ur_slot[rc]] = ur;
+        Xw[X_UN + C.un_slot[rc]] = (1.0 - c) * un + c * R.rad_un[k];
       }
     }
   }
@@ -1237,7 +1278,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   }
   x.sync();
   x.mark(PH_NOISE);
-  x.par([&](int gl, Lane<W> &R) { phase_rows<W>(gl, R, X, U, C); });
+  x.par([&](int gl, Lane<W> &R) { phase_rows<W>(gl, R, X, X, U, C); });
   x.sync();
   x.mark(PH_ROWS);
   const int nr = U.n_rounds;
@@ -1271,7 +1312,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
     x.sync();
   }
   x.mark(PH_BACKWARD);
-  x.par([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, U, C); });
+  x.par([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, X, U, C); });
   x.sync();
   x.mark(PH_UPDATE);
   x.one([&](Lane<W> &R) { R.sample = phase_output(X, U, C); });
