@@ -143,6 +143,27 @@ AFS_HD inline double pivot_recip(double d) {
 #endif
 }
 
+// Square root of a positive, finite, normal operand (areas, Q, masses x stiffnesses; the
+// inputs of this kernel are >= 1e-3): LLVM's correctly rounded f64 sequence (v_rsq_f64 and
+// Goldschmidt/Newton steps) without its range scaling and zero/infinity fix-up, bit-identical
+// to sqrt() for x >= 2^-767 (tools/microbench/f64_ops.hip checks 3M inputs).  About 40 of
+// sqrt()'s 107 cycles of dependent latency are the parts left out.  Host builds call sqrt.
+AFS_HD inline double fast_sqrt(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  return fma(d, h, g);
+#else
+  return sqrt(x);
+#endif
+}
+
 // Reciprocal and quotient of positive, normal operands (areas, surfaces, capacitances) without
 // the scaling/fixup steps of IEEE division: v_rcp_f64 + two Newton steps, and for the quotient
 // one residual correction (within 1 ulp of a / b).  Host builds (the CPU emulator) divide.
@@ -240,7 +261,7 @@ AFS_HD inline void glottis_open_close(const double *gp, double cord, double rel0
 AFS_HD inline void two_mass_glottis(double *X, const Consts &C, const double *gp) {
   double Q = 1.0 + (gp[0] - TM_NAT_F0) * (1.0 / TM_F0_DIV_Q);  // getTensionParameter (:467-485)
   if (Q < 0.05) Q = 0.05;
-  const double f = sqrt(Q), inv_f = fast_rcp(f), inv_q = fast_rcp(Q);
+  const double f = fast_sqrt(Q), inv_f = fast_rcp(f), inv_q = fast_rcp(Q);
   const double len = TM_REST_LEN * f, th0 = TM_REST_THICK0 * inv_f, th1 = TM_REST_THICK1 * inv_f;
   const double rel0 = X[X_RELX + 0], rel1 = X[X_RELX + 1];
   const double rest0 = gp[2], rest1 = gp[3];
@@ -268,7 +289,7 @@ AFS_HD inline void two_mass_glottis(double *X, const Consts &C, const double *gp
   double dr0 = TM_DAMP0, dr1 = TM_DAMP1;
   if (ab0 <= crit) dr0 += 1.0;
   if (ab1 <= crit) dr1 += 1.0;
-  const double r0 = 2.0 * dr0 * sqrt(m0 * k0) * df * df, r1 = 2.0 * dr1 * sqrt(m1 * k1) * df * df;
+  const double r0 = 2.0 * dr0 * fast_sqrt(m0 * k0) * df * df, r1 = 2.0 * dr1 * fast_sqrt(m1 * k1) * df * df;
   const double p0 = X[X_P4 + 0], p1 = X[X_P4 + 1], p2 = X[X_P4 + 2], p3 = X[X_P4 + 3];
   const bool open0 = ab0 > TM_CRIT_WIDTH, open1 = ab1 > TM_CRIT_WIDTH;
   const double fp0 = open0 ? p1 : p0;
@@ -315,9 +336,8 @@ AFS_HD inline double fulcher_kent(double pressure_dPa, double d_cm) {
 AFS_HD inline double junction_l(double A1, double A2) {
   if (A1 < AMIN) A1 = AMIN;
   if (A2 < AMIN) A2 = AMIN;
-  double a, b;
-  if (A1 > A2) { a = sqrt(A1 * (1.0 / PI)); b = sqrt(A2 * (1.0 / PI)); }
-  else { a = sqrt(A2 * (1.0 / PI)); b = sqrt(A1 * (1.0 / PI)); }
+  const double Ahi = A1 > A2 ? A1 : A2, Alo = A1 > A2 ? A2 : A1;  // (one sqrt each, no branch)
+  const double a = fast_sqrt(Ahi * (1.0 / PI)), b = fast_sqrt(Alo * (1.0 / PI));
   const double r = fast_rcp(a * b);
   const double H = 1.0 - (b * b) * r;
   return (8.0 * RHO / (3.0 * PI * PI)) * H * (a * r);
@@ -502,7 +522,7 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, c
     // m ~ 1/q and k ~ q)
     double chink = gp[4] < 0.0 ? 0.0 : gp[4];
     double q = glottis_q(gp[0]);
-    double f = sqrt(q);
+    double f = fast_sqrt(q);
     const double inv_f = fast_rcp(f), inv_q = fast_rcp(q);
     double cord = G_REST_LEN * f;
     const double inv_cord = fast_rcp(cord);
@@ -583,7 +603,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     const double vol = area * len;
     const double inv_area = fast_rcp(area);
     double alpha = 0.0, beta = 0.0;
-    const double r0 = sqrt(area * (1.0 / PI));
+    const double r0 = fast_sqrt(area * (1.0 / PI));
     const double circ = 2.0 * PI * r0;
     double a = r0, b = r0;
     const double rmin = glot ? 0.8 : 1.6;
@@ -730,10 +750,10 @@ AFS_HD inline void dipole_targets(Xc &x, double *X, const Uni &U, const Consts &
   } else if (c.art == VOCAL_FOLDS) {
     gain = 0.5e-7 * exp(X[X_GP + 5] * (2.302585092994045684 / 20.0));  // 10^(dB/20)
   } else {
-    fc = 0.15 * v * sqrt((PI / 4.0) * inv_A);  // 0.15 v / d, d = sqrt(4 A / pi)
+    fc = 0.15 * v * fast_sqrt((PI / 4.0) * inv_A);  // 0.15 v / d, d = sqrt(4 A / pi)
     gain = (fabs(c.obst - teeth) < 0.0001) ? 10.0e-7 : 5.0e-7;
   }
-  double full = gain * fabs(v) * v * v * sqrt(A);
+  double full = gain * fabs(v) * v * v * fast_sqrt(A);
   if (c.lat > 0.1) full = 0.0;
   if (fc < 50.0) fc = 50.0;
   if (fc > 2000.0) fc = 2000.0;
@@ -1083,7 +1103,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
       Xw[X_RHS + rc] = -(H - DB);
     }
     {
-      double Lrad = fast_div(C.h.lrad_num, 3.0 * PI * sqrt(AB * PI));
+      double Lrad = fast_div(C.h.lrad_num, 3.0 * PI * fast_sqrt(AB * PI));
       double LAB2 = LA2 + Lrad;
       double G = LAB2 * idt + RA2;
       double H = -idt * (LA2 * uR + LAB2 * uL) - (TH1 / TH) * (LA2 * uRr + LAB2 * uLr) + Sr;
