@@ -89,8 +89,13 @@ enum : int {
   X_TGLOT = X_GP + 8,          // transglottal-pressure filter x1..x4, y1..y4 (variable entrance loss)
   X_TVEL = X_TGLOT + 8,        // transvelar coupling filters H1, H2: x1..x4, y1..y4 each
   X_TVP = X_TVEL + 16,         // p[43], p[67] after the last update (transvelar filter inputs)
-  X_TOTAL = X_TVP + 2
+  X_TOTAL = X_TVP + 2,
+  // LDS stride of the utterance blocks: 128 B modulo the 256-B bank row, so that the two
+  // utterances of a 32-lane LDS lane group (ds_read_b64: lanes 0-31, 32-63) address the
+  // same slot through disjoint banks
+  X_STRIDE = X_TOTAL + ((16 - X_TOTAL % 32) + 32) % 32
 };
+static_assert(X_STRIDE % 32 == 16, "utterance blocks offset by half a bank row");
 
 // Phase ids for Exec::mark (cycle accounting in tools/phase_prof; a no-op otherwise).
 enum : int {
@@ -484,7 +489,7 @@ AFS_HD inline void frame_load(int gl, Lane<W> &R, double *X, const afs_frame *fl
 // Phase G: tube interpolation (all lanes) and the glottis (lane 0).
 // ---------------------------------------------------------------------------
 template <int W>
-AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C, double ratio) {
+AFS_HD inline void phase_interpolate(int gl, Lane<W> &R, double *X, const Consts &C, double ratio) {
   using S = Shape<W>;
   const double r1 = 1.0 - ratio;
 #pragma unroll
@@ -500,7 +505,13 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, c
       X[X_AREA + s - DYN0] = clampA(open + ((double)(i * i) * (C.h.nose4_area - open)) * (1.0 / 16));
     }
   }
-  if (gl == 0 && U.opt.glottis_model == AFS_GLOTTIS_TWO_MASS) {
+}
+
+// The glottis (lane-uniform inputs: every lane of the utterance computes the same values, see
+// Exec::par_uniform).
+AFS_HD inline void phase_glottis(double *X, const Uni &U, const Consts &C, double ratio) {
+  const double r1 = 1.0 - ratio;
+  if (U.opt.glottis_model == AFS_GLOTTIS_TWO_MASS) {
     double gp[6];
     for (int k = 0; k < 6; ++k) {
       gp[k] = r1 * X[X_FRAME + 4 + k] + ratio * X[X_FRAME + 10 + k];
@@ -509,7 +520,7 @@ AFS_HD inline void phase_geometry(int gl, Lane<W> &R, double *X, const Uni &U, c
     X[X_GP + 5] = GLOTTIS_DEFAULT_ASPIRATION_DB;  // X_GP + 5 is read as the aspiration strength
     X[X_GP + 6] = r1 * X[X_FRAME + 0] + ratio * X[X_FRAME + 1];
     two_mass_glottis(X, C, gp);
-  } else if (gl == 0) {
+  } else {
     double gp[6];
     for (int k = 0; k < 6; ++k) {
       gp[k] = r1 * X[X_FRAME + 4 + k] + ratio * X[X_FRAME + 10 + k];
@@ -721,18 +732,28 @@ AFS_HD inline MinIdx mouth_min(Xc &x, const double *X, P pred) {
   });
 }
 
-// Dipole targets of one constriction (TdsModel.cpp:1456-1602).
+// Dipole targets of one constriction (TdsModel.cpp:1456-1602), in two steps: the first
+// section that contains the obstacle (a ballot over the owners, obstacle_mask) and the
+// arithmetic (dipole_target<ART>), so that the constrictions of a sample run as independent
+// chains; store_target writes them in the reference's order.
+struct DipTarget { int up, dn; double tup, tdn, fc; };
+
 template <int W, class Xc>
-AFS_HD inline void dipole_targets(Xc &x, double *X, const Uni &U, const Consts &C, double teeth, const Cons &c) {
-  const uint64_t M = mouth_mask<W>(x, [&](Lane<W> &R, int j, int m) {
+AFS_HD inline uint64_t obstacle_mask(Xc &x, const double *X, double obst) {
+  return mouth_mask<W>(x, [&](Lane<W> &R, int j, int m) {
     (void)R; (void)j;
     const double pos = X[X_POS + m];
-    return pos <= c.obst && pos + X[X_LEN + m] >= c.obst;
+    return pos <= obst && pos + X[X_LEN + m] >= obst;
   });
-  if (M == 0) return;
-  const int up = __builtin_ctzll(M);  // the first section that contains the obstacle
-  const int dn = (up < NPM - 1) ? up + 1 : DIP_LIPS;
-  double fdn = fast_div(c.obst - X[X_POS + up], X[X_LEN + up]);
+}
+
+// M == 0 (no section contains the obstacle): the result is not stored.
+template <int ART>
+AFS_HD inline DipTarget dipole_target(const double *X, const Consts &C, double teeth, const Cons &c, uint64_t M) {
+  DipTarget t;
+  t.up = M ? __builtin_ctzll(M) : 0;  // the first section that contains the obstacle
+  t.dn = (t.up < NPM - 1) ? t.up + 1 : DIP_LIPS;
+  double fdn = fast_div(c.obst - X[X_POS + t.up], X[X_LEN + t.up]);
   double fup = 1.0 - fdn;
   double A = X[X_AREA + c.narrow - DYN0];
   if (A < 0.1) A = 0.1;
@@ -745,9 +766,9 @@ AFS_HD inline void dipole_targets(Xc &x, double *X, const Uni &U, const Consts &
   if (flow < 0.0) flow = 0.0;
   double v = flow * inv_A;
   double fc = 6000.0, gain = 0.0;
-  if (c.art == LOWER_LIP) {
+  if (ART == LOWER_LIP) {
     gain = 2.0e-7;
-  } else if (c.art == VOCAL_FOLDS) {
+  } else if (ART == VOCAL_FOLDS) {
     gain = 0.5e-7 * exp(X[X_GP + 5] * (2.302585092994045684 / 20.0));  // 10^(dB/20)
   } else {
     fc = 0.15 * v * fast_sqrt((PI / 4.0) * inv_A);  // 0.15 v / d, d = sqrt(4 A / pi)
@@ -757,10 +778,18 @@ AFS_HD inline void dipole_targets(Xc &x, double *X, const Uni &U, const Consts &
   if (c.lat > 0.1) full = 0.0;
   if (fc < 50.0) fc = 50.0;
   if (fc > 2000.0) fc = 2000.0;
+  t.tup = fup * full;
+  t.tdn = fdn * full;
+  t.fc = fc;
+  return t;
+}
+
+template <int W, class Xc>
+AFS_HD inline void store_target(Xc &x, double *X, const DipTarget &t) {
   x.one([&](Lane<W> &R) {
     (void)R;
-    X[X_TGT + up] = fup * full; X[X_CUTN + up] = fc;
-    X[X_TGT + dn] = fdn * full; X[X_CUTN + dn] = fc;
+    X[X_TGT + t.up] = t.tup; X[X_CUTN + t.up] = t.fc;
+    X[X_TGT + t.dn] = t.tdn; X[X_CUTN + t.dn] = t.fc;
   });
 }
 
@@ -820,11 +849,21 @@ AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Con
     }
   };
   // Up to four constrictions in the reference's order: glottis, tongue, second tongue, lip.
+  // (Absent ones keep a dummy of their kind with valid indices; their targets are not stored.)
   const Cons cg = Cons{S_GLOT_LO, S_GLOT_UP, S_GLOT_UP, VOCAL_FOLDS, 1.5, 0.0};
-  Cons ct1 = cg, ct2 = cg, cl = cg;
-  bool has_t1 = false, has_t2 = false, has_l = false;
+  Cons ct1 = Cons{S_GLOT_UP, S_GLOT_UP, S_GLOT_UP, TONGUE, 1.5, 0.0}, ct2 = ct1;
+  Cons cl = Cons{S_GLOT_UP, S_GLOT_UP, S_GLOT_UP, LOWER_LIP, 1.5, 0.0};
+  bool has_t1 = false, has_t2 = false;
   double min_teeth = 1000000.0;
+  // the tongue and the lip minimum: independent scans
   const MinIdx t1 = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) { (void)m; return R.art[j] == TONGUE; });
+  const MinIdx lp = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) { (void)m; return R.art[j] == LOWER_LIP; });
+  if (lp.v < 1.0) {  // the lip constriction's extent (used if it is narrower than a tongue at the teeth)
+    const int s = S_PHARYNX0 + lp.i;
+    cl = Cons{s, s, s, LOWER_LIP, 0.0, 0.0};
+    grow(cl, lp.v, LOWER_LIP);
+    cl.obst = X[X_POS + cl.last + 1 - S_PHARYNX0];
+  }
   if (t1.v < 1.0) {
     has_t1 = true;
     const int s = S_PHARYNX0 + t1.i;
@@ -848,19 +887,21 @@ AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Con
     }
   }
   x.mark(PH_C_T2);
-  const MinIdx lp = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) { (void)m; return R.art[j] == LOWER_LIP; });
-  if (lp.v < 1.0 && lp.v < min_teeth) {
-    has_l = true;
-    const int s = S_PHARYNX0 + lp.i;
-    cl = Cons{s, s, s, LOWER_LIP, 0.0, 0.0};
-    grow(cl, lp.v, LOWER_LIP);
-    cl.obst = X[X_POS + cl.last + 1 - S_PHARYNX0];
-  }
+  const bool has_l = lp.v < 1.0 && lp.v < min_teeth;
   x.mark(PH_C_LIP);
-  dipole_targets<W>(x, X, U, C, teeth, cg);
-  if (has_t1) dipole_targets<W>(x, X, U, C, teeth, ct1);
-  if (has_t2) dipole_targets<W>(x, X, U, C, teeth, ct2);
-  if (has_l) dipole_targets<W>(x, X, U, C, teeth, cl);
+  const uint64_t Mg = obstacle_mask<W>(x, X, cg.obst);
+  const uint64_t M1 = obstacle_mask<W>(x, X, ct1.obst);
+  const uint64_t Ml = obstacle_mask<W>(x, X, cl.obst);
+  const DipTarget tg = dipole_target<VOCAL_FOLDS>(X, C, teeth, cg, Mg);
+  const DipTarget tt1 = dipole_target<TONGUE>(X, C, teeth, ct1, M1);
+  const DipTarget tl = dipole_target<LOWER_LIP>(X, C, teeth, cl, Ml);
+  if (Mg) store_target<W>(x, X, tg);
+  if (has_t1 && M1) store_target<W>(x, X, tt1);
+  if (has_t2) {
+    const uint64_t M2 = obstacle_mask<W>(x, X, ct2.obst);
+    if (M2) store_target<W>(x, X, dipole_target<TONGUE>(X, C, teeth, ct2, M2));
+  }
+  if (has_l && Ml) store_target<W>(x, X, tl);
 }
 
 // Phase N: noise sources (TdsModel.cpp:1630-1708).  Amplitude smoothing of the owned
@@ -1254,15 +1295,29 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
   }
 }
 
+// The new pressure of dynamic section s from the solution, as phase_update computes it (the
+// same operations on the same values), for readers in the update phase itself.
+AFS_HD inline double section_pressure(const double *X, const Consts &C, int s) {
+  const SecRec &q = C.sec[s];
+  double cin = 0.0;
+  cin += X[X_U + s];
+  double cout = 0.0;
+  cout += X[q.x_o0];
+  cout += X[q.x_o1];
+  const double net = cin - cout;
+  return X[X_D + s] + X[X_E + s - DYN0] * net;
+}
+
 // Phase O (lane 0): radiated flow, glottal tone, output filter (TdsModel.cpp:687-705,
 // Synthesizer.cpp:614-627).  Returns the audio sample.
-AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C) {
+// p25 = the new pressure of section 25 (section_pressure), the glottal tone filter's input.
+AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, double p25) {
   double flow = 0.0;
   flow += X[X_U + 93];
   flow += X[X_U + 94];
   flow += X[X_U + 95];
   flow += X[X_U + 96];
-  if (U.opt.radiation_from_skin) flow += iir_run<4>(X + X_TONE, C.h.tone_a, C.h.tone_b, X[X_P4 + 3]);
+  if (U.opt.radiation_from_skin) flow += iir_run<4>(X + X_TONE, C.h.tone_a, C.h.tone_b, p25);
   double op = (flow - X[X_PREVFLOW]) * C.h.inv_dt;
   X[X_PREVFLOW] = flow;
   double y = iir_run<8>(X + X_OUTF, C.h.out_a, C.h.out_b, op);
@@ -1279,7 +1334,8 @@ AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C) {
 template <int W, class Xc>
 AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
   static_assert(W >= TREE_CHAINS, "every solver chain needs a lane of the utterance");
-  x.par([&](int gl, Lane<W> &R) { phase_geometry<W>(gl, R, X, U, C, ratio); });
+  x.par_uniform([&](int gl, Lane<W> &R) { phase_interpolate<W>(gl, R, X, C, ratio); },
+                [&](Lane<W> &R) { (void)R; phase_glottis(X, U, C, ratio); });
   x.sync();
   x.mark(PH_GEOMETRY);
   x.par([&](int gl, Lane<W> &R) { phase_network<W>(gl, R, X, U, C); });
@@ -1332,10 +1388,11 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
     x.sync();
   }
   x.mark(PH_BACKWARD);
-  x.par([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, X, U, C); });
+  // the state update and the output stage (lane-uniform: radiated flow, filters) in one phase
+  x.par_uniform([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, X, U, C); },
+                [&](Lane<W> &R) { R.sample = phase_output(X, U, C, section_pressure(X, C, S_PHARYNX0)); });
   x.sync();
   x.mark(PH_UPDATE);
-  x.one([&](Lane<W> &R) { R.sample = phase_output(X, U, C); });
   x.mark(PH_OUTPUT);
 }
 

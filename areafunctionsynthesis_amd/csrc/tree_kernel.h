@@ -34,6 +34,9 @@ struct GpuExec {
   uint64_t acc[PROF ? PH_COUNT : 1] = {};
   template <class F> __device__ __forceinline__ void par(F f) { f(gl, *R); }
   template <class F> __device__ __forceinline__ void one(F f) { if (gl == 0) f(*R); }
+  // Per-lane work and lane-uniform work in one block: every lane also evaluates the uniform
+  // part (same inputs, same values, same stores), so the two interleave without a branch.
+  template <class F, class G> __device__ __forceinline__ void par_uniform(F f, G g) { f(gl, *R); g(*R); }
   template <class F> __device__ __forceinline__ void lanes(int n, F f) { if (gl < n) f(gl, *R); }
   __device__ __forceinline__ void sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -112,7 +115,7 @@ struct GpuExec {
 // utterance.
 struct WaveLds {
   Consts C;
-  double X[UPB][X_TOTAL];
+  double X[UPB][X_STRIDE];
 };
 
 // prof (PROF only): per wave, PH_COUNT cycle sums (s_memtime) over the launch.

@@ -20,6 +20,7 @@ struct CpuExec {
   Lane<W> *R;
   template <class F> void par(F f) { for (int gl = 0; gl < W; ++gl) f(gl, R[gl]); }
   template <class F> void one(F f) { f(R[0]); }
+  template <class F, class G> void par_uniform(F f, G g) { par(f); g(R[0]); }
   template <class F> void lanes(int n, F f) { for (int k = 0; k < n; ++k) f(k, R[k]); }
   void sync() {}
   void mark(int) {}
