@@ -72,10 +72,11 @@ AFS_HD constexpr bool is_static_section(int s) {
 // edge[s][0] = (a,b), edge[s][1] = (a,c), edge[s][2] = (b,c).  In round r, chain lane k
 // eliminates step[r][k].c, whose remaining neighbours are n0 (and n1) through edges e0
 // (e1); e01 is the edge n0-n1 that receives the update (a fill edge when n0 and n1 were not
-// adjacent).  Edge storage ids: 0..TREE_NE-1 = X_OFF slots, TREE_NE + x = a fill edge kept
-// in the solution slot of current x (free during the forward pass).  c = -1: idle.
-constexpr int TREE_CHAINS = 12;
-constexpr int TREE_MAX_ROUNDS = 20;
+// adjacent).  Edge storage ids: 0..TREE_NE-1 = X_OFF slots, TREE_NE + f = fill edge f
+// (X_FILL slot f, zeroed before the forward pass).  c = -1: idle.
+constexpr int TREE_CHAINS = 16;
+constexpr int TREE_MAX_ROUNDS = 14;
+constexpr int TREE_NFILL = 64;  // fill edges (tree_core.h X_FILL)
 constexpr int TREE_NE = 104;
 struct SolveStep {
   int16_t c, n0, n1, e0, e1, e01;

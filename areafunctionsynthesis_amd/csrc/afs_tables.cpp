@@ -146,13 +146,29 @@ void topology(Tables *t) {
 }
 
 // Edges of the current graph and the elimination schedule of the tree solver.
-// Chains (eliminated concurrently by 4 lanes, one step per round):
-//   lane 0: trachea + glottis + lower pharynx, from the lungs up:  0, 1, ..., 31
-//   lane 1: lips inward: 94, 93 (mouth radiation), 64, 63, ..., 34
-//   lane 2: nostrils inward: 96, 95, 83, 82, ..., 65 (the sinus leaves are gone by then)
-//   lane 3: paranasal sinuses 89..92, then the piriform fossa 88, ..., 84
-// then 32 and finally the root 33.  build_schedule() checks that every elimination is
-// fill-free and that no two lanes touch the same unknown in one round.
+// Sixteen lanes eliminate up to sixteen unknowns per round.  An unknown can go when it has
+// at most two remaining neighbours; the lanes of a round touch disjoint unknowns and edges;
+// eliminating c with non-adjacent neighbours n0, n1 creates the fill edge n0-n1 (its own
+// X_FILL slot).  Like a path (which loses at most a third of its nodes per round under these
+// rules), the graph needs 12 rounds; the plan below was found by a randomised greedy list
+// schedule (tools/sched_search.py) and assigns each step to the lane that eliminated its
+// neighbour the round before where it can, so that the pivot stays in registers.  The
+// builder re-derives every step symbolically and rejects a plan that breaks a rule.
+static const int8_t TREE_PLAN[12][TREE_CHAINS] = {
+    {0, 3, 6, 9, 12, 15, 93, 18, 61, 95, 21, 58, 81, 24, 55, 88},
+    {1, 92, 5, 10, 53, 14, 94, 19, 62, 96, 27, 57, 80, 23, 50, 87},
+    {2, 78, 90, 8, 52, 16, 64, 30, 72, 83, 48, 59, 33, 22, 45, 86},
+    {4, 91, 89, 70, 54, 13, 63, 31, 35, 82, 47, 67, 43, 25, 38, 85},
+    {7, -1, 74, 69, -1, -1, 60, -1, 34, 79, 49, -1, 42, 20, 39, 84},
+    {11, 76, -1, 71, -1, -1, 56, -1, -1, -1, -1, -1, 44, -1, 37, 29},
+    {17, 77, -1, 68, -1, -1, 51, -1, -1, -1, -1, -1, -1, -1, -1, 32},
+    {26, 75, -1, -1, -1, -1, 46, -1, -1, -1, -1, -1, -1, -1, -1, -1},
+    {28, 73, -1, -1, -1, -1, 41, -1, -1, -1, -1, -1, -1, -1, -1, -1},
+    {36, 66, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1},
+    {-1, 65, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1},
+    {-1, 40, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1},
+};
+
 bool tree_schedule(Tables *t) {
   int e = 0;
   for (int s = 0; s < NS; ++s) {
@@ -176,56 +192,28 @@ bool tree_schedule(Tables *t) {
       for (int b = 0; b < 3; ++b)
         if (a != b && m[a] >= 0 && m[b] >= 0) eid[m[a]][m[b]] = t->edge[s][pk[a][b]];
   }
-  // Lane programs: nested dissection of the tube graph (verified below).  Main path 0..64:
-  // an end chain from the lungs (0..9) and segments eliminated towards separators with fill
-  // into the separator behind them (11..19 -> 10, 21..27 -> 20, 39..30 -> 40, 42..52 -> 41);
-  // the lips end chain (after the radiation leaves 94, 93) 64..54; nose: 96, 95 then 83..77,
-  // and 66..76 with fill into 65, then 65 into the velum junction 40/41; fossa 88..84 into
-  // 28/29; sinus leaves; finally the separator path 10-20-28-29 and 53-41-40.
-  struct Prog { int start; std::vector<int> nodes; };
-  auto span = [](int a, int b) {
-    std::vector<int> v;
-    if (a <= b) for (int i = a; i <= b; ++i) v.push_back(i);
-    else for (int i = a; i >= b; --i) v.push_back(i);
-    return v;
-  };
-  auto cat = [](std::vector<int> a, const std::vector<int> &b) { a.insert(a.end(), b.begin(), b.end()); return a; };
-  std::vector<std::vector<Prog>> lanes(TREE_CHAINS);
-  lanes[0] = {{0, span(0, 9)}};
-  lanes[1] = {{0, span(11, 19)}};
-  lanes[2] = {{0, span(21, 27)}};
-  lanes[3] = {{0, span(88, 84)}};
-  lanes[4] = {{0, span(39, 30)}};
-  lanes[5] = {{0, span(42, 52)}};
-  lanes[6] = {{0, cat({94, 93}, span(64, 54))}, {13, {53, 41, 40}}};
-  lanes[7] = {{0, cat({96, 95}, span(83, 77))}};
-  lanes[8] = {{0, cat(span(66, 76), {65})}};
-  lanes[9] = {{0, {89, 90}}};
-  lanes[10] = {{0, {91, 92}}};
-  lanes[11] = {{10, {10, 20, 28, 29}}};
   int prog[TREE_MAX_ROUNDS][TREE_CHAINS];
   int order[NC];
   for (int i = 0; i < NC; ++i) order[i] = -1;
   for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
     for (int k = 0; k < TREE_CHAINS; ++k) prog[r][k] = -1;
-  int rounds = 0;
-  for (int k = 0; k < TREE_CHAINS; ++k)
-    for (const Prog &p : lanes[k])
-      for (size_t i = 0; i < p.nodes.size(); ++i) {
-        const int r = p.start + (int)i, c = p.nodes[i];
-        if (r >= TREE_MAX_ROUNDS - 2 || prog[r][k] != -1 || order[c] != -1) return false;
-        prog[r][k] = c;
-        order[c] = r;
-        rounds = std::max(rounds, r + 1);
-      }
+  const int rounds = (int)(sizeof(TREE_PLAN) / sizeof(TREE_PLAN[0]));
+  if (rounds > TREE_MAX_ROUNDS - 2) return false;
+  for (int r = 0; r < rounds; ++r)
+    for (int k = 0; k < TREE_CHAINS; ++k) {
+      const int c = TREE_PLAN[r][k];
+      if (c < 0) continue;
+      if (c >= NC || order[c] != -1) return false;
+      prog[r][k] = c;
+      order[c] = r;
+    }
   for (int i = 0; i < NC; ++i)
     if (order[i] < 0) return false;
   t->n_rounds = rounds;
   // Symbolic elimination in lock step: at most two remaining neighbours per step, lanes of a
-  // round touch disjoint unknowns and edges, fill edges go to the solution slot of their
-  // first-eliminated end (whose backward step reads them before writing its solution).
+  // round touch disjoint unknowns and edges, every fill edge gets its own X_FILL slot.
   bool gone[NC] = {false};
-  bool uslot[NC] = {false};
+  int nfill = 0;
   for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
     for (int k = 0; k < TREE_CHAINS; ++k) t->step[r][k] = SolveStep{-1, -1, -1, -1, -1, -1};
   for (int r = 0; r < rounds; ++r) {
@@ -258,10 +246,8 @@ bool tree_schedule(Tables *t) {
       SolveStep &st = t->step[r][k];
       if (st.c < 0) continue;
       if (st.n1 >= 0 && st.e01 < 0) {
-        const int x = order[st.n0] < order[st.n1] ? st.n0 : st.n1;
-        if (uslot[x]) return false;
-        uslot[x] = true;
-        const int id = TREE_NE + x;
+        if (nfill >= TREE_NFILL) return false;
+        const int id = TREE_NE + nfill++;
         eid[st.n0][st.n1] = eid[st.n1][st.n0] = (int16_t)id;
         st.e01 = (int16_t)id;
       }
@@ -409,7 +395,7 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   // step records: LDS byte offsets of the tree kernel's utterance block (tree_core.h)
   using namespace tree;
   auto off = [](int slot) { return (uint16_t)(slot * 8); };
-  auto eoff = [&](int id) { return id < TREE_NE ? off(X_OFF + id) : off(X_U + (id - TREE_NE)); };
+  auto eoff = [&](int id) { return id < TREE_NE ? off(X_OFF + id) : off(X_FILL + (id - TREE_NE)); };
   for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
     for (int k = 0; k < TREE_CHAINS; ++k) {
       const SolveStep &st = t->step[r][k];

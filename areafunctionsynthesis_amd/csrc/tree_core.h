@@ -72,7 +72,8 @@ enum : int {
   X_CUTN = X_TGT + NDIP, X_ACT = X_CUTN + NDIP, X_NOISE_END = X_ACT + NDIP,
   //   solver
   //   (pivot / rhs with a sink slot at NC; edges with EDGE_ZERO and EDGE_SINK after TREE_NE)
-  X_DIAG = X_UNION, X_RHS = X_DIAG + NC + 2, X_OFF = X_RHS + NC + 2, X_SOLVE_END = X_OFF + TREE_NE + 2,
+  X_DIAG = X_UNION, X_RHS = X_DIAG + NC + 2, X_OFF = X_RHS + NC + 2, X_FILL = X_OFF + TREE_NE + 2,
+  X_SOLVE_END = X_FILL + TREE_NFILL,
   X_AFTER = (X_NOISE_END > X_SOLVE_END ? X_NOISE_END : X_SOLVE_END),
   // frame-rate values written by lane 0 at every frame transition
   X_FRAME = X_AFTER,           // teethL, teethR, velL, velR, gL[6], gR[6]
@@ -1358,10 +1359,11 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.sync();
   x.mark(PH_ROWS);
   const int nr = U.n_rounds;
-  // X_U is free until the backward pass rewrites it: it holds the fill edges (zero at first)
+  // fill edges start at zero
   x.par([&](int gl, Lane<W> &R) {
     (void)R;
-    for (int i = gl; i < NC; i += W) X[X_U + i] = 0.0;
+#pragma unroll
+    for (int i = gl; i < TREE_NFILL; i += W) X[X_FILL + i] = 0.0;
   });
   x.sync();
   x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) {

@@ -56,7 +56,7 @@ def emu():
 
 def test_schedule_is_valid(emu):
     # build_tables verifies fill-freeness / round conflicts and reports -1 otherwise
-    assert emu.lib.emu_tree_rounds(22050.0) == 16  # nested-dissection plan (afs_tables.cpp tree_schedule)
+    assert emu.lib.emu_tree_rounds(22050.0) == 12  # 16-lane plan (afs_tables.cpp tree_schedule)
 
 
 def test_golden_utterances(emu, golden_dir):

@@ -229,3 +229,64 @@ CURRENT = [
     [(0, [96, 95] + span(83, 77))], [(0, span(66, 76) + [65])], [(0, [89, 90])], [(0, [91, 92])],
     [(10, [10, 20, 28, 29])],
 ]
+
+
+def assign_lanes(rounds, K):
+    """Lane programs for a round list [[(c, nb), ...], ...]: a step goes to the lane whose
+    previous step had c as a neighbour when possible (so the pivot can stay in registers).
+    Returns prog[r][k] (node or -1)."""
+    prog = []
+    prev = [None] * K  # neighbours of each lane's previous step
+    for st in rounds:
+        row = [-1] * K
+        free = set(range(K))
+        rest = []
+        for c, nb in st:
+            k = next((k for k in sorted(free) if prev[k] and c in prev[k]), None)
+            if k is None:
+                rest.append((c, nb))
+            else:
+                row[k] = c
+                free.discard(k)
+                prev[k] = nb
+        for c, nb in rest:
+            k = min(free)
+            row[k] = c
+            free.discard(k)
+            prev[k] = nb
+        for k in free:
+            prev[k] = None
+        prog.append(row)
+    return prog
+
+
+def search_best(K=16, trials=4000, seed=1, root=40):
+    adj0 = topology()
+    dist = [None] * NC
+    dist[root] = 0
+    q = deque([root])
+    while q:
+        u = q.popleft()
+        for v in adj0[u]:
+            if dist[v] is None:
+                dist[v] = dist[u] + 1
+                q.append(v)
+    rng = random.Random(seed)
+    best = None
+    for t in range(trials):
+        w = rng.random() * 0.5
+        prio = [dist[c] + w * rng.random() * 10 for c in range(NC)]
+        res = simulate(adj0, K, 1000, prio, rng)
+        if not res:
+            continue
+        rounds, _ = res
+        prog = assign_lanes(rounds, K)
+        lanes = [[(r, [prog[r][k]]) for r in range(len(prog)) if prog[r][k] >= 0] for k in range(K)]
+        try:
+            R, fwd, bwd = check_programs(lanes, nslot=1000, verbose=False)
+        except ValueError:
+            continue
+        key = (R, -(fwd + bwd))
+        if best is None or key < best[0]:
+            best = (key, prog, fwd, bwd)
+    return best
