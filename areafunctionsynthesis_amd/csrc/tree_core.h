@@ -51,6 +51,7 @@ namespace tree {
 
 constexpr int DYN0 = 23;     // first dynamic section
 constexpr int NDYNS = 46;    // sections 23..68
+constexpr int NDYP = 48;     // dynamic slots of 16 lanes (3 each); absent slots write the sinks
 constexpr int NSTATS = 47;   // sections 0..22, 69..92
 constexpr double THR = 0.001;  // MIN_DIPOLE_AMP (TdsModel.cpp:1611)
 
@@ -62,9 +63,11 @@ enum : int {
   // currents; X_U has two extra slots: U_SINK (idle / absent writes) and U_ZERO (0.0)
   X_U = 0, X_UR = X_U + NC + 2, X_UN = X_UR + NUR,
   X_P4 = X_UN + NUN,                                     // p[22], p[23], p[24], p[25]
-  X_E = X_P4 + 4, X_D = X_E + NDYNS,                     // E: dynamic sections (s-23), D: all
-  X_L = X_D + NS, X_R1 = X_L + NDYNS, X_R0 = X_R1 + NDYNS, X_AREA = X_R0 + NDYNS,  // dynamic, s-23
-  X_GLEN = X_AREA + NDYNS,                               // glottis section lengths (2)
+  // (the dynamic arrays have NDYP slots: the ones past NDYNS are sinks of absent lane slots;
+  // X_D has a sink at NS)
+  X_E = X_P4 + 4, X_D = X_E + NDYP,                      // E: dynamic sections (s-23), D: all
+  X_L = X_D + NS + 1, X_R1 = X_L + NDYP, X_R0 = X_R1 + NDYP, X_AREA = X_R0 + NDYP,  // dynamic, s-23
+  X_GLEN = X_AREA + NDYP,                                // glottis section lengths (2)
   X_SMP = X_GLEN + 2,                                    // dipole samples (41)
   X_UNION = X_SMP + NDIP,
   //   noise scratch (n)
@@ -591,97 +594,121 @@ AFS_HD inline double static_beta(const Lane<W> &R, int j, const Uni &U, const Co
 
 template <int W>
 AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
+  // One branch-free block over the lane's slots (absent slots compute on a valid section and
+  // store into the sinks), so that the scheduler interleaves the slots' reciprocal and square
+  // root chains; the glottal entrance (one section) and the transvelar source follow.
   using S = Shape<W>;
   const afs_options &opt = U.opt;
   const double dt = C.h.dt, idt = C.h.inv_dtTH, idt2 = C.h.inv_dt2TH2;
 #pragma unroll
   for (int j = 0; j < S::NST; ++j) {
     const int jj = S::ND + j;
-    const int s = static_section(W, j, gl);
-    if (s < 0) continue;
+    const int s0 = static_section(W, j, gl);
+    const int s = s0 < 0 ? 0 : s0;
     const double E = C.stat[static_index(s)][ST_E];
     const double beta = static_beta<W>(R, jj, U, C, s);
-    X[X_D + s] = R.p[jj] + C.h.dtTH1 * R.pr[jj] - E * (beta - 0.0);  // (E: a table constant)
+    X[X_D + (s0 < 0 ? NS : s)] = R.p[jj] + C.h.dtTH1 * R.pr[jj] - E * (beta - 0.0);  // (E: a table constant)
   }
+  double R0g = 0.0, R1g = 0.0, Eg[S::ND], betag[S::ND];
 #pragma unroll
   for (int j = 0; j < S::ND; ++j) {
-    const int s = dyn_section(W, j, gl);
-    if (s < 0) continue;
+    const int k = j * W + gl;
+    const bool present = k < NDYNS;
+    if constexpr (S::ND * W > NDYP) {  // wider utterances (CPU emulator only): no sinks for all
+      if (!present) continue;
+    }
+    const int s = present ? DYN0 + k : S_PHARYNX0;  // an absent slot computes on section 25
+    const int ks = present ? k : NDYNS;             // and stores into the sinks
     const bool glot = (s == S_GLOT_LO || s == S_GLOT_UP);
+    const bool pm = s >= S_PHARYNX0 && s <= S_LAST_MOUTH;
     const double area = X[X_AREA + s - DYN0];
-    const double len = glot ? X[X_GLEN + s - DYN0] : (s <= S_LAST_MOUTH ? X[X_LEN + s - S_PHARYNX0] : C.h.len_nose0);
+    const double lx = X[glot ? X_GLEN + s - DYN0 : (pm ? X_LEN + s - S_PHARYNX0 : X_GLEN)];
+    const double len = (glot || pm) ? lx : C.h.len_nose0;
     // prepareTimeStep's section quantities (TdsModel.cpp:732-834), with the repeated
     // divisions folded into one reciprocal of the area and one of the wall surface.
     const double vol = area * len;
     const double inv_area = fast_rcp(area);
-    double alpha = 0.0, beta = 0.0;
     const double r0 = fast_sqrt(area * (1.0 / PI));
     const double circ = 2.0 * PI * r0;
-    double a = r0, b = r0;
     const double rmin = glot ? 0.8 : 1.6;
-    if (a < rmin) { a = rmin; b = area * (glot ? 1.0 / (PI * 0.8) : 1.0 / (PI * 1.6)); }
+    const bool ell = r0 < rmin;
+    const double a = ell ? rmin : r0;
+    const double b = ell ? area * (glot ? 1.0 / (PI * 0.8) : 1.0 / (PI * 1.6)) : r0;
     const double L = (RHO * 0.5 * len) * inv_area;
     const double Cc = vol * (1.0 / (RHO * CSND * CSND));
     const double Rr = fast_div((2.0 * MU * len) * (a * a + b * b), PI * a * a * a * b * b * b);
-    if (opt.soft_walls && !glot) {
-      double surf = circ * len;
-      if (surf < AMIN) surf = AMIN;
-      const double inv_surf = fast_rcp(surf);
-      double Rw = C.h.Bw_ph0 * inv_surf, Lw = C.h.Mw_ph0 * inv_surf;
-      alpha = fast_rcp(Lw * idt2 + Rw * idt + C.h.Kw_ph0 * inv_surf);
-      beta = alpha * (R.w[j] * (Lw * idt2 + Rw * idt) +
-                      R.wr[j] * (Lw * (TH1 / TH + 1.0) * idt + Rw * (TH1 / TH)) +
-                      R.wr2[j] * Lw * (TH1 / TH));
-    }
+    // soft walls (not for the glottis); evaluated for every slot, selected
+    double surf = circ * len;
+    if (surf < AMIN) surf = AMIN;
+    const double inv_surf = fast_rcp(surf);
+    const double Rw = C.h.Bw_ph0 * inv_surf, Lw = C.h.Mw_ph0 * inv_surf;
+    const double alw = fast_rcp(Lw * idt2 + Rw * idt + C.h.Kw_ph0 * inv_surf);
+    const double bew = alw * (R.w[j] * (Lw * idt2 + Rw * idt) +
+                              R.wr[j] * (Lw * (TH1 / TH + 1.0) * idt + Rw * (TH1 / TH)) +
+                              R.wr2[j] * Lw * (TH1 / TH));
+    const bool walls = opt.soft_walls && !glot;
+    const double alpha = walls ? alw : 0.0, beta = walls ? bew : 0.0;
     const double E = fast_div(dt * TH, Cc + alpha);
     double R0 = Rr, R1 = Rr;
     // Bernoulli losses between pharynx/mouth sections (TdsModel.cpp:850-877)
-    if (opt.turbulence_losses && s >= S_PHARYNX0 && s <= S_LAST_MOUTH) {
-      if (s < S_LAST_MOUTH && s != S_PHARYNX0 + 3 && s != S_LAST_PHARYNX) {  // pair (s, s+1)
-        double u = 0.0;
-        u += X[X_U + s + 1];
-        double Ai = X[X_AREA + s + 1 - DYN0];
-        if ((Ai < area && u > 0) || (Ai > area && u < 0)) R1 = R1 - u * (0.5 * RHO) * (inv_area * inv_area);
-      }
-      if (s > S_PHARYNX0 && s - 1 != S_PHARYNX0 + 3 && s - 1 != S_LAST_PHARYNX) {  // pair (s-1, s)
-        double u = 0.0;
-        u += R.u[j];
-        double Aa = X[X_AREA + s - 1 - DYN0];
-        if ((area < Aa && u > 0) || (area > Aa && u < 0)) R0 = R0 + u * (0.5 * RHO) * (inv_area * inv_area);
-      }
+    const bool turb = opt.turbulence_losses && pm;
+    const double ia2 = inv_area * inv_area;
+    {  // pair (s, s+1)
+      double u = 0.0;
+      u += X[X_U + s + 1];
+      const double Ai = X[X_AREA + s + 1 - DYN0];
+      const bool on = turb && s < S_LAST_MOUTH && s != S_PHARYNX0 + 3 && s != S_LAST_PHARYNX;
+      if (on && ((Ai < area && u > 0) || (Ai > area && u < 0))) R1 = R1 - u * (0.5 * RHO) * ia2;
     }
-    if (s == S_GLOT_LO) {  // glottal entrance and transition (TdsModel.cpp:898-950)
-      double kent = 1.0;
-      if (opt.glottis_loss == AFS_ENTRANCE_LOSS_VAN_DEN_BERG) {
-        kent = 1.375;
-      } else if (opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE) {  // :1019-1039
-        const double tp = X[X_P4 + 0] - X[X_P4 + 3];
-        kent = fulcher_kent(iir_run<4>(X + X_TGLOT, C.h.tglot_a, C.h.tglot_b, tp), area / 1.25);
-      }
-      double sa = C.h.area_last_trachea, ta = area;
+    {  // pair (s-1, s)
       double u = 0.0;
       u += R.u[j];
-      if (u > 0) R0 = R0 + kent * 0.5 * RHO * fabs(u) * (fast_rcp(ta * ta) - fast_rcp(sa * sa));
-      sa = ta;
-      ta = X[X_AREA + 1];
-      double bt = (ta < opt.flow_separation_area_ratio * sa) ? 1.0 : 0.0;
-      double g = 0.8 * X[X_GBF] + (1.0 - 0.8) * bt;
-      X[X_GBF] = g;
-      u = 0.0;
-      u += X[X_U + S_GLOT_UP];
-      if (u > 0) R1 = R1 + g * fabs(u) * 0.5 * RHO * (fast_rcp(ta * ta) - fast_rcp(sa * sa));
+      const double Aa = X[X_AREA + s - 1 - DYN0];
+      const bool on = turb && s > S_PHARYNX0 && s - 1 != S_PHARYNX0 + 3 && s - 1 != S_LAST_PHARYNX;
+      if (on && ((area < Aa && u > 0) || (area > Aa && u < 0))) R0 = R0 + u * (0.5 * RHO) * ia2;
     }
+    if (j == 0) { R0g = R0; R1g = R1; }
+    Eg[j] = E;
+    betag[j] = beta;
     R.al[j] = alpha;
     R.be[j] = beta;
-    X[X_E + s - DYN0] = E;
+    X[X_E + ks] = E;
+    X[X_D + (present ? s : NS)] = R.p[j] + C.h.dtTH1 * R.pr[j] - E * (beta - 0.0);
+    X[X_L + ks] = L;
+    X[X_R0 + ks] = R0;
+    X[X_R1 + ks] = R1;
+  }
+  if (gl == S_GLOT_LO - DYN0) {  // glottal entrance and transition (TdsModel.cpp:898-950), slot 0
+    const double area = X[X_AREA + 0];
+    double R0 = R0g, R1 = R1g;
+    double kent = 1.0;
+    if (opt.glottis_loss == AFS_ENTRANCE_LOSS_VAN_DEN_BERG) {
+      kent = 1.375;
+    } else if (opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE) {  // :1019-1039
+      const double tp = X[X_P4 + 0] - X[X_P4 + 3];
+      kent = fulcher_kent(iir_run<4>(X + X_TGLOT, C.h.tglot_a, C.h.tglot_b, tp), area / 1.25);
+    }
+    double sa = C.h.area_last_trachea, ta = area;
+    double u = 0.0;
+    u += R.u[0];
+    if (u > 0) R0 = R0 + kent * 0.5 * RHO * fabs(u) * (fast_rcp(ta * ta) - fast_rcp(sa * sa));
+    sa = ta;
+    ta = X[X_AREA + 1];
+    double bt = (ta < opt.flow_separation_area_ratio * sa) ? 1.0 : 0.0;
+    double g = 0.8 * X[X_GBF] + (1.0 - 0.8) * bt;
+    X[X_GBF] = g;
+    u = 0.0;
+    u += X[X_U + S_GLOT_UP];
+    if (u > 0) R1 = R1 + g * fabs(u) * 0.5 * RHO * (fast_rcp(ta * ta) - fast_rcp(sa * sa));
+    X[X_R0 + 0] = R0;
+    X[X_R1 + 0] = R1;
+  }
+  constexpr int KTV = S_NOSE0 + 2 - DYN0, JTV = KTV / W, GTV = KTV % W;
+  if (opt.transvelar_coupling && gl == GTV) {  // flow through the velum (:966-980, 996)
     double src = 0.0;
-    if (opt.transvelar_coupling && s == S_NOSE0 + 2)  // flow through the velum (:966-980, 996)
-      src += iir_run<4>(X + X_TVEL, C.h.tone_a, C.h.tone_b, X[X_TVP]) +
-             iir_run<4>(X + X_TVEL + 8, C.h.tvel2_a, C.h.tone_b, X[X_TVP + 1]);
-    X[X_D + s] = R.p[j] + C.h.dtTH1 * R.pr[j] - E * (beta - src);
-    X[X_L + s - DYN0] = L;
-    X[X_R0 + s - DYN0] = R0;
-    X[X_R1 + s - DYN0] = R1;
+    src += iir_run<4>(X + X_TVEL, C.h.tone_a, C.h.tone_b, X[X_TVP]) +
+           iir_run<4>(X + X_TVEL + 8, C.h.tvel2_a, C.h.tone_b, X[X_TVP + 1]);
+    X[X_D + S_NOSE0 + 2] = R.p[JTV] + C.h.dtTH1 * R.pr[JTV] - Eg[JTV] * (betag[JTV] - src);
   }
   // reset the dipole targets this lane owns (calcNoiseSources, TdsModel.cpp:1203-1208)
 #pragma unroll
