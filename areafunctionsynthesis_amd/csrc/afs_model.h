@@ -122,8 +122,11 @@ struct alignas(16) SecRec {
   int16_t x_la, x_ra, x_ea, x_da, x_ub, x_urb, x_sx, x_e0, x_e1, x_e2;
   int16_t x_o0, x_o1, x_ur, x_un, x_p4;
   uint16_t flags;
+  // 80-byte stride: the 16 sections a 16-lane ds_read_b128 group reads start on 16 distinct
+  // 16-byte bank slots (at 64 bytes, sections s and s+4 share banks: 4-way conflicts)
+  int16_t pad_[8];
 };
-static_assert(sizeof(SecRec) == 64, "SecRec: four 16-byte loads");
+static_assert(sizeof(SecRec) == 80, "SecRec: 80-byte stride");
 // Scalars of the time loop (copies of Tables fields; see build_tables).
 struct Hot {
   double fs, dt, dtTH1, noise_amp_F, noise_lp_c, noise_x_2000, sqrt12, nose4_area, fossa_R0;
