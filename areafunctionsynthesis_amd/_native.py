@@ -9,7 +9,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libafs.so")
+# (AFS_LIB: another in-tree build of the same library, for A/B timing of kernel variants)
+LIB_PATH = os.environ.get("AFS_LIB") or os.path.join(HERE, "libafs.so")
 
 AFS_OK = 0
 STATUS = {0: "ok", 1: "invalid argument", 2: "no HIP device", 3: "HIP runtime error",

@@ -122,9 +122,11 @@ struct alignas(16) SecRec {
   int16_t x_la, x_ra, x_ea, x_da, x_ub, x_urb, x_sx, x_e0, x_e1, x_e2;
   int16_t x_o0, x_o1, x_ur, x_un, x_p4;
   uint16_t flags;
+  // constriction phase: the noise-smoothed flows of the section's outputs (X_UN, or zero)
+  int16_t x_uo0, x_uo1;
   // 80-byte stride: the 16 sections a 16-lane ds_read_b128 group reads start on 16 distinct
   // 16-byte bank slots (at 64 bytes, sections s and s+4 share banks: 4-way conflicts)
-  int16_t pad_[8];
+  int16_t pad_[6];
 };
 static_assert(sizeof(SecRec) == 80, "SecRec: 80-byte stride");
 // Scalars of the time loop (copies of Tables fields; see build_tables).

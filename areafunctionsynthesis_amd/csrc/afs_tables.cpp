@@ -484,6 +484,8 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
     q.x_ur = real && c.ur_slot[s] >= 0 ? (int16_t)(X_UR + c.ur_slot[s]) : sink;
     q.x_un = real && c.un_slot[s] >= 0 ? (int16_t)(X_UN + c.un_slot[s]) : sink;
     q.x_p4 = (s >= S_LAST_TRACHEA && s <= S_PHARYNX0) ? (int16_t)(X_P4 + s - S_LAST_TRACHEA) : sink;
+    q.x_uo0 = o0 >= 0 && c.un_slot[o0] >= 0 ? (int16_t)(X_UN + c.un_slot[o0]) : zero;
+    q.x_uo1 = o1 >= 0 && c.un_slot[o1] >= 0 ? (int16_t)(X_UN + c.un_slot[o1]) : zero;
     q.flags = (uint16_t)((br >= 0 ? SR_BIF : 0) |
                          (real && a >= S_PHARYNX0 && s <= S_LAST_MOUTH ? SR_JUNCTION : 0) |
                          (s == S_LAST_MOUTH || s == S_LAST_NOSE ? SR_RADIATION : 0));

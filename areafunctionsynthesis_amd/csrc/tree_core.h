@@ -592,6 +592,20 @@ AFS_HD inline double static_beta(const Lane<W> &R, int j, const Uni &U, const Co
                           : 0.0;
 }
 
+// Section positions (Tube::calcPositions, Tube.cpp:611-622): one sequential sum, as in the
+// reference (the comparisons against obstacle positions depend on its rounding).  Every lane
+// of the utterance evaluates it (same values, same stores) inside the network phase, where
+// the scheduler interleaves the chain of dependent adds with the per-section arithmetic.
+AFS_HD inline void phase_positions(double *X) {
+  double p = 0.0;
+#pragma unroll
+  for (int m = 0; m < NPM; ++m) {
+    const double l = X[X_LEN + m];
+    X[X_POS + m] = p;
+    p += l;
+  }
+}
+
 template <int W>
 AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
   // One branch-free block over the lane's slots (absent slots compute on a valid section and
@@ -600,6 +614,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
   using S = Shape<W>;
   const afs_options &opt = U.opt;
   const double dt = C.h.dt, idt = C.h.inv_dtTH, idt2 = C.h.inv_dt2TH2;
+  phase_positions(X);  // (for the constriction phase; lane-uniform)
 #pragma unroll
   for (int j = 0; j < S::NST; ++j) {
     const int jj = S::ND + j;
@@ -787,10 +802,9 @@ AFS_HD inline DipTarget dipole_target(const double *X, const Consts &C, double t
   if (A < 0.1) A = 0.1;
   const double inv_A = fast_rcp(A);
   double flow = 0.0;
-  const Topo tn = C.topo[c.narrow];
-  const int o0 = tn.out0, o1 = tn.out1;
-  if (o0 != -1) flow += X[X_UN + C.un_slot[o0]];
-  if (o1 != -1) flow += X[X_UN + C.un_slot[o1]];
+  const SecRec &q = C.sec[c.narrow];  // (an absent output reads the zero slot)
+  flow += X[q.x_uo0];
+  flow += X[q.x_uo1];
   if (flow < 0.0) flow = 0.0;
   double v = flow * inv_A;
   double fc = 6000.0, gain = 0.0;
@@ -812,37 +826,23 @@ AFS_HD inline DipTarget dipole_target(const double *X, const Consts &C, double t
   return t;
 }
 
+// Every lane of the utterance stores the same values (no exec-mask branch); a target that is
+// not stored (on == false) goes to the sink slots X_ACT, X_ACT + 1.
 template <int W, class Xc>
-AFS_HD inline void store_target(Xc &x, double *X, const DipTarget &t) {
-  x.one([&](Lane<W> &R) {
-    (void)R;
-    X[X_TGT + t.up] = t.tup; X[X_CUTN + t.up] = t.fc;
-    X[X_TGT + t.dn] = t.tdn; X[X_CUTN + t.dn] = t.fc;
+AFS_HD inline void store_target(Xc &x, double *X, const DipTarget &t, bool on) {
+  x.par([&](int gl, Lane<W> &R) {
+    (void)gl; (void)R;
+    const int tu = on ? X_TGT + t.up : X_ACT, cu = on ? X_CUTN + t.up : X_ACT + 1;
+    const int td = on ? X_TGT + t.dn : X_ACT, cd = on ? X_CUTN + t.dn : X_ACT + 1;
+    X[tu] = t.tup; X[cu] = t.fc;
+    X[td] = t.tdn; X[cd] = t.fc;
   });
 }
 
 template <int W, class Xc>
 AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  // Section positions (Tube::calcPositions, Tube.cpp:611-622): one sequential sum, as in
-  // the reference (the comparisons against obstacle positions depend on its rounding).
-  x.one([&](Lane<W> &R) {
-    (void)R;
-    double p = 0.0;
-#pragma unroll
-    for (int m0 = 0; m0 < NPM; m0 += 8) {  // 8 loads in flight, then the sequential adds
-      double l[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) l[i] = X[X_LEN + m0 + i];
-      AFS_SCHED_BARRIER();
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        X[X_POS + m0 + i] = p;
-        p += l[i];
-      }
-    }
-  });
-  x.sync();
+  // (the section positions come from the network phase: phase_positions)
   x.mark(PH_C_POS);
   const double teeth = X[X_GP + 6];
   // Extend a constriction over the neighbours with area < amin + 0.2 and the same
@@ -917,19 +917,21 @@ AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Con
   x.mark(PH_C_T2);
   const bool has_l = lp.v < 1.0 && lp.v < min_teeth;
   x.mark(PH_C_LIP);
+  // The four targets as independent chains, all evaluated (absent constrictions hold dummies
+  // with valid indices), stored in the reference's order; a target that is not stored writes
+  // the sink slots (X_ACT), so the phase has no branch.
   const uint64_t Mg = obstacle_mask<W>(x, X, cg.obst);
   const uint64_t M1 = obstacle_mask<W>(x, X, ct1.obst);
+  const uint64_t M2 = obstacle_mask<W>(x, X, ct2.obst);
   const uint64_t Ml = obstacle_mask<W>(x, X, cl.obst);
   const DipTarget tg = dipole_target<VOCAL_FOLDS>(X, C, teeth, cg, Mg);
   const DipTarget tt1 = dipole_target<TONGUE>(X, C, teeth, ct1, M1);
+  const DipTarget tt2 = dipole_target<TONGUE>(X, C, teeth, ct2, M2);
   const DipTarget tl = dipole_target<LOWER_LIP>(X, C, teeth, cl, Ml);
-  if (Mg) store_target<W>(x, X, tg);
-  if (has_t1 && M1) store_target<W>(x, X, tt1);
-  if (has_t2) {
-    const uint64_t M2 = obstacle_mask<W>(x, X, ct2.obst);
-    if (M2) store_target<W>(x, X, dipole_target<TONGUE>(X, C, teeth, ct2, M2));
-  }
-  if (has_l && Ml) store_target<W>(x, X, tl);
+  store_target<W>(x, X, tg, Mg != 0);
+  store_target<W>(x, X, tt1, has_t1 && M1 != 0);
+  store_target<W>(x, X, tt2, has_t2 && M2 != 0);
+  store_target<W>(x, X, tl, has_l && Ml != 0);
 }
 
 // Phase N: noise sources (TdsModel.cpp:1630-1708).  Amplitude smoothing of the owned
