@@ -28,6 +28,12 @@ __global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_prof_kernel
 extern "C" int pp_phase_count() { return PH_COUNT; }
 
 // frames[B][F] host; cycles[PH_COUNT] = sum over waves; returns kernel ms in *ms.
+static std::vector<uint64_t> g_wave;  // per-wave cycle totals of the last pp_run
+extern "C" int pp_waves_per_block() { return WPB; }
+extern "C" void pp_wave_totals(uint64_t *out) {
+  for (size_t w = 0; w < g_wave.size(); ++w) out[w] = g_wave[w];
+}
+
 extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int F, int hop, double fs,
                       uint64_t *cycles, double *ms) {
   Tables *ht = new Tables();
@@ -66,8 +72,12 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   std::vector<uint64_t> h((size_t)waves * PH_COUNT);
   CK(hipMemcpy(h.data(), dprof, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
   for (int p = 0; p < PH_COUNT; ++p) cycles[p] = 0;
+  g_wave.assign(waves, 0);
   for (int w = 0; w < waves; ++w)
-    for (int p = 0; p < PH_COUNT; ++p) cycles[p] += h[(size_t)w * PH_COUNT + p];
+    for (int p = 0; p < PH_COUNT; ++p) {
+      cycles[p] += h[(size_t)w * PH_COUNT + p];
+      g_wave[w] += h[(size_t)w * PH_COUNT + p];
+    }
   (void)hipFree(dt); (void)hipFree(df); (void)hipFree(ds); (void)hipFree(dout);
   (void)hipFree(dlds); (void)hipFree(dlanes); (void)hipFree(dprof);
   delete ht;

@@ -43,6 +43,15 @@ def main():
     for p in range(n):
         print(f"  {PHASES[p]:14s} {cyc[p] / waves / T:10.1f} clk/sample  {100 * cyc[p] / tot:5.1f} %")
     print(f"  {'total':14s} {tot / waves / T:10.1f} clk/sample")
+    if not hasattr(lib, "pp_wave_totals"):
+        return
+    wt = (ctypes.c_uint64 * waves)()
+    lib.pp_wave_totals(wt)
+    wt = np.array(wt, dtype=np.float64) / T
+    wpb = lib.pp_waves_per_block()
+    bmax = wt.reshape(-1, wpb).max(axis=1)
+    print(f"  per wave: mean {wt.mean():.0f}  p10 {np.percentile(wt, 10):.0f}  p90 {np.percentile(wt, 90):.0f}  "
+          f"max {wt.max():.0f};  mean of block maxima ({wpb} waves) {bmax.mean():.0f} clk/sample")
 
 
 if __name__ == "__main__":
