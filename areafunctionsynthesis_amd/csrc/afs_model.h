@@ -124,9 +124,11 @@ struct alignas(16) SecRec {
   uint16_t flags;
   // constriction phase: the noise-smoothed flows of the section's outputs (X_UN, or zero)
   int16_t x_uo0, x_uo1;
-  // 80-byte stride: the 16 sections a 16-lane ds_read_b128 group reads start on 16 distinct
-  // 16-byte bank slots (at 64 bytes, sections s and s+4 share banks: 4-way conflicts)
-  int16_t pad_[6];
+  // radiation sections (SR_RADIATION): flow, d/dt and noise-smoothed flow of the two
+  // radiation currents (X_U + rc, X_U + lc, X_UR.., X_UR.., X_UN.., X_UN..)
+  int16_t x_rad[6];
+  // (80-byte stride: the 16 sections a 16-lane ds_read_b128 group reads start on 16 distinct
+  // 16-byte bank slots; at 64 bytes, sections s and s+4 share banks: 4-way conflicts)
 };
 static_assert(sizeof(SecRec) == 80, "SecRec: 80-byte stride");
 // Scalars of the time loop (copies of Tables fields; see build_tables).

@@ -486,6 +486,15 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
     q.x_p4 = (s >= S_LAST_TRACHEA && s <= S_PHARYNX0) ? (int16_t)(X_P4 + s - S_LAST_TRACHEA) : sink;
     q.x_uo0 = o0 >= 0 && c.un_slot[o0] >= 0 ? (int16_t)(X_UN + c.un_slot[o0]) : zero;
     q.x_uo1 = o1 >= 0 && c.un_slot[o1] >= 0 ? (int16_t)(X_UN + c.un_slot[o1]) : zero;
+    for (int k = 0; k < 6; ++k) q.x_rad[k] = zero;
+    if (real && (s == S_LAST_MOUTH || s == S_LAST_NOSE) && o0 >= 0 && o1 >= 0) {
+      q.x_rad[0] = (int16_t)(X_U + o0);
+      q.x_rad[1] = (int16_t)(X_U + o1);
+      q.x_rad[2] = c.ur_slot[o0] >= 0 ? (int16_t)(X_UR + c.ur_slot[o0]) : zero;
+      q.x_rad[3] = c.ur_slot[o1] >= 0 ? (int16_t)(X_UR + c.ur_slot[o1]) : zero;
+      q.x_rad[4] = c.un_slot[o0] >= 0 ? (int16_t)(X_UN + c.un_slot[o0]) : zero;
+      q.x_rad[5] = c.un_slot[o1] >= 0 ? (int16_t)(X_UN + c.un_slot[o1]) : zero;
+    }
     q.flags = (uint16_t)((br >= 0 ? SR_BIF : 0) |
                          (real && a >= S_PHARYNX0 && s <= S_LAST_MOUTH ? SR_JUNCTION : 0) |
                          (s == S_LAST_MOUTH || s == S_LAST_NOSE ? SR_RADIATION : 0));

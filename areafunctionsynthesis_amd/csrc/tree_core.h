@@ -588,8 +588,9 @@ AFS_HD inline int static_index(int s) { return s < 23 ? s : s - 46; }
 template <int W>
 AFS_HD inline double static_beta(const Lane<W> &R, int j, const Uni &U, const Consts &C, int s) {
   const double *k = C.stat[static_index(s)];
-  return U.opt.soft_walls ? k[ST_ALPHA] * (R.w[j] * k[ST_WC1] + R.wr[j] * k[ST_WC2] + R.wr2[j] * k[ST_LW] * (TH1 / TH))
-                          : 0.0;
+  // (evaluated either way and selected: a branch here would split the slot block)
+  const double v = k[ST_ALPHA] * (R.w[j] * k[ST_WC1] + R.wr[j] * k[ST_WC2] + R.wr2[j] * k[ST_LW] * (TH1 / TH));
+  return U.opt.soft_walls ? v : 0.0;
 }
 
 // Section positions (Tube::calcPositions, Tube.cpp:611-622): one sequential sum, as in the
@@ -1160,11 +1161,11 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
     const double AB = dyn ? X[X_AREA + s - DYN0] : C.h.area_last_nose;
     const double EB = dyn ? X[X_E + s - DYN0] : ks[ST_E], DB = X[X_D + s];
-    const Topo tp = C.topo[s];
-    const int rc = tp.out0, lc = tp.out1;
-    double uR = X[X_U + rc], uL = X[X_U + lc], uRr = X[X_UR + C.ur_slot[rc]], uLr = X[X_UR + C.ur_slot[lc]];
+    const SecRec &q = rec[j];  // rc = q.x_rad[0] - X_U, lc = q.x_rad[1] - X_U
+    const int rc = q.x_rad[0] - X_U, lc = q.x_rad[1] - X_U;
+    double uR = X[q.x_rad[0]], uL = X[q.x_rad[1]], uRr = X[q.x_rad[2]], uLr = X[q.x_rad[3]];
     R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
-    R.rad_un[0] = X[X_UN + C.un_slot[rc]]; R.rad_un[1] = X[X_UN + C.un_slot[lc]];
+    R.rad_un[0] = X[q.x_rad[4]]; R.rad_un[1] = X[q.x_rad[5]];
     const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
     {
       double Rrad = fast_div(C.h.rrad_num, 9.0 * PI * PI * AB);
@@ -1312,14 +1313,12 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
       if (s == S_NOSE0 + 2) Xw[X_TVP + 1] = R.p[j];
     }
     if (rec[j].flags & SR_RADIATION) {  // the two radiation currents of s = 64 / 83
-      const Topo tu = C.topo[s];
-      const int o0 = tu.out0, o1 = tu.out1;
+      const SecRec &q = rec[j];
       for (int k = 0; k < 2; ++k) {
-        const int rc = k == 0 ? o0 : o1;
-        double un = X[X_U + rc];
+        double un = X[q.x_rad[k]];
         double ur = (un - R.rad_u[k]) * idt - (TH1 / TH) * R.rad_ur[k];
-        Xw[X_UR + C.ur_slot[rc]] = ur;
-        Xw[X_UN + C.un_slot[rc]] = (1.0 - c) * un + c * R.rad_un[k];
+        Xw[q.x_rad[2 + k]] = ur;
+        Xw[q.x_rad[4 + k]] = (1.0 - c) * un + c * R.rad_un[k];
       }
     }
   }
@@ -1347,7 +1346,9 @@ AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, doub
   flow += X[X_U + 94];
   flow += X[X_U + 95];
   flow += X[X_U + 96];
-  if (U.opt.radiation_from_skin) flow += iir_run<4>(X + X_TONE, C.h.tone_a, C.h.tone_b, p25);
+  // (the tone filter runs either way, its output is selected: no branch in the output stage)
+  const double tone = iir_run<4>(X + X_TONE, C.h.tone_a, C.h.tone_b, p25);
+  flow += U.opt.radiation_from_skin ? tone : 0.0;
   double op = (flow - X[X_PREVFLOW]) * C.h.inv_dt;
   X[X_PREVFLOW] = flow;
   double y = iir_run<8>(X + X_OUTF, C.h.out_a, C.h.out_b, op);
