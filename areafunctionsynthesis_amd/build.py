@@ -20,6 +20,9 @@ HEADERS = ["afs_model.h", "afs_af.h", "afs_lane.h", "afs_tree.h", "afs_audio.h",
 # Per-source extra flags.  (Contracting a*b+c in the tree kernel was measured: ~1 % faster,
 # and it moves some chaotic utterances past the 1e-9 parity bound -- not used.)
 PER_SOURCE: dict = {}
+# (AFS_TREE_FLAGS: extra compiler flags for the tree kernel, for A/B builds of scheduler options)
+if os.environ.get("AFS_TREE_FLAGS"):
+    PER_SOURCE["tds_tree.hip"] = os.environ["AFS_TREE_FLAGS"].split()
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
           # keep the reference's rounding: no contraction of a*b+c into fma

@@ -8,8 +8,10 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for rep in 1 2; do
   for t in ${AB:-A B}; do
-    PP_LIB=libphase_prof_$t.so timeout -k 10 240 python tools/phase_prof/run.py --batch 8192 --seconds ${PP_SECONDS:-0.05} > gpurun_out/ab_pp_${t}_$rep.txt 2>&1 || { echo "STOP pp $t"; exit 3; }
-    head -1 gpurun_out/ab_pp_${t}_$rep.txt; tail -1 gpurun_out/ab_pp_${t}_$rep.txt
+    if [ "${AB_PP:-1}" = 1 ]; then
+      PP_LIB=libphase_prof_$t.so timeout -k 10 240 python tools/phase_prof/run.py --batch 8192 --seconds ${PP_SECONDS:-0.05} > gpurun_out/ab_pp_${t}_$rep.txt 2>&1 || { echo "STOP pp $t"; exit 3; }
+      head -1 gpurun_out/ab_pp_${t}_$rep.txt; tail -1 gpurun_out/ab_pp_${t}_$rep.txt
+    fi
     AFS_LIB=$PWD/areafunctionsynthesis_amd/libafs_$t.so timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 --seconds ${AB_SECONDS:-0.25} > gpurun_out/ab_bench_${t}_$rep.txt 2>&1 || { echo "STOP bench $t"; exit 3; }
     python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split('\n')[-1]); print('$t bench', round(d['value']/1e6,2), 'M samples/s', round(d['ms_per_step'],1), 'ms')" gpurun_out/ab_bench_${t}_$rep.txt
   done
