@@ -204,6 +204,9 @@ struct Lane {
   uint32_t racc[S::NDP];                                             // rand() sums of owned dipoles
   uint32_t rtmp[3];                                                  // rand() block scratch
   SolveCarry sc;                                                     // chain lanes, during the solve
+  // per-sample values of the geometry/network block (not state: cleared before a save)
+  double acur[S::ND], lcur[S::ND];                                   // area, length of the slots
+  double anx[S::ND], apv[S::ND];                                     // areas of sections s+1, s-1
 };
 
 // Cross-lane collectives every execution policy provides (results are uniform over the W
@@ -212,6 +215,8 @@ struct Lane {
 //   x.min_index(f)  -> the smallest MinIdx::v of f(gl, R), ties to the smallest index
 //   x.max_value(f)  -> the largest f(gl, R) under strict ">" (a NaN never wins)
 struct MinIdx { double v; int i; };
+// x.dyn_neighbors(): R.anx[j] / R.apv[j] = R.acur of the owners of dynamic sections s+1 / s-1
+// (s = the section of slot j; lanes' values as the interpolation left them).
 // x.scan_add<N>(f, g): f(gl, R) -> U4; inclusive prefix sums (mod 2^32) of the first N
 // components over lanes 0..gl are handed to g(gl, R, sums).
 struct U4 { uint32_t v[4]; };
@@ -235,39 +240,37 @@ AFS_HD inline double glottis_q(double f0) {
   return q < 0.05 ? 0.05 : q;
 }
 
-// getOpenCloseDimensions (TriangularGlottis.cpp:474-576)
+// getOpenCloseDimensions (TriangularGlottis.cpp:474-576), as selects (the three cases and the
+// apex test are evaluated and chosen; no branch splits the geometry block)
 AFS_HD inline void glottis_open_close(const double *gp, double cord, double rel0, double rel1,
                                       double *olen, double *clen, double *ow, double *cz) {
   const double rest[2] = {gp[2], gp[3]};
   const double rel[2] = {rel0, rel1};
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    double back = rest[i] + rel[i];
-    double front = (rest[i] < 0.0) ? back : rel[i];
-    olen[i] = 0.0; ow[i] = 0.0; clen[i] = cord; cz[i] = 0.5 * cord;
-    if (back > 0.0 && front > 0.0) {
-      olen[i] = cord; ow[i] = back + front; clen[i] = 0.0; cz[i] = 0.0;
-    } else if (back <= 0.0 && front <= 0.0) {
-      olen[i] = 0.0; ow[i] = 0.0; clen[i] = cord; cz[i] = 0.5 * cord;
-    } else {
-      double r = rest[i];
-      if (fabs(r) < 0.000000001) r = 0.000000001;
-      double apex = cord * (1.0 + fast_div(rel[i], r));
-      if (apex >= 0.0 && apex <= cord) {
-        if (back > 0.0) {
-          olen[i] = apex; ow[i] = back; clen[i] = cord - apex; cz[i] = 0.5 * (apex + cord);
-        } else {
-          olen[i] = cord - apex; ow[i] = front; clen[i] = apex; cz[i] = 0.5 * apex;
-        }
-      }
-    }
+    const double back = rest[i] + rel[i];
+    const double front = (rest[i] < 0.0) ? back : rel[i];
+    const bool open = back > 0.0 && front > 0.0;
+    const bool closed = back <= 0.0 && front <= 0.0;
+    double r = rest[i];
+    if (fabs(r) < 0.000000001) r = 0.000000001;
+    const double apex = cord * (1.0 + fast_div(rel[i], r));
+    const bool part = !open && !closed && apex >= 0.0 && apex <= cord;
+    const bool pb = part && back > 0.0, pf = part && !(back > 0.0);
+    olen[i] = open ? cord : pb ? apex : pf ? cord - apex : 0.0;
+    ow[i] = open ? back + front : pb ? back : pf ? front : 0.0;
+    clen[i] = open ? 0.0 : pb ? cord - apex : pf ? apex : cord;
+    cz[i] = open ? 0.0 : pb ? 0.5 * (apex + cord) : pf ? 0.5 * apex : 0.5 * cord;
   }
 }
+
+// Areas and lengths of the two glottis sections (23, 24) for the network phase.
+struct GlotOut { double a0, a1, l0, l1; };
 
 // TwoMassModel::calcGeometry / getTubeData (TwoMassModel.cpp:359-440) and incTime (:157-349)
 // on lane 0, with the previous sample's pressures X_P4; relative displacements in X_RELX
 // (current 0/1, previous 2/3) as for the triangular glottis.
-AFS_HD inline void two_mass_glottis(double *X, const Consts &C, const double *gp) {
+AFS_HD inline GlotOut two_mass_glottis(double *X, const Consts &C, const double *gp) {
   double Q = 1.0 + (gp[0] - TM_NAT_F0) * (1.0 / TM_F0_DIV_Q);  // getTensionParameter (:467-485)
   if (Q < 0.05) Q = 0.05;
   const double f = fast_sqrt(Q), inv_f = fast_rcp(f), inv_q = fast_rcp(Q);
@@ -283,8 +286,9 @@ AFS_HD inline void two_mass_glottis(double *X, const Consts &C, const double *gp
   if (passive < 0.0) passive = 0.0;
   double chink = passive * TM_CHINK_LEN + gp[4];
   if (chink < 0.0) chink = 0.0;
-  X[X_AREA + 0] = clampA(2.0 * len * a0 + chink);
-  X[X_AREA + 1] = clampA(2.0 * len * a1 + chink);
+  GlotOut go{clampA(2.0 * len * a0 + chink), clampA(2.0 * len * a1 + chink), th0, th1};
+  X[X_AREA + 0] = go.a0;
+  X[X_AREA + 1] = go.a1;
   X[X_GLEN + 0] = th0;
   X[X_GLEN + 1] = th1;
   // incTime
@@ -323,6 +327,7 @@ AFS_HD inline void two_mass_glottis(double *X, const Consts &C, const double *gp
   X[X_RELX + 3] = rel1;
   X[X_RELX + 0] = (E * D - B * F) * inv_det;
   X[X_RELX + 1] = (A * F - E * Cq) * inv_det;
+  return go;
 }
 
 // getGlottalEntranceLossCoeffFlucher2011(pressure, d) (TdsModel.cpp:1048-1092)
@@ -494,28 +499,44 @@ AFS_HD inline void frame_load(int gl, Lane<W> &R, double *X, const afs_frame *fl
 // ---------------------------------------------------------------------------
 template <int W>
 AFS_HD inline void phase_interpolate(int gl, Lane<W> &R, double *X, const Consts &C, double ratio) {
+  // Branch-free over the lane's slots: pharynx/mouth sections interpolate area, length and
+  // laterality, the nose sections 65..68 take the velum taper (Tube.cpp:402-416); other slots
+  // (glottis, absent) store into sinks.  The area and length stay in the lane (acur, lcur)
+  // for the network phase of the same block.
   using S = Shape<W>;
   const double r1 = 1.0 - ratio;
+  const double open = r1 * X[X_FRAME + 2] + ratio * X[X_FRAME + 3];
 #pragma unroll
   for (int j = 0; j < S::ND; ++j) {
-    const int s = dyn_section(W, j, gl);
-    if (s >= S_PHARYNX0 && s <= S_LAST_MOUTH) {
-      X[X_AREA + s - DYN0] = clampA(r1 * R.aL[j] + ratio * R.aR[j]);
-      X[X_LEN + s - S_PHARYNX0] = r1 * R.lL[j] + ratio * R.lR[j];
-      X[X_LAT + s - S_PHARYNX0] = r1 * R.tL[j] + ratio * R.tR[j];
-    } else if (s >= S_NOSE0) {  // nose sections 65..68: velum taper (Tube.cpp:402-416)
-      double open = r1 * X[X_FRAME + 2] + ratio * X[X_FRAME + 3];
-      int i = s - S_NOSE0;
-      X[X_AREA + s - DYN0] = clampA(open + ((double)(i * i) * (C.h.nose4_area - open)) * (1.0 / 16));
+    const int k = j * W + gl;
+    const int s = DYN0 + k;
+    const bool pm = s >= S_PHARYNX0 && s <= S_LAST_MOUTH;
+    const bool nose = s >= S_NOSE0 && k < NDYNS;
+    const double apm = clampA(r1 * R.aL[j] + ratio * R.aR[j]);
+    const double lpm = r1 * R.lL[j] + ratio * R.lR[j];
+    const double tpm = r1 * R.tL[j] + ratio * R.tR[j];
+    const int i = s - S_NOSE0;
+    const double anose = clampA(open + ((double)(i * i) * (C.h.nose4_area - open)) * (1.0 / 16));
+    const double a = pm ? apm : (nose ? anose : 1.0);
+    R.acur[j] = a;
+    R.lcur[j] = pm ? lpm : C.h.len_nose0;
+    if constexpr (S::ND * W <= NDYP) {
+      X[X_AREA + ((pm || nose) ? k : NDYNS)] = a;
+      X[pm ? X_LEN + s - S_PHARYNX0 : X_ACT] = lpm;
+      X[pm ? X_LAT + s - S_PHARYNX0 : X_ACT] = tpm;
+    } else {  // wider utterances (CPU emulator only)
+      if (pm || nose) X[X_AREA + k] = a;
+      if (pm) { X[X_LEN + s - S_PHARYNX0] = lpm; X[X_LAT + s - S_PHARYNX0] = tpm; }
     }
   }
 }
 
 // The glottis (lane-uniform inputs: every lane of the utterance computes the same values, see
 // Exec::par_uniform).
-AFS_HD inline void phase_glottis(double *X, const Uni &U, const Consts &C, double ratio) {
+template <int MODEL>
+AFS_HD inline GlotOut phase_glottis(double *X, const Consts &C, double ratio) {
   const double r1 = 1.0 - ratio;
-  if (U.opt.glottis_model == AFS_GLOTTIS_TWO_MASS) {
+  if constexpr (MODEL == AFS_GLOTTIS_TWO_MASS) {
     double gp[6];
     for (int k = 0; k < 6; ++k) {
       gp[k] = r1 * X[X_FRAME + 4 + k] + ratio * X[X_FRAME + 10 + k];
@@ -523,7 +544,7 @@ AFS_HD inline void phase_glottis(double *X, const Uni &U, const Consts &C, doubl
     }
     X[X_GP + 5] = GLOTTIS_DEFAULT_ASPIRATION_DB;  // X_GP + 5 is read as the aspiration strength
     X[X_GP + 6] = r1 * X[X_FRAME + 0] + ratio * X[X_FRAME + 1];
-    two_mass_glottis(X, C, gp);
+    return two_mass_glottis(X, C, gp);
   } else {
     double gp[6];
     for (int k = 0; k < 6; ++k) {
@@ -544,8 +565,9 @@ AFS_HD inline void phase_glottis(double *X, const Uni &U, const Consts &C, doubl
     double th0 = G_REST_THICK0 * inv_f, th1 = G_REST_THICK1 * inv_f;
     double olen[2], clen[2], ow[2], cz[2];
     glottis_open_close(gp, cord, rel0, rel1, olen, clen, ow, cz);
-    X[X_AREA + 0] = clampA(olen[0] * ow[0] + chink);
-    X[X_AREA + 1] = clampA(olen[1] * ow[1] + chink);
+    const GlotOut go{clampA(olen[0] * ow[0] + chink), clampA(olen[1] * ow[1] + chink), th0, th1};
+    X[X_AREA + 0] = go.a0;
+    X[X_AREA + 1] = go.a1;
     X[X_GLEN + 0] = th0;
     X[X_GLEN + 1] = th1;
     // incTime (TriangularGlottis.cpp:154-330) with the previous sample's pressures
@@ -576,6 +598,7 @@ AFS_HD inline void phase_glottis(double *X, const Uni &U, const Consts &C, doubl
     X[X_RELX + 3] = rel1;
     X[X_RELX + 0] = (Ee * Dq - B * Ff) * inv_det;
     X[X_RELX + 1] = (A * Ff - Ee * Cq) * inv_det;
+    return go;
   }
 }
 
@@ -608,14 +631,13 @@ AFS_HD inline void phase_positions(double *X) {
 }
 
 template <int W>
-AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C) {
+AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C, const GlotOut &go) {
   // One branch-free block over the lane's slots (absent slots compute on a valid section and
   // store into the sinks), so that the scheduler interleaves the slots' reciprocal and square
   // root chains; the glottal entrance (one section) and the transvelar source follow.
   using S = Shape<W>;
   const afs_options &opt = U.opt;
   const double dt = C.h.dt, idt = C.h.inv_dtTH, idt2 = C.h.inv_dt2TH2;
-  phase_positions(X);  // (for the constriction phase; lane-uniform)
 #pragma unroll
   for (int j = 0; j < S::NST; ++j) {
     const int jj = S::ND + j;
@@ -637,9 +659,9 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     const int ks = present ? k : NDYNS;             // and stores into the sinks
     const bool glot = (s == S_GLOT_LO || s == S_GLOT_UP);
     const bool pm = s >= S_PHARYNX0 && s <= S_LAST_MOUTH;
-    const double area = X[X_AREA + s - DYN0];
-    const double lx = X[glot ? X_GLEN + s - DYN0 : (pm ? X_LEN + s - S_PHARYNX0 : X_GLEN)];
-    const double len = (glot || pm) ? lx : C.h.len_nose0;
+    // (from this block's interpolation and glottis; an absent slot has area and length 1)
+    const double area = glot ? (s == S_GLOT_LO ? go.a0 : go.a1) : R.acur[j];
+    const double len = glot ? (s == S_GLOT_LO ? go.l0 : go.l1) : R.lcur[j];
     // prepareTimeStep's section quantities (TdsModel.cpp:732-834), with the repeated
     // divisions folded into one reciprocal of the area and one of the wall surface.
     const double vol = area * len;
@@ -672,14 +694,14 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     {  // pair (s, s+1)
       double u = 0.0;
       u += X[X_U + s + 1];
-      const double Ai = X[X_AREA + s + 1 - DYN0];
+      const double Ai = R.anx[j];
       const bool on = turb && s < S_LAST_MOUTH && s != S_PHARYNX0 + 3 && s != S_LAST_PHARYNX;
       if (on && ((Ai < area && u > 0) || (Ai > area && u < 0))) R1 = R1 - u * (0.5 * RHO) * ia2;
     }
     {  // pair (s-1, s)
       double u = 0.0;
       u += R.u[j];
-      const double Aa = X[X_AREA + s - 1 - DYN0];
+      const double Aa = R.apv[j];
       const bool on = turb && s > S_PHARYNX0 && s - 1 != S_PHARYNX0 + 3 && s - 1 != S_LAST_PHARYNX;
       if (on && ((area < Aa && u > 0) || (area > Aa && u < 0))) R0 = R0 + u * (0.5 * RHO) * ia2;
     }
@@ -695,7 +717,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     X[X_R1 + ks] = R1;
   }
   if (gl == S_GLOT_LO - DYN0) {  // glottal entrance and transition (TdsModel.cpp:898-950), slot 0
-    const double area = X[X_AREA + 0];
+    const double area = go.a0;
     double R0 = R0g, R1 = R1g;
     double kent = 1.0;
     if (opt.glottis_loss == AFS_ENTRANCE_LOSS_VAN_DEN_BERG) {
@@ -709,7 +731,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     u += R.u[0];
     if (u > 0) R0 = R0 + kent * 0.5 * RHO * fabs(u) * (fast_rcp(ta * ta) - fast_rcp(sa * sa));
     sa = ta;
-    ta = X[X_AREA + 1];
+    ta = go.a1;
     double bt = (ta < opt.flow_separation_area_ratio * sa) ? 1.0 : 0.0;
     double g = 0.8 * X[X_GBF] + (1.0 - 0.8) * bt;
     X[X_GBF] = g;
@@ -843,7 +865,9 @@ AFS_HD inline void store_target(Xc &x, double *X, const DipTarget &t, bool on) {
 template <int W, class Xc>
 AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  // (the section positions come from the network phase: phase_positions)
+  // section positions: every lane evaluates the chain (same values, same stores), in the
+  // block of the first scans, which do not need them
+  x.par([&](int gl, Lane<W> &R) { (void)gl; (void)R; phase_positions(X); });
   x.mark(PH_C_POS);
   const double teeth = X[X_GP + 6];
   // Extend a constriction over the neighbours with area < amin + 0.2 and the same
@@ -1362,15 +1386,25 @@ AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, doub
 // One audio sample.  Xc: execution policy (par / one / lanes / sync).
 // ---------------------------------------------------------------------------
 
+template <int W, int MODEL, class Xc>
+AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
+  GlotOut go{};
+  x.par_uniform([&](int gl, Lane<W> &R) { phase_interpolate<W>(gl, R, X, C, ratio); },
+                [&](Lane<W> &R) { (void)R; go = phase_glottis<MODEL>(X, C, ratio); });
+  x.dyn_neighbors();
+  x.par([&](int gl, Lane<W> &R) { phase_network<W>(gl, R, X, U, C, go); });
+}
+
 template <int W, class Xc>
 AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
   static_assert(W >= TREE_CHAINS, "every solver chain needs a lane of the utterance");
-  x.par_uniform([&](int gl, Lane<W> &R) { phase_interpolate<W>(gl, R, X, C, ratio); },
-                [&](Lane<W> &R) { (void)R; phase_glottis(X, U, C, ratio); });
+  // geometry and network in one block (no LDS round trip between them): the interpolated
+  // areas stay in the lanes, the neighbours' come by lane exchange, the glottis values are
+  // lane-uniform
+  if (U.opt.glottis_model == AFS_GLOTTIS_TWO_MASS) geometry_network<W, AFS_GLOTTIS_TWO_MASS>(x, X, U, C, ratio);
+  else geometry_network<W, AFS_GLOTTIS_TRIANGULAR>(x, X, U, C, ratio);
   x.sync();
   x.mark(PH_GEOMETRY);
-  x.par([&](int gl, Lane<W> &R) { phase_network<W>(gl, R, X, U, C); });
-  x.sync();
   x.mark(PH_NETWORK);
   if (U.opt.generate_noise_sources) {
     phase_constrictions<W>(x, X, U, C);

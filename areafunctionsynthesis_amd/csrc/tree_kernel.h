@@ -82,6 +82,31 @@ struct GpuExec {
     if constexpr (TW == 32) b = max_combine(b, xor16(b));
     return b;
   }
+  // Areas of the neighbouring dynamic sections: section s = 23 + jW + gl, so s+1 is slot j
+  // of lane gl+1 (slot j+1 of lane 0 for the last lane) and s-1 slot j of lane gl-1 (slot
+  // j-1 of the last lane for lane 0).  16 lanes: row rotations (row_ror 15 / 1) of the
+  // utterance's DPP row; 32 lanes: ds_bpermute.
+  __device__ __forceinline__ void dyn_neighbors() {
+    using S = Shape<TW>;
+#pragma unroll
+    for (int j = 0; j < S::ND; ++j) {
+      const double up = (j + 1 < S::ND) ? R->acur[j + 1 < S::ND ? j + 1 : j] : 0.0;
+      const double dn = (j >= 1) ? R->acur[j >= 1 ? j - 1 : j] : 0.0;
+      if constexpr (TW == 16) {
+        const double a = dpp<0x12F>(R->acur[j]), b = dpp<0x12F>(up);  // from lane gl+1 (mod 16)
+        const double c = dpp<0x121>(R->acur[j]), d = dpp<0x121>(dn);  // from lane gl-1 (mod 16)
+        R->anx[j] = gl == TW - 1 ? b : a;
+        R->apv[j] = gl == 0 ? d : c;
+      } else {
+        const int base = (int)(__lane_id() & ~(TW - 1));
+        const int nl = base + (gl + 1) % TW, pl = base + (gl + TW - 1) % TW;
+        const double a = __shfl(R->acur[j], nl, 64), b = __shfl(up, nl, 64);
+        const double c = __shfl(R->acur[j], pl, 64), d = __shfl(dn, pl, 64);
+        R->anx[j] = gl == TW - 1 ? b : a;
+        R->apv[j] = gl == 0 ? d : c;
+      }
+    }
+  }
   // Inclusive prefix sums over the utterance's lanes: row_shr 1, 2, 4, 8 with zero fill
   // (bound_ctrl) inside the 16-lane row; for 32 lanes, lane 15 of the first row is added to
   // the second (row_bcast15 into rows 1 and 3).
@@ -155,6 +180,10 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   }
   ex.sync();
   if (valid) {
+    // (the per-sample fields carry nothing to the next launch; zero them so that their
+    // last values are not kept alive through the time loop for this store)
+#pragma unroll
+    for (int j = 0; j < Shape<TW>::ND; ++j) R.acur[j] = R.lcur[j] = R.anx[j] = R.apv[j] = 0.0;
     ((Lane<TW> *)a.lane_state)[(int64_t)u * TW + gl] = R;
     double *ws = a.lds_state + (int64_t)u * X_TOTAL;
     for (int k = gl; k < X_TOTAL; k += TW) ws[k] = X[k];

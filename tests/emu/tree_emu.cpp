@@ -22,6 +22,15 @@ struct CpuExec {
   template <class F> void one(F f) { f(R[0]); }
   template <class F, class G> void par_uniform(F f, G g) { par(f); g(R[0]); }
   template <class F> void lanes(int n, F f) { for (int k = 0; k < n; ++k) f(k, R[k]); }
+  void dyn_neighbors() {
+    using S = Shape<W>;
+    for (int gl = 0; gl < W; ++gl)
+      for (int j = 0; j < S::ND; ++j) {
+        const int k = j * W + gl, kn = k + 1, kp = k - 1;
+        R[gl].anx[j] = kn < S::ND * W ? R[kn % W].acur[kn / W] : 0.0;
+        R[gl].apv[j] = kp >= 0 ? R[kp % W].acur[kp / W] : 0.0;
+      }
+  }
   void sync() {}
   void mark(int) {}
   template <class F> uint64_t ballot(F f) {
