@@ -67,7 +67,8 @@ enum : int {
   // X_D has a sink at NS)
   X_E = X_P4 + 4, X_D = X_E + NDYP,                      // E: dynamic sections (s-23), D: all
   X_L = X_D + NS + 1, X_R1 = X_L + NDYP, X_R0 = X_R1 + NDYP, X_AREA = X_R0 + NDYP,  // dynamic, s-23
-  X_GLEN = X_AREA + NDYP,                                // glottis section lengths (2)
+  X_RAD = X_AREA + NDYP,                                 // radius sqrt(A / pi) of the dynamic sections
+  X_GLEN = X_RAD + NDYP,                                 // glottis section lengths (2)
   X_SMP = X_GLEN + 2,                                    // dipole samples (41)
   X_UNION = X_SMP + NDIP,
   //   noise scratch (n)
@@ -89,7 +90,7 @@ enum : int {
   X_NONFIN = X_PREVFLOW + 1,
   X_ART = X_NONFIN + 1,        // 40 articulator bytes
   X_RNG = X_ART + 5,           // rand(): value ring, prefix-sum ring (64 u32 each), head, pending (65 doubles)
-  X_GP = X_RNG + 65,           // interpolated glottis controls (6) and teeth position (lane 0)
+  X_GP = X_RNG + 65,           // interpolated glottis controls (6), teeth position, glottis dipole gain
   X_TGLOT = X_GP + 8,          // transglottal-pressure filter x1..x4, y1..y4 (variable entrance loss)
   X_TVEL = X_TGLOT + 8,        // transvelar coupling filters H1, H2: x1..x4, y1..y4 each
   X_TVP = X_TVEL + 16,         // p[43], p[67] after the last update (transvelar filter inputs)
@@ -264,6 +265,12 @@ AFS_HD inline void glottis_open_close(const double *gp, double cord, double rel0
   }
 }
 
+// Gain of the glottis dipole source, 0.5e-7 * 10^(aspiration dB / 20) (TdsModel.cpp:1546),
+// evaluated with the glottis (off the constriction phase's chains).
+AFS_HD inline double glottis_dipole_gain(double aspiration_db) {
+  return 0.5e-7 * exp(aspiration_db * (2.302585092994045684 / 20.0));
+}
+
 // Areas and lengths of the two glottis sections (23, 24) for the network phase.
 struct GlotOut { double a0, a1, l0, l1; };
 
@@ -345,13 +352,12 @@ AFS_HD inline double fulcher_kent(double pressure_dPa, double d_cm) {
   return k;
 }
 
-// getJunctionInductance (TdsModel.cpp:1745-1778)
-// (one reciprocal for b / a and H / b)
-AFS_HD inline double junction_l(double A1, double A2) {
-  if (A1 < AMIN) A1 = AMIN;
-  if (A2 < AMIN) A2 = AMIN;
-  const double Ahi = A1 > A2 ? A1 : A2, Alo = A1 > A2 ? A2 : A1;  // (one sqrt each, no branch)
-  const double a = fast_sqrt(Ahi * (1.0 / PI)), b = fast_sqrt(Alo * (1.0 / PI));
+// getJunctionInductance (TdsModel.cpp:1745-1778) from the radii sqrt(A / pi) of the two
+// sections, which the network phase computed already (X_RAD).  The areas are >= MIN_AREA (the
+// reference's clamps are no-ops) and sqrt is monotone, so max/min of the radii are the radii of
+// max/min of the areas.  (One reciprocal for b / a and H / b.)
+AFS_HD inline double junction_l(double r1, double r2) {
+  const double a = r1 > r2 ? r1 : r2, b = r1 > r2 ? r2 : r1;
   const double r = fast_rcp(a * b);
   const double H = 1.0 - (b * b) * r;
   return (8.0 * RHO / (3.0 * PI * PI)) * H * (a * r);
@@ -544,6 +550,7 @@ AFS_HD inline GlotOut phase_glottis(double *X, const Consts &C, double ratio) {
     }
     X[X_GP + 5] = GLOTTIS_DEFAULT_ASPIRATION_DB;  // X_GP + 5 is read as the aspiration strength
     X[X_GP + 6] = r1 * X[X_FRAME + 0] + ratio * X[X_FRAME + 1];
+    X[X_GP + 7] = glottis_dipole_gain(GLOTTIS_DEFAULT_ASPIRATION_DB);
     return two_mass_glottis(X, C, gp);
   } else {
     double gp[6];
@@ -552,6 +559,7 @@ AFS_HD inline GlotOut phase_glottis(double *X, const Consts &C, double ratio) {
       X[X_GP + k] = gp[k];
     }
     X[X_GP + 6] = r1 * X[X_FRAME + 0] + ratio * X[X_FRAME + 1];
+    X[X_GP + 7] = glottis_dipole_gain(gp[5]);
     double rel0 = X[X_RELX + 0], rel1 = X[X_RELX + 1];
     // calcGeometry + getTubeData + Tube::setGlottisGeometry (TriangularGlottis.cpp:338-411)
     // (divisions sharing a denominator use one reciprocal; sqrt(m k) is a constant since
@@ -713,6 +721,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     X[X_E + ks] = E;
     X[X_D + (present ? s : NS)] = R.p[j] + C.h.dtTH1 * R.pr[j] - E * (beta - 0.0);
     X[X_L + ks] = L;
+    X[X_RAD + ks] = r0;  // (the row phase's junction inductance)
     X[X_R0 + ks] = R0;
     X[X_R1 + ks] = R1;
   }
@@ -834,7 +843,7 @@ AFS_HD inline DipTarget dipole_target(const double *X, const Consts &C, double t
   if (ART == LOWER_LIP) {
     gain = 2.0e-7;
   } else if (ART == VOCAL_FOLDS) {
-    gain = 0.5e-7 * exp(X[X_GP + 5] * (2.302585092994045684 / 20.0));  // 10^(dB/20)
+    gain = X[X_GP + 7];  // 0.5e-7 * 10^(aspiration dB / 20), from the glottis phase
   } else {
     fc = 0.15 * v * fast_sqrt((PI / 4.0) * inv_A);  // 0.15 v / d, d = sqrt(4 A / pi)
     gain = (fabs(c.obst - teeth) < 0.0001) ? 10.0e-7 : 5.0e-7;
@@ -1157,7 +1166,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     // simple junction, with Sondhi's inner length correction between pharynx/mouth sections
     double LAB = LAB0;
     if (dyn) {
-      const double jl = junction_l(X[q.x_la + (X_AREA - X_L)], X[X_AREA + s - DYN0]);
+      const double jl = junction_l(X[q.x_la + (X_RAD - X_L)], X[X_RAD + s - DYN0]);
       if (opt.inner_length_corrections && (q.flags & SR_JUNCTION)) LAB += jl;
     }
     const double G = LAB * idt + RAB;
