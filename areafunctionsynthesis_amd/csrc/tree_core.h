@@ -1370,10 +1370,70 @@ AFS_HD inline double section_pressure(const double *X, const Consts &C, int s) {
   return X[X_D + s] + X[X_E + s - DYN0] * net;
 }
 
-// Phase O (lane 0): radiated flow, glottal tone, output filter (TdsModel.cpp:687-705,
-// Synthesizer.cpp:614-627).  Returns the audio sample.
+// The output stage after the radiated flow (Synthesizer.cpp:614-627): dU/dt, the 8-pole
+// Chebyshev low-pass, x 0.004 / 32767.  It does not feed back into the tube, so it can run
+// over a whole hop of flows afterwards (output_filter_run) or per sample (output_filter_one);
+// both evaluate the same operations on the same state (X_PREVFLOW, X_OUTF).
+AFS_HD inline double output_filter_one(double *X, const Consts &C, double flow) {
+  double op = (flow - X[X_PREVFLOW]) * C.h.inv_dt;
+  X[X_PREVFLOW] = flow;
+  double y = iir_run<8>(X + X_OUTF, C.h.out_a, C.h.out_b, op);
+  double smp = y * 0.004;
+  smp = smp * (1.0 / 32767);
+  if (!isfinite(smp)) X[X_NONFIN] = 1.0;
+  return smp;
+}
+
+// o[0..n) holds the radiated flows of n consecutive samples; they are replaced by the audio
+// samples.  The filter state stays in registers over the run; loads go 8 samples ahead.
+AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int n) {
+  double sx[8], sy[8], ca[9], cb[9];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sx[k] = X[X_OUTF + k]; sy[k] = X[X_OUTF + 8 + k]; }
+#pragma unroll
+  for (int k = 0; k <= 8; ++k) { ca[k] = C.h.out_a[k]; cb[k] = C.h.out_b[k]; }
+  const double inv_dt = C.h.inv_dt;
+  double prev = X[X_PREVFLOW];
+  bool nonfin = false;
+  for (int t0 = 0; t0 < n; t0 += 8) {
+    double f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = (t0 + i < n) ? o[t0 + i] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (t0 + i >= n) break;
+      const double op = (f[i] - prev) * inv_dt;
+      prev = f[i];
+      double acc = ca[0] * op;
+#pragma unroll
+      for (int k = 1; k <= 8; ++k) {
+        acc += ca[k] * sx[k - 1];
+        acc += cb[k] * sy[k - 1];
+      }
+#pragma unroll
+      for (int k = 7; k > 0; --k) { sx[k] = sx[k - 1]; sy[k] = sy[k - 1]; }
+      sx[0] = op;
+      sy[0] = acc;
+      double smp = acc * 0.004;
+      smp = smp * (1.0 / 32767);
+      nonfin = nonfin || !isfinite(smp);
+      o[t0 + i] = smp;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { X[X_OUTF + k] = sx[k]; X[X_OUTF + 8 + k] = sy[k]; }
+  X[X_PREVFLOW] = prev;
+  if (nonfin) X[X_NONFIN] = 1.0;
+}
+
+// Hops of at least this many samples run the output filter once per hop (output_filter_run)
+// instead of inside the sample step.
+constexpr int OUT_DEFER_MIN_HOP = 32;
+
+// Phase O (lane-uniform): radiated flow and glottal tone (TdsModel.cpp:687-705); with
+// defer == false also the output filter.  Returns the audio sample, or with defer the flow.
 // p25 = the new pressure of section 25 (section_pressure), the glottal tone filter's input.
-AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, double p25) {
+AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, double p25, bool defer) {
   double flow = 0.0;
   flow += X[X_U + 93];
   flow += X[X_U + 94];
@@ -1382,13 +1442,8 @@ AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, doub
   // (the tone filter runs either way, its output is selected: no branch in the output stage)
   const double tone = iir_run<4>(X + X_TONE, C.h.tone_a, C.h.tone_b, p25);
   flow += U.opt.radiation_from_skin ? tone : 0.0;
-  double op = (flow - X[X_PREVFLOW]) * C.h.inv_dt;
-  X[X_PREVFLOW] = flow;
-  double y = iir_run<8>(X + X_OUTF, C.h.out_a, C.h.out_b, op);
-  double smp = y * 0.004;
-  smp = smp * (1.0 / 32767);
-  if (!isfinite(smp)) X[X_NONFIN] = 1.0;
-  return smp;
+  if (defer) return flow;
+  return output_filter_one(X, C, flow);
 }
 
 // ---------------------------------------------------------------------------
@@ -1405,7 +1460,7 @@ AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts
 }
 
 template <int W, class Xc>
-AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
+AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio, bool defer_out) {
   static_assert(W >= TREE_CHAINS, "every solver chain needs a lane of the utterance");
   // geometry and network in one block (no LDS round trip between them): the interpolated
   // areas stay in the lanes, the neighbours' come by lane exchange, the glottis values are
@@ -1465,7 +1520,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.mark(PH_BACKWARD);
   // the state update and the output stage (lane-uniform: radiated flow, filters) in one phase
   x.par_uniform([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, X, U, C); },
-                [&](Lane<W> &R) { R.sample = phase_output(X, U, C, section_pressure(X, C, S_PHARYNX0)); });
+                [&](Lane<W> &R) { R.sample = phase_output(X, U, C, section_pressure(X, C, S_PHARYNX0), defer_out); });
   x.sync();
   x.mark(PH_UPDATE);
   x.mark(PH_OUTPUT);

@@ -168,15 +168,23 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   const afs_frame *fu = a.frames + (int64_t)(a.frame_row ? a.frame_row[ue] : ue) * a.frame_stride;
   double *o = a.out + (int64_t)ue * a.out_stride;
   int64_t t = 0;
+  // long hops: the output filter runs over each hop's flows once the hop is done (lane 0
+  // re-reads the flows it stored; the filter does not feed back into the tube)
+  const bool defer = a.hop >= OUT_DEFER_MIN_HOP;
   for (int k = a.k_begin; k < a.k_end; ++k) {
     frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
     ex.sync();
+    const int64_t t0 = t;
     for (int i = 0; i < a.hop; ++i) {
       const double ratio = (double)i / (double)a.hop;
-      sample_step<TW>(ex, X, a.uni, C, ratio);
+      sample_step<TW>(ex, X, a.uni, C, ratio, defer);
       if (valid && gl == 0) o[t] = R.sample;
       ++t;
     }
+    if (defer && gl == 0) {
+      if (valid) output_filter_run(X, C, o + t0, a.hop);
+    }
+    ex.sync();
   }
   ex.sync();
   if (valid) {

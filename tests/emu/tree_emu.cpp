@@ -73,11 +73,13 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
   reset_lds(X.data(), seed);
   CpuExec<W> ex{R.data()};
   long t = 0;
+  const bool defer = hop >= OUT_DEFER_MIN_HOP;  // as the GPU kernel (tree_kernel.h)
   for (int k = 1; k < F; ++k) {
     for (int gl = 0; gl < W; ++gl) frame_load<W>(gl, R[gl], X.data(), frames + k - 1, frames + k);
+    const long t0 = t;
     for (int i = 0; i < hop; ++i) {
       double ratio = (double)i / (double)hop;
-      sample_step<W>(ex, X.data(), T.uni, T.consts, ratio);
+      sample_step<W>(ex, X.data(), T.uni, T.consts, ratio, defer);
       out[t] = R[0].sample;
       if (t < ndump) {
         for (int gl = 0; gl < W; ++gl)
@@ -89,6 +91,7 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
       }
       ++t;
     }
+    if (defer) output_filter_run(X.data(), T.consts, out + t0, hop);
   }
   return t;
 }
