@@ -1385,7 +1385,8 @@ AFS_HD inline double output_filter_one(double *X, const Consts &C, double flow) 
 }
 
 // o[0..n) holds the radiated flows of n consecutive samples; they are replaced by the audio
-// samples.  The filter state stays in registers over the run; loads go 8 samples ahead.
+// samples.  The filter state stays in registers over the run; the loads of the next 8 samples
+// are issued before the current 8 are filtered (their latency hides behind the filter chain).
 AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int n) {
   double sx[8], sy[8], ca[9], cb[9];
 #pragma unroll
@@ -1395,10 +1396,13 @@ AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int 
   const double inv_dt = C.h.inv_dt;
   double prev = X[X_PREVFLOW];
   bool nonfin = false;
-  for (int t0 = 0; t0 < n; t0 += 8) {
-    double f[8];
+  double f[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = (t0 + i < n) ? o[t0 + i] : 0.0;
+  for (int i = 0; i < 8; ++i) f[i] = (i < n) ? o[i] : 0.0;
+  for (int t0 = 0; t0 < n; t0 += 8) {
+    double g[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = (t0 + 8 + i < n) ? o[t0 + 8 + i] : 0.0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if (t0 + i >= n) break;
@@ -1419,6 +1423,8 @@ AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int 
       nonfin = nonfin || !isfinite(smp);
       o[t0 + i] = smp;
     }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = g[i];
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) { X[X_OUTF + k] = sx[k]; X[X_OUTF + 8 + k] = sy[k]; }
