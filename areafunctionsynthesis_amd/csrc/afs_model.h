@@ -136,6 +136,7 @@ struct Hot {
   double fs, dt, dtTH1, noise_amp_F, noise_lp_c, noise_x_2000, sqrt12, nose4_area, fossa_R0;
   double rrad_num, lrad_num, tone_a[5], tone_b[5], out_a[9], out_b[9];
   double len_nose0, Bw_ph0, Mw_ph0, Kw_ph0, area_last_trachea, area_last_nose;
+  double rrad_nose, lrad_nose;  // radiation R and L of the nostrils (static section 83)
   double inv_dtTH, inv_dt2TH2;  // 1 / (dt theta), 1 / (dt theta)^2
   double Tt;                    // glottis time step 1 / fs
   double inv_dt;                // 1 / dt

@@ -386,6 +386,10 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   for (int i = 0; i < 5; ++i) { h.tglot_a[i] = t->tglot_a[i]; h.tglot_b[i] = t->tglot_b[i]; h.tvel2_a[i] = t->tvel2_a[i]; }
   h.len_nose0 = t->len[S_NOSE0]; h.Bw_ph0 = t->Bw[S_PHARYNX0]; h.Mw_ph0 = t->Mw[S_PHARYNX0];
   h.Kw_ph0 = t->Kw[S_PHARYNX0]; h.area_last_trachea = t->area[S_LAST_TRACHEA]; h.area_last_nose = t->area[S_LAST_NOSE];
+  // the nostrils' radiation elements, as the row phase evaluates them for a static area
+  // (tree_core.h radiation_rl; the device's division is within an ulp of this one)
+  h.rrad_nose = t->rrad_num / (9.0 * PI * PI * h.area_last_nose);
+  h.lrad_nose = t->lrad_num / (3.0 * PI * std::sqrt(h.area_last_nose * PI));
   h.inv_dtTH = 1.0 / (t->dt * TH);
   h.inv_dt2TH2 = 1.0 / (t->dt * t->dt * TH * TH);
   h.Tt = 1.0 / t->fs;

@@ -94,7 +94,8 @@ enum : int {
   X_TGLOT = X_GP + 8,          // transglottal-pressure filter x1..x4, y1..y4 (variable entrance loss)
   X_TVEL = X_TGLOT + 8,        // transvelar coupling filters H1, H2: x1..x4, y1..y4 each
   X_TVP = X_TVEL + 16,         // p[43], p[67] after the last update (transvelar filter inputs)
-  X_TOTAL = X_TVP + 2,
+  X_RRAD = X_TVP + 2,          // mouth radiation R and L (section 64), from the network phase
+  X_TOTAL = X_RRAD + 2,
   // LDS stride of the utterance blocks: 128 B modulo the 256-B bank row, so that the two
   // utterances of a 32-lane LDS lane group (ds_read_b64: lanes 0-31, 32-63) address the
   // same slot through disjoint banks
@@ -713,6 +714,14 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
       const bool on = turb && s > S_PHARYNX0 && s - 1 != S_PHARYNX0 + 3 && s - 1 != S_LAST_PHARYNX;
       if (on && ((area < Aa && u > 0) || (area > Aa && u < 0))) R0 = R0 + u * (0.5 * RHO) * ia2;
     }
+    if (j == (S_LAST_MOUTH - DYN0) / W) {  // the slot that holds section 64 on one lane
+      // radiation resistance and inductance of the mouth (TdsModel.cpp:1874, 1889)
+      const double Rrad = fast_div(C.h.rrad_num, 9.0 * PI * PI * area);
+      const double Lrad = fast_div(C.h.lrad_num, 3.0 * PI * fast_sqrt(area * PI));
+      const bool own = s == S_LAST_MOUTH;
+      X[own ? X_RRAD : X_ACT] = Rrad;
+      X[own ? X_RRAD + 1 : X_ACT + 1] = Lrad;
+    }
     if (j == 0) { R0g = R0; R1g = R1; }
     Eg[j] = E;
     betag[j] = beta;
@@ -1183,8 +1192,10 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     Xw[q.x_e1] = -EB;
     Xw[q.x_e2] = -(-EB - (LB * idt + R1B));
   }
+  constexpr int J64 = (S_LAST_MOUTH - DYN0) / W, J83 = S::ND + (S_LAST_NOSE - 46) / W;
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
+    if (j != J64 && j != J83) continue;  // (no other slot holds a radiation section)
     if (!(rec[j].flags & SR_RADIATION)) continue;
     // radiation rows of s = 64 / 83 (TdsModel.cpp:1841-1911)
     const bool dyn = j < S::ND;
@@ -1200,15 +1211,16 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
     R.rad_un[0] = X[q.x_rad[4]]; R.rad_un[1] = X[q.x_rad[5]];
     const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
+    (void)AB;
     {
-      double Rrad = fast_div(C.h.rrad_num, 9.0 * PI * PI * AB);
+      const double Rrad = dyn ? X[X_RRAD] : C.h.rrad_nose;  // (network phase / tables)
       double F = LA2 * idt + RA2 + Rrad;
       double H = -(LA2 * idt) * (uR + uL) - (LA2 * (TH1 / TH)) * (uRr + uLr) + Sr;
       Xw[X_DIAG + rc] = -(-EB - F);
       Xw[X_RHS + rc] = -(H - DB);
     }
     {
-      double Lrad = fast_div(C.h.lrad_num, 3.0 * PI * fast_sqrt(AB * PI));
+      const double Lrad = dyn ? X[X_RRAD + 1] : C.h.lrad_nose;
       double LAB2 = LA2 + Lrad;
       double G = LAB2 * idt + RA2;
       double H = -idt * (LA2 * uR + LAB2 * uL) - (TH1 / TH) * (LA2 * uRr + LAB2 * uLr) + Sr;
@@ -1345,7 +1357,8 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
       if (s == S_MOUTH0 + 2) Xw[X_TVP] = R.p[j];
       if (s == S_NOSE0 + 2) Xw[X_TVP + 1] = R.p[j];
     }
-    if (rec[j].flags & SR_RADIATION) {  // the two radiation currents of s = 64 / 83
+    constexpr int J64 = (S_LAST_MOUTH - DYN0) / W, J83 = S::ND + (S_LAST_NOSE - 46) / W;
+    if ((j == J64 || j == J83) && (rec[j].flags & SR_RADIATION)) {  // the two radiation currents of s = 64 / 83
       const SecRec &q = rec[j];
       for (int k = 0; k < 2; ++k) {
         double un = X[q.x_rad[k]];
