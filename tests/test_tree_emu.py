@@ -105,3 +105,24 @@ def test_options_vs_oracle(emu, oracle, opt):
         y = oracle.utterance(frames, hop, 5, fs, opt=opt)
         assert np.abs(x[:2048] - y[:2048]).max() <= TOL, fs
         assert np.sqrt(np.mean((x - y) ** 2)) < 1e-8, fs
+
+
+@pytest.mark.parametrize("hop", [7, 31, 32, 97])
+def test_output_stage_paths_vs_oracle(emu, oracle, hop):
+    """Hops below OUT_DEFER_MIN_HOP (32) run the output filter inside the sample step, longer
+    hops once per hop over the hop's flows (tree_core.h output_filter_run); both match the
+    oracle, including across frame transitions."""
+    from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS
+    from areafunctionsynthesis_amd.params import default_shapes
+    sh = default_shapes()
+    frames = []
+    for name, f0 in (("a:", 120.0), ("i:", 130.0), ("s", 125.0), ("u:", 110.0), ("a:", 118.0)):
+        f = oracle.af_to_frame(sh[name])
+        f["glottis"] = DEFAULT_GLOTTIS
+        f["glottis"][0] = f0
+        frames.append(f)
+    frames = np.stack(frames * 6)
+    x = emu.opt(frames, hop, 3, 22050.0, {})
+    y = oracle.utterance(frames, hop, 3, 22050.0)
+    assert x.size == y.size == (frames.size - 1) * hop
+    assert np.abs(x - y).max() <= TOL
