@@ -986,11 +986,13 @@ AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Con
 template <int W, class Xc>
 AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
+  // (branch-free over the lane's dipole slots: a slot past the 41 dipoles reads dipole 0's
+  // values into its own, never used, state)
   x.par([&](int gl, Lane<W> &R) {
 #pragma unroll
     for (int k = 0; k < S::NDP; ++k) {
-      const int d = gl + k * W;
-      if (d >= NDIP) continue;
+      const int d0 = gl + k * W;
+      const int d = d0 < NDIP ? d0 : 0;
       double cn = X[X_CUTN + d];
       if (cn != 0.0) R.dcut[k] = cn;  // targeted this step: cutoff was (re)assigned
       double old = R.damp[k];
@@ -1019,16 +1021,18 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
   const int base = head0 - pend;  // ring index of this sample's first draw
   const int need = 12 * __builtin_popcountll(act);
   // draws [lo, hi) of this sample are generated: add their share to the owners' sums
+  // (branch-free: every slot loads its two prefix sums, inactive ones add zero)
   auto consume = [&](int lo, int hi) {
     x.par([&](int gl, Lane<W> &R) {
 #pragma unroll
       for (int k = 0; k < S::NDP; ++k) {
-        const int d = gl + k * W;
-        if (d >= NDIP || !((act >> d) & 1)) continue;
+        const int d = gl + k * W;  // < 64
+        const bool on = d < NDIP && ((act >> d) & 1);
         const int q0 = 12 * __builtin_popcountll(act & ((1ull << d) - 1));
         const int a = q0 > lo ? q0 : lo, b = q0 + 12 < hi ? q0 + 12 : hi;
-        if (a < b)
-          R.racc[k] += g[RNG_S + ((base + b - 1) & (RNG_RING - 1))] - g[RNG_S + ((base + a - 1) & (RNG_RING - 1))];
+        const uint32_t sb = g[RNG_S + ((base + b - 1) & (RNG_RING - 1))];
+        const uint32_t sa = g[RNG_S + ((base + a - 1) & (RNG_RING - 1))];
+        R.racc[k] += (on && a < b) ? sb - sa : 0u;
       }
     });
   };
@@ -1079,8 +1083,10 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
   }
   x.sync();
   x.mark(PH_N_RNG);
-  x.one([&](Lane<W> &R) {
-    (void)R;
+  // (every lane stores the same ring head / pending count; the shaping filter is branch-free
+  // over the slots except for the exponential of a cutoff other than the clamped 2000 Hz)
+  x.par([&](int gl, Lane<W> &R) {
+    (void)gl; (void)R;
     int32_t *c = (int32_t *)g;
     c[RNG_HEAD] = head;
     c[RNG_PEND] = avail - need;
@@ -1089,21 +1095,18 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
 #pragma unroll
     for (int k = 0; k < S::NDP; ++k) {
       const int d = gl + k * W;
-      if (d >= NDIP) continue;
-      double smp = 0.0;
-      if ((act >> d) & 1) {
-        double xi = (double)(int32_t)R.racc[k];
-        xi *= 1.0 / 2147483647.0;  // constant reciprocals (within 1 ulp of the divisions)
-        xi -= 6.0;
-        xi *= 0.28867513459481288225;  // 1 / sqrt(12)
-        double cut = R.dcut[k];
-        double xx = (cut == 2000.0) ? C.h.noise_x_2000 : exp(-2.0 * PI * (cut * C.h.dt));
-        double y = (1.0 - xx) * xi;
-        y += xx * R.dout[k];
-        R.dout[k] = y;
-        smp = y * R.damp[k];
-      }
-      X[X_SMP + d] = smp;
+      const bool on = d < NDIP && ((act >> d) & 1);
+      double xi = (double)(int32_t)R.racc[k];
+      xi *= 1.0 / 2147483647.0;  // constant reciprocals (within 1 ulp of the divisions)
+      xi -= 6.0;
+      xi *= 0.28867513459481288225;  // 1 / sqrt(12)
+      const double cut = R.dcut[k];
+      double xx = C.h.noise_x_2000;
+      if (on && cut != 2000.0) xx = exp(-2.0 * PI * (cut * C.h.dt));
+      double y = (1.0 - xx) * xi;
+      y += xx * R.dout[k];
+      R.dout[k] = on ? y : R.dout[k];
+      X[d < NDIP ? X_SMP + d : X_ACT + 2] = on ? y * R.damp[k] : 0.0;
     }
   });
 }
