@@ -76,6 +76,11 @@ AFS_HD constexpr bool is_static_section(int s) {
 // (X_FILL slot f, zeroed before the forward pass).  c = -1: idle.
 constexpr int TREE_CHAINS = 16;
 constexpr int TREE_MAX_ROUNDS = 14;
+// The plan's round count and the rounds whose pivot (forward) / neighbour solution (backward)
+// stays in registers; the kernel unrolls the rounds with these, and build_tables checks that
+// the schedule it derives from the plan has exactly these values.
+constexpr int TREE_ROUNDS = 12;
+constexpr uint64_t TREE_FWD_CARRY = 0xfd0, TREE_BWD_CARRY = 0x480;
 constexpr int TREE_NFILL = 64;  // fill edges (tree_core.h X_FILL)
 constexpr int TREE_NE = 104;
 struct SolveStep {

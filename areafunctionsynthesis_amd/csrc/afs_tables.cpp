@@ -288,7 +288,8 @@ bool tree_schedule(Tables *t) {
     if (all) t->bwd_carry |= 1ull << r;
     for (int k = 0; k < TREE_CHAINS; ++k) carry[k] = t->step[r][k].c;
   }
-  return true;
+  // the tree kernel unrolls the rounds with these values compiled in (afs_model.h)
+  return t->n_rounds == TREE_ROUNDS && t->fwd_carry == TREE_FWD_CARRY && t->bwd_carry == TREE_BWD_CARRY;
 }
 
 }  // namespace

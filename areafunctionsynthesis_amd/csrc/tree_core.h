@@ -1269,12 +1269,12 @@ AFS_HD inline void forward_body(const StepRec &s, double *X, SolveCarry &cr) {
   lds_at(X, s.e01) = a01 - f0 * a1;
 }
 
-AFS_HD inline void solve_forward(int k, int r, bool carried, double *X, const Consts &C, SolveCarry &cr) {
+template <int R>
+AFS_HD inline void solve_forward(int k, double *X, const Consts &C, SolveCarry &cr) {
   const StepRec s = cr.cur;
   cr.cur = cr.next;
-  cr.next = C.step[r + 2 < TREE_MAX_ROUNDS ? r + 2 : TREE_MAX_ROUNDS - 1][k];
-  if (carried) forward_body<true>(s, X, cr);
-  else forward_body<false>(s, X, cr);
+  cr.next = C.step[R + 2 < TREE_MAX_ROUNDS ? R + 2 : TREE_MAX_ROUNDS - 1][k];
+  forward_body<((TREE_FWD_CARRY >> R) & 1) != 0>(s, X, cr);
 }
 
 // Backward round (descending): x_c = (y_c - a0 x_n0 - a1 x_n1) / d_c (absent neighbours read
@@ -1293,12 +1293,30 @@ AFS_HD inline void backward_body(const StepRec &s, double *X, SolveCarry &cr) {
   cr.y = xc;
 }
 
-AFS_HD inline void solve_backward(int k, int r, bool carried, double *X, const Consts &C, SolveCarry &cr) {
+template <int R>
+AFS_HD inline void solve_backward(int k, double *X, const Consts &C, SolveCarry &cr) {
   const StepRec s = cr.cur;
   cr.cur = cr.next;
-  cr.next = C.step[r >= 2 ? r - 2 : 0][k];
-  if (carried) backward_body<true>(s, X, cr);
-  else backward_body<false>(s, X, cr);
+  cr.next = C.step[R >= 2 ? R - 2 : 0][k];
+  backward_body<((TREE_BWD_CARRY >> R) & 1) != 0>(s, X, cr);
+}
+
+// The rounds, unrolled (TREE_ROUNDS, the carried rounds compiled in: no loop and no branch).
+template <int W, int R, class Xc>
+AFS_HD inline void forward_rounds(Xc &x, double *X, const Consts &C) {
+  if constexpr (R < TREE_ROUNDS) {
+    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &L) { solve_forward<R>(k, X, C, L.sc); });
+    x.sync();
+    forward_rounds<W, R + 1>(x, X, C);
+  }
+}
+template <int W, int R, class Xc>
+AFS_HD inline void backward_rounds(Xc &x, double *X, const Consts &C) {
+  if constexpr (R >= 0) {
+    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &L) { solve_backward<R>(k, X, C, L.sc); });
+    x.sync();
+    backward_rounds<W, R - 1>(x, X, C);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1508,7 +1526,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.par([&](int gl, Lane<W> &R) { phase_rows<W>(gl, R, X, X, U, C); });
   x.sync();
   x.mark(PH_ROWS);
-  const int nr = U.n_rounds;
+  constexpr int nr = TREE_ROUNDS;  // (build_tables checks the schedule against it)
   // fill edges start at zero
   x.par([&](int gl, Lane<W> &R) {
     (void)R;
@@ -1521,12 +1539,8 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
     R.sc.next = C.step[1][k];
     R.sc.d = R.sc.y = 0.0;
   });
-  AFS_LDS_DRAIN();  // the loop head must not wait for the previous round's stores
-  for (int r = 0; r < nr; ++r) {
-    const bool carried = (U.fwd_carry >> r) & 1;
-    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { solve_forward(k, r, carried, X, C, R.sc); });
-    x.sync();
-  }
+  AFS_LDS_DRAIN();  // the first round must not wait for the previous round's stores
+  forward_rounds<W, 0>(x, X, C);
   x.mark(PH_FORWARD);
   x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) {
     R.sc.cur = C.step[nr - 1][k];
@@ -1534,11 +1548,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
     R.sc.y = 0.0;
   });
   AFS_LDS_DRAIN();
-  for (int r = nr - 1; r >= 0; --r) {
-    const bool carried = (U.bwd_carry >> r) & 1;
-    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { solve_backward(k, r, carried, X, C, R.sc); });
-    x.sync();
-  }
+  backward_rounds<W, nr - 1>(x, X, C);
   x.mark(PH_BACKWARD);
   // the state update and the output stage (lane-uniform: radiated flow, filters) in one phase
   x.par_uniform([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, X, U, C); },
