@@ -787,12 +787,16 @@ struct Cons { int first, last, narrow, art; double obst, lat; };
 template <int W, class Xc, class P>
 AFS_HD inline uint64_t mouth_mask(Xc &x, P pred) {
   using S = Shape<W>;
+  // (pred is evaluated for every slot, on section 25 for slots outside the pharynx/mouth, so
+  // that its LDS loads are not under a short-circuit branch)
   uint64_t M = 0;
 #pragma unroll
   for (int j = 0; j < S::ND; ++j)
     M |= x.ballot([&](int gl, Lane<W> &R) {
       const int m = j * W + gl - 2;
-      return m >= 0 && m < NPM && pred(R, j, m);
+      const bool in = m >= 0 && m < NPM;
+      const bool p = pred(R, j, in ? m : 0);
+      return in && p;
     }) << (j * W);
   return (M >> 2) & ((1ull << NPM) - 1);
 }
@@ -807,10 +811,11 @@ AFS_HD inline MinIdx mouth_min(Xc &x, const double *X, P pred) {
 #pragma unroll
     for (int j = 0; j < S::ND; ++j) {
       const int m = j * W + gl - 2;
-      if (m >= 0 && m < NPM && pred(R, j, m)) {
-        const double a = X[X_AREA + m + 2];
-        if (a < b.v) b = MinIdx{a, m};
-      }
+      const bool in = m >= 0 && m < NPM;
+      const int mm = in ? m : 0;
+      const bool p = pred(R, j, mm);
+      const double a = X[X_AREA + mm + 2];  // (loaded for every slot: no branch around it)
+      if (in && p && a < b.v) b = MinIdx{a, m};
     }
     return b;
   });
@@ -826,8 +831,10 @@ template <int W, class Xc>
 AFS_HD inline uint64_t obstacle_mask(Xc &x, const double *X, double obst) {
   return mouth_mask<W>(x, [&](Lane<W> &R, int j, int m) {
     (void)R; (void)j;
-    const double pos = X[X_POS + m];
-    return pos <= obst && pos + X[X_LEN + m] >= obst;
+    const double pos = X[X_POS + m], len = X[X_LEN + m];  // (both loads unconditional)
+    const bool lo = pos <= obst;
+    const bool hi = pos + len >= obst;
+    return lo && hi;
   });
 }
 
@@ -907,7 +914,9 @@ AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Con
 #pragma unroll
       for (int j = 0; j < S::ND; ++j) {
         const int m = j * W + gl - 2;
-        if (m >= 0 && m < NPM && m >= f && m <= l) b = max_combine(b, X[X_LAT + m]);
+        const bool in = m >= 0 && m < NPM && m >= f && m <= l;
+        const double lat = X[X_LAT + (m >= 0 && m < NPM ? m : 0)];  // (unconditional load)
+        if (in) b = max_combine(b, lat);
       }
       return b;
     });
