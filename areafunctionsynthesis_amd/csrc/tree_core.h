@@ -705,14 +705,20 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
       u += X[X_U + s + 1];
       const double Ai = R.anx[j];
       const bool on = turb && s < S_LAST_MOUTH && s != S_PHARYNX0 + 3 && s != S_LAST_PHARYNX;
-      if (on && ((Ai < area && u > 0) || (Ai > area && u < 0))) R1 = R1 - u * (0.5 * RHO) * ia2;
+      // (bitwise conditions and a select: with && / if, the compiler sinks the load of u into
+      // a branch and waits for it there)
+      const bool c = ((Ai < area) & (u > 0)) | ((Ai > area) & (u < 0));
+      const double Rb = R1 - u * (0.5 * RHO) * ia2;
+      R1 = (on & c) ? Rb : R1;
     }
     {  // pair (s-1, s)
       double u = 0.0;
       u += R.u[j];
       const double Aa = R.apv[j];
       const bool on = turb && s > S_PHARYNX0 && s - 1 != S_PHARYNX0 + 3 && s - 1 != S_LAST_PHARYNX;
-      if (on && ((area < Aa && u > 0) || (area > Aa && u < 0))) R0 = R0 + u * (0.5 * RHO) * ia2;
+      const bool c = ((area < Aa) & (u > 0)) | ((area > Aa) & (u < 0));
+      const double Rb = R0 + u * (0.5 * RHO) * ia2;
+      R0 = (on & c) ? Rb : R0;
     }
     if (j == (S_LAST_MOUTH - DYN0) / W) {  // the slot that holds section 64 on one lane
       // radiation resistance and inductance of the mouth (TdsModel.cpp:1874, 1889)
@@ -921,12 +927,12 @@ AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Con
       return b;
     });
     const double jet = X[X_POS + l] + X[X_LEN + l];
-    if (teeth - jet < 2.0) {
-      c.obst = teeth;
-      min_teeth = X[X_AREA + c.narrow - DYN0];
-    } else {
-      c.obst = X[X_POS + l + 1] + 0.5 * X[X_LEN + l + 1];
-    }
+    // (all loads first, then selects)
+    const double an = X[X_AREA + c.narrow - DYN0];
+    const double ob = X[X_POS + l + 1] + 0.5 * X[X_LEN + l + 1];
+    const bool at_teeth = teeth - jet < 2.0;
+    c.obst = at_teeth ? teeth : ob;
+    min_teeth = at_teeth ? an : min_teeth;
   };
   // Up to four constrictions in the reference's order: glottis, tongue, second tongue, lip.
   // (Absent ones keep a dummy of their kind with valid indices; their targets are not stored.)
@@ -1046,7 +1052,7 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
     });
   };
   int avail = pend;
-  if (avail > 0) consume(0, avail);
+  consume(0, avail);  // (with avail == 0 it adds nothing)
   int head = head0;
   constexpr int RJ = rng_lanes<W>(), RNG_BLOCK = 3 * RJ;
   while (avail < need) {
@@ -1058,32 +1064,35 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
     x.template scan_add<3>(
         [&](int gl, Lane<W> &R) {
           (void)R;
+          // (every lane loads; lanes past RJ only feed their own, discarded, prefix sums)
           U4 v{{0u, 0u, 0u, 0u}};
-          if (gl < RJ)
-            for (int c = 0; c < 3; ++c) v.v[c] = g[RNG_R + ((head + 3 * gl + c - 31) & (RNG_RING - 1))];
+          for (int c = 0; c < 3; ++c) v.v[c] = g[RNG_R + ((head + 3 * gl + c - 31) & (RNG_RING - 1))];
           return v;
         },
         [&](int gl, Lane<W> &R, const U4 &p) {
-          if (gl >= RJ) return;
+          const bool on = gl < RJ;  // lanes past RJ store into a sink
+          uint32_t *sink = (uint32_t *)(X + X_ACT + 8);
           const uint32_t n0 = b0 + p.v[0], n1 = b1 + p.v[1], n2 = b2 + p.v[2];
-          g[RNG_R + ((head + 3 * gl) & (RNG_RING - 1))] = n0;
-          g[RNG_R + ((head + 3 * gl + 1) & (RNG_RING - 1))] = n1;
-          g[RNG_R + ((head + 3 * gl + 2) & (RNG_RING - 1))] = n2;
+          *(on ? &g[RNG_R + ((head + 3 * gl) & (RNG_RING - 1))] : sink) = n0;
+          *(on ? &g[RNG_R + ((head + 3 * gl + 1) & (RNG_RING - 1))] : sink) = n1;
+          *(on ? &g[RNG_R + ((head + 3 * gl + 2) & (RNG_RING - 1))] : sink) = n2;
           R.rtmp[0] = n0 >> 1; R.rtmp[1] = n1 >> 1; R.rtmp[2] = n2 >> 1;
         });
     // prefix sums of the outputs in sequence order
     x.template scan_add<1>(
         [&](int gl, Lane<W> &R) {
+          (void)gl;
           U4 v{{0u, 0u, 0u, 0u}};
-          if (gl < RJ) v.v[0] = R.rtmp[0] + R.rtmp[1] + R.rtmp[2];
+          v.v[0] = R.rtmp[0] + R.rtmp[1] + R.rtmp[2];
           return v;
         },
         [&](int gl, Lane<W> &R, const U4 &p) {
-          if (gl >= RJ) return;
+          const bool on = gl < RJ;
+          uint32_t *sink = (uint32_t *)(X + X_ACT + 8);
           const uint32_t s2 = sb + p.v[0], s1 = s2 - R.rtmp[2], s0 = s1 - R.rtmp[1];
-          g[RNG_S + ((head + 3 * gl) & (RNG_RING - 1))] = s0;
-          g[RNG_S + ((head + 3 * gl + 1) & (RNG_RING - 1))] = s1;
-          g[RNG_S + ((head + 3 * gl + 2) & (RNG_RING - 1))] = s2;
+          *(on ? &g[RNG_S + ((head + 3 * gl) & (RNG_RING - 1))] : sink) = s0;
+          *(on ? &g[RNG_S + ((head + 3 * gl + 1) & (RNG_RING - 1))] : sink) = s1;
+          *(on ? &g[RNG_S + ((head + 3 * gl + 2) & (RNG_RING - 1))] : sink) = s2;
         });
     x.sync();
     consume(avail, avail + RNG_BLOCK);
@@ -1157,7 +1166,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
   const afs_options &opt = U.opt;
   SecRec rec[S::NSL];
   load_sec_recs<W>(gl, C, rec);
-  if (gl == 0) Xw[X_OFF + EDGE_ZERO] = 0.0;  // the solver's zero edge (union slot)
+  Xw[X_OFF + EDGE_ZERO] = 0.0;  // the solver's zero edge (union slot; every lane stores it)
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const bool dyn = j < S::ND;
@@ -1188,7 +1197,8 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     double LAB = LAB0;
     if (dyn) {
       const double jl = junction_l(X[q.x_la + (X_RAD - X_L)], X[X_RAD + s - DYN0]);
-      if (opt.inner_length_corrections && (q.flags & SR_JUNCTION)) LAB += jl;
+      const bool use = (opt.inner_length_corrections != 0) & ((q.flags & SR_JUNCTION) != 0);
+      LAB = use ? LAB + jl : LAB;  // (a select: no branch around the radii loads)
     }
     const double G = LAB * idt + RAB;
     const double H = -uur * LAB * (TH1 / TH) - (LAB * uu) * idt + Sx;
