@@ -935,43 +935,40 @@ AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Con
     min_teeth = at_teeth ? an : min_teeth;
   };
   // Up to four constrictions in the reference's order: glottis, tongue, second tongue, lip.
-  // (Absent ones keep a dummy of their kind with valid indices; their targets are not stored.)
+  // Every step runs for every utterance (no branch: a wave serves four utterances); an absent
+  // constriction works on a stand-in section with valid indices, and the has_* flags decide
+  // what is used and stored.
   const Cons cg = Cons{S_GLOT_LO, S_GLOT_UP, S_GLOT_UP, VOCAL_FOLDS, 1.5, 0.0};
-  Cons ct1 = Cons{S_GLOT_UP, S_GLOT_UP, S_GLOT_UP, TONGUE, 1.5, 0.0}, ct2 = ct1;
-  Cons cl = Cons{S_GLOT_UP, S_GLOT_UP, S_GLOT_UP, LOWER_LIP, 1.5, 0.0};
-  bool has_t1 = false, has_t2 = false;
-  double min_teeth = 1000000.0;
   // the tongue and the lip minimum: independent scans
   const MinIdx t1 = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) { (void)m; return R.art[j] == TONGUE; });
   const MinIdx lp = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) { (void)m; return R.art[j] == LOWER_LIP; });
-  if (lp.v < 1.0) {  // the lip constriction's extent (used if it is narrower than a tongue at the teeth)
-    const int s = S_PHARYNX0 + lp.i;
-    cl = Cons{s, s, s, LOWER_LIP, 0.0, 0.0};
-    grow(cl, lp.v, LOWER_LIP);
-    cl.obst = X[X_POS + cl.last + 1 - S_PHARYNX0];
-  }
-  if (t1.v < 1.0) {
-    has_t1 = true;
-    const int s = S_PHARYNX0 + t1.i;
-    ct1 = Cons{s, s, s, TONGUE, 0.0, 0.0};
-    grow(ct1, t1.v, TONGUE);
-    tongue_obstacle(ct1, min_teeth);
-    const int pf = ct1.first, pl = ct1.last;
-    const MinIdx t2 = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) {
-      const int sm = S_PHARYNX0 + m;
-      return R.art[j] == TONGUE && (sm < pf || sm > pl);
-    });
-    x.mark(PH_C_T1);
-    if (t2.v < 1.0) {
-      const int s2 = S_PHARYNX0 + t2.i;
-      ct2 = Cons{s2, s2, s2, TONGUE, 0.0, 0.0};
-      grow(ct2, t2.v, TONGUE);
-      if (ct2.first > pl + 1 || ct2.last < pf - 1) {
-        has_t2 = true;
-        tongue_obstacle(ct2, min_teeth);
-      }
-    }
-  }
+  const bool has_lp = lp.v < 1.0, has_t1 = t1.v < 1.0;
+  // the lip constriction's extent (used if it is narrower than a tongue at the teeth)
+  const int sl = S_PHARYNX0 + (has_lp ? lp.i : 0);
+  Cons cl = Cons{sl, sl, sl, LOWER_LIP, 0.0, 0.0};
+  grow(cl, lp.v, LOWER_LIP);
+  cl.obst = X[X_POS + cl.last + 1 - S_PHARYNX0];
+  // the first tongue constriction
+  const int st1 = S_PHARYNX0 + (has_t1 ? t1.i : 0);
+  Cons ct1 = Cons{st1, st1, st1, TONGUE, 0.0, 0.0};
+  grow(ct1, t1.v, TONGUE);
+  double mt1 = 1000000.0, mt2 = 1000000.0;
+  tongue_obstacle(ct1, mt1);
+  const int pf = ct1.first, pl = ct1.last;
+  const MinIdx t2 = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) {
+    const int sm = S_PHARYNX0 + m;
+    return R.art[j] == TONGUE && (sm < pf || sm > pl);
+  });
+  x.mark(PH_C_T1);
+  // the second one (kept if it does not touch the first)
+  const bool cand_t2 = has_t1 && t2.v < 1.0;
+  const int st2 = S_PHARYNX0 + (cand_t2 ? t2.i : 0);
+  Cons ct2 = Cons{st2, st2, st2, TONGUE, 0.0, 0.0};
+  grow(ct2, t2.v, TONGUE);
+  const bool has_t2 = cand_t2 && (ct2.first > pl + 1 || ct2.last < pf - 1);
+  tongue_obstacle(ct2, mt2);
+  double min_teeth = has_t1 ? mt1 : 1000000.0;
+  min_teeth = (has_t2 && mt2 < 1000000.0) ? mt2 : min_teeth;
   x.mark(PH_C_T2);
   const bool has_l = lp.v < 1.0 && lp.v < min_teeth;
   x.mark(PH_C_LIP);
