@@ -1052,10 +1052,11 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
   consume(0, avail);  // (with avail == 0 it adds nothing)
   int head = head0;
   constexpr int RJ = rng_lanes<W>(), RNG_BLOCK = 3 * RJ;
-  while (avail < need) {
-    // Block of 3 RJ values = the next 10 of each residue chain c (i = head + 3j + c):
-    // r_{head+3j+c} = r_{head+c-3} + sum_{t<=j} r_{head+3t+c-31}, an inclusive prefix sum
-    // over the lanes j = 0..9 of history values.
+  // One block of 3 RJ values = the next 10 of each residue chain c (i = head + 3j + c):
+  // r_{head+3j+c} = r_{head+c-3} + sum_{t<=j} r_{head+3t+c-31}, an inclusive prefix sum over
+  // the lanes j = 0..9 of history values.  gen == false (per utterance): everything is
+  // evaluated, the stores go to a sink and nothing advances.
+  auto block = [&](bool gen) {
     const uint32_t b0 = g[RNG_R + ((head - 3) & (RNG_RING - 1))], b1 = g[RNG_R + ((head - 2) & (RNG_RING - 1))],
                    b2 = g[RNG_R + ((head - 1) & (RNG_RING - 1))], sb = g[RNG_S + ((head - 1) & (RNG_RING - 1))];
     x.template scan_add<3>(
@@ -1067,7 +1068,7 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
           return v;
         },
         [&](int gl, Lane<W> &R, const U4 &p) {
-          const bool on = gl < RJ;  // lanes past RJ store into a sink
+          const bool on = gen && gl < RJ;  // the others store into a sink
           uint32_t *sink = (uint32_t *)(X + X_ACT + 8);
           const uint32_t n0 = b0 + p.v[0], n1 = b1 + p.v[1], n2 = b2 + p.v[2];
           *(on ? &g[RNG_R + ((head + 3 * gl) & (RNG_RING - 1))] : sink) = n0;
@@ -1084,7 +1085,7 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
           return v;
         },
         [&](int gl, Lane<W> &R, const U4 &p) {
-          const bool on = gl < RJ;
+          const bool on = gen && gl < RJ;
           uint32_t *sink = (uint32_t *)(X + X_ACT + 8);
           const uint32_t s2 = sb + p.v[0], s1 = s2 - R.rtmp[2], s0 = s1 - R.rtmp[1];
           *(on ? &g[RNG_S + ((head + 3 * gl) & (RNG_RING - 1))] : sink) = s0;
@@ -1092,10 +1093,14 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
           *(on ? &g[RNG_S + ((head + 3 * gl + 2) & (RNG_RING - 1))] : sink) = s2;
         });
     x.sync();
-    consume(avail, avail + RNG_BLOCK);
-    avail += RNG_BLOCK;
-    head = (head + RNG_BLOCK) & (RNG_RING - 1);
-  }
+    consume(avail, gen ? avail + RNG_BLOCK : avail);
+    avail += gen ? RNG_BLOCK : 0;
+    head = gen ? (head + RNG_BLOCK) & (RNG_RING - 1) : head;
+  };
+  // the first block as straight-line code (most samples of a wave need one in some
+  // utterance), further ones in a loop (three or more active sources)
+  block(avail < need);
+  while (avail < need) block(true);
   x.sync();
   x.mark(PH_N_RNG);
   // (every lane stores the same ring head / pending count; the shaping filter is branch-free
