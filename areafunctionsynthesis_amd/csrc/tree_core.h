@@ -639,7 +639,7 @@ AFS_HD inline void phase_positions(double *X) {
   }
 }
 
-template <int W>
+template <int W, bool VARLOSS>
 AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C, const GlotOut &go) {
   // One branch-free block over the lane's slots (absent slots compute on a valid section and
   // store into the sinks), so that the scheduler interleaves the slots' reciprocal and square
@@ -655,6 +655,27 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     const double E = C.stat[static_index(s)][ST_E];
     const double beta = static_beta<W>(R, jj, U, C, s);
     X[X_D + (s0 < 0 ? NS : s)] = R.p[jj] + C.h.dtTH1 * R.pr[jj] - E * (beta - 0.0);  // (E: a table constant)
+  }
+  // Glottal entrance and transition terms of section 23 (TdsModel.cpp:898-950) with the
+  // standard / van den Berg entrance loss: lane-uniform inputs (the flows into 23 and 24 are the
+  // previous solution, the areas the glottis values), so every lane computes them inside the
+  // block and slot 0 of lane 0 adds them; only lane 0 stores the separation state (the others
+  // store into a sink).  The variable (Fulcher) loss keeps its lane-0 block after the loop.
+  double dR0g = 0.0, dR1g = 0.0;
+  bool on0 = false, on1 = false;
+  if constexpr (!VARLOSS) {
+    const double kent = opt.glottis_loss == AFS_ENTRANCE_LOSS_VAN_DEN_BERG ? 1.375 : 1.0;
+    double u23 = 0.0, u24 = 0.0;
+    u23 += X[X_U + S_GLOT_LO];
+    u24 += X[X_U + S_GLOT_UP];
+    const double sa = C.h.area_last_trachea;
+    dR0g = kent * 0.5 * RHO * fabs(u23) * (fast_rcp(go.a0 * go.a0) - fast_rcp(sa * sa));
+    const double bt = (go.a1 < opt.flow_separation_area_ratio * go.a0) ? 1.0 : 0.0;
+    const double gsep = 0.8 * X[X_GBF] + (1.0 - 0.8) * bt;
+    X[gl == 0 ? X_GBF : X_ACT + 3] = gsep;
+    dR1g = gsep * fabs(u24) * 0.5 * RHO * (fast_rcp(go.a1 * go.a1) - fast_rcp(go.a0 * go.a0));
+    on0 = u23 > 0;
+    on1 = u24 > 0;
   }
   double R0g = 0.0, R1g = 0.0, Eg[S::ND], betag[S::ND];
 #pragma unroll
@@ -728,7 +749,15 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
       X[own ? X_RRAD : X_ACT] = Rrad;
       X[own ? X_RRAD + 1 : X_ACT + 1] = Lrad;
     }
-    if (j == 0) { R0g = R0; R1g = R1; }
+    if (j == 0) {
+      if constexpr (VARLOSS) {
+        R0g = R0; R1g = R1;
+      } else {  // section 23: the glottal entrance / transition terms
+        const bool glo = s == S_GLOT_LO;
+        R0 = (glo & on0) ? R0 + dR0g : R0;
+        R1 = (glo & on1) ? R1 + dR1g : R1;
+      }
+    }
     Eg[j] = E;
     betag[j] = beta;
     R.al[j] = alpha;
@@ -740,7 +769,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     X[X_R0 + ks] = R0;
     X[X_R1 + ks] = R1;
   }
-  if (gl == S_GLOT_LO - DYN0) {  // glottal entrance and transition (TdsModel.cpp:898-950), slot 0
+  if (VARLOSS && gl == S_GLOT_LO - DYN0) {  // glottal entrance and transition (TdsModel.cpp:898-950), slot 0
     const double area = go.a0;
     double R0 = R0g, R1 = R1g;
     double kent = 1.0;
@@ -1395,9 +1424,13 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const int s = slot_section<W>(j, gl);
-    if (U.opt.transvelar_coupling) {
-      if (s == S_MOUTH0 + 2) Xw[X_TVP] = R.p[j];
-      if (s == S_NOSE0 + 2) Xw[X_TVP + 1] = R.p[j];
+    // transvelar filter inputs p[43], p[67]: only the slots that can hold sections 43 / 67
+    // store, a lane without them into the sink (no branch)
+    constexpr int J43 = (S_MOUTH0 + 2 - DYN0) / W, J67 = (S_NOSE0 + 2 - DYN0) / W;
+    if (j == J43 || j == J67) {
+      const bool tv = U.opt.transvelar_coupling != 0;
+      const int dst = (tv & (s == S_MOUTH0 + 2)) ? X_TVP : (tv & (s == S_NOSE0 + 2)) ? X_TVP + 1 : X_U + U_SINK;
+      Xw[dst] = R.p[j];
     }
     constexpr int J64 = (S_LAST_MOUTH - DYN0) / W, J83 = S::ND + (S_LAST_NOSE - 46) / W;
     if ((j == J64 || j == J83) && (rec[j].flags & SR_RADIATION)) {  // the two radiation currents of s = 64 / 83
@@ -1511,13 +1544,13 @@ AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, doub
 // One audio sample.  Xc: execution policy (par / one / lanes / sync).
 // ---------------------------------------------------------------------------
 
-template <int W, int MODEL, class Xc>
+template <int W, int MODEL, bool VARLOSS, class Xc>
 AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
   GlotOut go{};
   x.par_uniform([&](int gl, Lane<W> &R) { phase_interpolate<W>(gl, R, X, C, ratio); },
                 [&](Lane<W> &R) { (void)R; go = phase_glottis<MODEL>(X, C, ratio); });
   x.dyn_neighbors();
-  x.par([&](int gl, Lane<W> &R) { phase_network<W>(gl, R, X, U, C, go); });
+  x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS>(gl, R, X, U, C, go); });
 }
 
 template <int W, class Xc>
@@ -1526,8 +1559,16 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   // geometry and network in one block (no LDS round trip between them): the interpolated
   // areas stay in the lanes, the neighbours' come by lane exchange, the glottis values are
   // lane-uniform
-  if (U.opt.glottis_model == AFS_GLOTTIS_TWO_MASS) geometry_network<W, AFS_GLOTTIS_TWO_MASS>(x, X, U, C, ratio);
-  else geometry_network<W, AFS_GLOTTIS_TRIANGULAR>(x, X, U, C, ratio);
+  // (one instantiation per glottis model and entrance-loss kind: no option branch in the block)
+  const bool two_mass = U.opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
+  const bool varloss = U.opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE;
+  if (two_mass) {
+    if (varloss) geometry_network<W, AFS_GLOTTIS_TWO_MASS, true>(x, X, U, C, ratio);
+    else geometry_network<W, AFS_GLOTTIS_TWO_MASS, false>(x, X, U, C, ratio);
+  } else {
+    if (varloss) geometry_network<W, AFS_GLOTTIS_TRIANGULAR, true>(x, X, U, C, ratio);
+    else geometry_network<W, AFS_GLOTTIS_TRIANGULAR, false>(x, X, U, C, ratio);
+  }
   x.sync();
   x.mark(PH_GEOMETRY);
   x.mark(PH_NETWORK);
