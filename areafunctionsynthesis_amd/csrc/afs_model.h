@@ -122,16 +122,18 @@ struct alignas(8) Topo {
 //   update: x_o0/x_o1 = flows of the output currents; x_ur/x_un/x_p4 = where d/dt and the
 //           noise-smoothed value of the in-current and the pressure are published.
 enum : uint16_t { SR_BIF = 1, SR_JUNCTION = 2, SR_RADIATION = 4 };
+// (The x_* fields are LDS byte offsets into the utterance block: the kernel adds them to the
+// block's address with one instruction, sub-dword operand select included.)
 struct alignas(16) SecRec {
   double c_la, c_ra, c_ea;
-  int16_t x_la, x_ra, x_ea, x_da, x_ub, x_urb, x_sx, x_e0, x_e1, x_e2;
-  int16_t x_o0, x_o1, x_ur, x_un, x_p4;
+  uint16_t x_la, x_ra, x_ea, x_da, x_ub, x_urb, x_sx, x_e0, x_e1, x_e2;
+  uint16_t x_o0, x_o1, x_ur, x_un, x_p4;
   uint16_t flags;
   // constriction phase: the noise-smoothed flows of the section's outputs (X_UN, or zero)
-  int16_t x_uo0, x_uo1;
+  uint16_t x_uo0, x_uo1;
   // radiation sections (SR_RADIATION): flow, d/dt and noise-smoothed flow of the two
   // radiation currents (X_U + rc, X_U + lc, X_UR.., X_UR.., X_UN.., X_UN..)
-  int16_t x_rad[6];
+  uint16_t x_rad[6];
   // (80-byte stride: the 16 sections a 16-lane ds_read_b128 group reads start on 16 distinct
   // 16-byte bank slots; at 64 bytes, sections s and s+4 share banks: 4-way conflicts)
 };

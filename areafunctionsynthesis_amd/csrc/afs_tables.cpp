@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <initializer_list>
 #include <vector>
 
 #include "afs_model.h"
@@ -503,6 +504,11 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
     q.flags = (uint16_t)((br >= 0 ? SR_BIF : 0) |
                          (real && a >= S_PHARYNX0 && s <= S_LAST_MOUTH ? SR_JUNCTION : 0) |
                          (s == S_LAST_MOUTH || s == S_LAST_NOSE ? SR_RADIATION : 0));
+    // block slots -> LDS byte offsets
+    for (uint16_t *f : {&q.x_la, &q.x_ra, &q.x_ea, &q.x_da, &q.x_ub, &q.x_urb, &q.x_sx, &q.x_e0, &q.x_e1,
+                        &q.x_e2, &q.x_o0, &q.x_o1, &q.x_ur, &q.x_un, &q.x_p4, &q.x_uo0, &q.x_uo1})
+      *f = (uint16_t)(*f * 8);
+    for (int k = 0; k < 6; ++k) q.x_rad[k] = (uint16_t)(q.x_rad[k] * 8);
   }
   for (int k = 0; k < NSTATIC; ++k) {
     int s = k < 23 ? k : k + 46;

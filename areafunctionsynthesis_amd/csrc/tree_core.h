@@ -189,6 +189,12 @@ AFS_HD inline double fast_div(double a, double b) {
 #endif
 }
 
+// The double at LDS byte offset b of an utterance block (SecRec / StepRec fields).
+AFS_HD inline double &xat(double *X, uint32_t b) { return *reinterpret_cast<double *>(reinterpret_cast<char *>(X) + b); }
+AFS_HD inline const double &xat(const double *X, uint32_t b) {
+  return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(X) + b);
+}
+
 // Lane registers.
 // Only the persistent state and the frame cache live here; per-sample intermediates
 // go through the LDS block or are recomputed from unchanged state.
@@ -886,8 +892,8 @@ AFS_HD inline DipTarget dipole_target(const double *X, const Consts &C, double t
   const double inv_A = fast_rcp(A);
   double flow = 0.0;
   const SecRec &q = C.sec[c.narrow];  // (an absent output reads the zero slot)
-  flow += X[q.x_uo0];
-  flow += X[q.x_uo1];
+  flow += xat(X, q.x_uo0);
+  flow += xat(X, q.x_uo1);
   if (flow < 0.0) flow = 0.0;
   double v = flow * inv_A;
   double fc = 6000.0, gain = 0.0;
@@ -1212,14 +1218,14 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     const double EB = dyn ? X[X_E + s - DYN0] : ks[ST_E], DB = X[X_D + s];
     // source section a: a static source's constants come from the record, a dynamic one's
     // from X (the other term is an exact 0.0; no source: both are)
-    const double LA = q.c_la + X[q.x_la], RA = q.c_ra + X[q.x_ra], EA = q.c_ea + X[q.x_ea];
-    const double DA = X[q.x_da];
+    const double LA = q.c_la + xat(X, q.x_la), RA = q.c_ra + xat(X, q.x_ra), EA = q.c_ea + xat(X, q.x_ea);
+    const double DA = xat(X, q.x_da);
     const double LAB0 = LA + LB, RAB = RA + RB;
     double Sx = 0.0;
-    Sx -= X[q.x_sx];  // dipole sample (pharynx/mouth) or the lung pressure (section 0)
+    Sx -= xat(X, q.x_sx);  // dipole sample (pharynx/mouth) or the lung pressure (section 0)
     const double uu = R.u[j], uur = R.ur[j];
     // the source section bifurcates: its other output is current br
-    const double uD = X[q.x_ub], uDr = X[q.x_urb];
+    const double uD = xat(X, q.x_ub), uDr = xat(X, q.x_urb);
     const double Fb = LAB0 * idt + RAB;
     const double Hb = -idt * (LAB0 * uu + LA * uD) - (TH1 / TH) * (LAB0 * uur + LA * uDr) + Sx;
     const double mb = -EB - EA - Fb;
@@ -1227,7 +1233,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     // simple junction, with Sondhi's inner length correction between pharynx/mouth sections
     double LAB = LAB0;
     if (dyn) {
-      const double jl = junction_l(X[q.x_la + (X_RAD - X_L)], X[X_RAD + s - DYN0]);
+      const double jl = junction_l(xat(X, q.x_la + (X_RAD - X_L) * 8), X[X_RAD + s - DYN0]);
       const bool use = (opt.inner_length_corrections != 0) & ((q.flags & SR_JUNCTION) != 0);
       LAB = use ? LAB + jl : LAB;  // (a select: no branch around the radii loads)
     }
@@ -1241,9 +1247,9 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     Xw[X_DIAG + i] = -(bif ? mb : m);
     Xw[X_RHS + i] = -(bif ? rb : rhs);
     // edges of section s: (in, out0) = -E, (in, out1) = -E, (out0, out1) = E + L/(dt th) + R1
-    Xw[q.x_e0] = -EB;
-    Xw[q.x_e1] = -EB;
-    Xw[q.x_e2] = -(-EB - (LB * idt + R1B));
+    xat(Xw, q.x_e0) = -EB;
+    xat(Xw, q.x_e1) = -EB;
+    xat(Xw, q.x_e2) = -(-EB - (LB * idt + R1B));
   }
   constexpr int J64 = (S_LAST_MOUTH - DYN0) / W, J83 = S::ND + (S_LAST_NOSE - 46) / W;
 #pragma unroll
@@ -1258,11 +1264,11 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
     const double AB = dyn ? X[X_AREA + s - DYN0] : C.h.area_last_nose;
     const double EB = dyn ? X[X_E + s - DYN0] : ks[ST_E], DB = X[X_D + s];
-    const SecRec &q = rec[j];  // rc = q.x_rad[0] - X_U, lc = q.x_rad[1] - X_U
-    const int rc = q.x_rad[0] - X_U, lc = q.x_rad[1] - X_U;
-    double uR = X[q.x_rad[0]], uL = X[q.x_rad[1]], uRr = X[q.x_rad[2]], uLr = X[q.x_rad[3]];
+    const SecRec &q = rec[j];
+    const int rc = q.x_rad[0] / 8 - X_U, lc = q.x_rad[1] / 8 - X_U;
+    double uR = xat(X, q.x_rad[0]), uL = xat(X, q.x_rad[1]), uRr = xat(X, q.x_rad[2]), uLr = xat(X, q.x_rad[3]);
     R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
-    R.rad_un[0] = X[q.x_rad[4]]; R.rad_un[1] = X[q.x_rad[5]];
+    R.rad_un[0] = xat(X, q.x_rad[4]); R.rad_un[1] = xat(X, q.x_rad[5]);
     const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
     (void)AB;
     {
@@ -1399,8 +1405,8 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
     double cin = 0.0;
     cin += unew;
     double cout = 0.0;
-    cout += X[q.x_o0];  // 0.0 for an absent output
-    cout += X[q.x_o1];
+    cout += xat(X, q.x_o0);  // 0.0 for an absent output
+    cout += xat(X, q.x_o1);
     double net = cin - cout;
     double old = R.p[j];
     double p = X[X_D + s] + (j < S::ND ? X[X_E + s - DYN0] : C.stat[static_index(s)][ST_E]) * net;
@@ -1417,9 +1423,9 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
   // publish (all stores after all loads: the scheduler may batch the loads of every slot)
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
-    Xw[rec[j].x_ur] = R.ur[j];  // for the bifurcation partner (or the sink)
-    Xw[rec[j].x_un] = R.un[j];  // for the noise sources (or the sink)
-    Xw[rec[j].x_p4] = R.p[j];   // p[22..25] for the glottis (or the sink)
+    xat(Xw, rec[j].x_ur) = R.ur[j];  // for the bifurcation partner (or the sink)
+    xat(Xw, rec[j].x_un) = R.un[j];  // for the noise sources (or the sink)
+    xat(Xw, rec[j].x_p4) = R.p[j];   // p[22..25] for the glottis (or the sink)
   }
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
@@ -1436,10 +1442,10 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
     if ((j == J64 || j == J83) && (rec[j].flags & SR_RADIATION)) {  // the two radiation currents of s = 64 / 83
       const SecRec &q = rec[j];
       for (int k = 0; k < 2; ++k) {
-        double un = X[q.x_rad[k]];
+        double un = xat(X, q.x_rad[k]);
         double ur = (un - R.rad_u[k]) * idt - (TH1 / TH) * R.rad_ur[k];
-        Xw[q.x_rad[2 + k]] = ur;
-        Xw[q.x_rad[4 + k]] = (1.0 - c) * un + c * R.rad_un[k];
+        xat(Xw, q.x_rad[2 + k]) = ur;
+        xat(Xw, q.x_rad[4 + k]) = (1.0 - c) * un + c * R.rad_un[k];
       }
     }
   }
@@ -1452,8 +1458,8 @@ AFS_HD inline double section_pressure(const double *X, const Consts &C, int s) {
   double cin = 0.0;
   cin += X[X_U + s];
   double cout = 0.0;
-  cout += X[q.x_o0];
-  cout += X[q.x_o1];
+  cout += xat(X, q.x_o0);
+  cout += xat(X, q.x_o1);
   const double net = cin - cout;
   return X[X_D + s] + X[X_E + s - DYN0] * net;
 }
