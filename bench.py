@@ -29,10 +29,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters (spec)
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (spec)
 # fp64 lane-flops per utterance-sample executed by the tree kernel, counted on the GPU:
-# SQ_INSTS_VALU_FLOPS_FP64 counts flops per wave-instruction (2057.5 per wave-sample), x 64 lanes
-# / 4 utterances per wave (profiles/r01_pmc_sq_v2n.txt).  Lane-uniform work (glottis, output
+# SQ_INSTS_VALU_FLOPS_FP64 counts flops per wave-instruction (2050.3 per wave-sample), x 64 lanes
+# / 4 utterances per wave (profiles/r01_pmc_sq_v2p.txt).  Lane-uniform work (glottis, output
 # stage) is counted on every lane.  (SURVEY.md 8(a)'s 1.8e4 is the reference algorithm's count.)
-FLOPS_PER_SAMPLE = 32920.0
+FLOPS_PER_SAMPLE = 32805.0
 
 
 def pmc_traffic(kernel: str, workload: str, batch: int, samples: int, hop: int):
