@@ -27,7 +27,7 @@ EXPORTED = (
     "afs_last_error", "afs_set_stream", "afs_synchronize", "afs_synthesize",
     "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_session_destroy",
     "afs_af_to_frames", "afs_to_int16", "afs_target_sequence_default", "afs_target_sequence_samples",
-    "afs_play_target_sequences",
+    "afs_play_target_sequences", "afs_rng_draws", "afs_session_rng_draws",
 )
 
 
@@ -85,10 +85,12 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.afs_last_error.argtypes = [vp]
     lib.afs_set_stream.argtypes = [vp, vp]
     lib.afs_synchronize.argtypes = [vp]
-    lib.afs_synthesize.argtypes = [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp,
+    lib.afs_synthesize.argtypes = [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp,
                                    ctypes.POINTER(AfsReport)]
+    lib.afs_rng_draws.argtypes = [vp, ctypes.c_int32, vp]
+    lib.afs_session_rng_draws.argtypes = [vp, vp]
     lib.afs_session_create.argtypes = [vp, ctypes.c_int32, vp, ctypes.POINTER(vp)]
-    lib.afs_session_synthesize.argtypes = [vp, vp, ctypes.c_int32, vp, ctypes.POINTER(ctypes.c_int32),
+    lib.afs_session_synthesize.argtypes = [vp, vp, ctypes.c_int32, vp, vp, ctypes.POINTER(ctypes.c_int32),
                                            ctypes.POINTER(AfsReport)]
     lib.afs_session_reset.argtypes = [vp, vp]
     lib.afs_session_destroy.argtypes = [vp]
@@ -99,10 +101,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.afs_target_sequence_samples.argtypes = [ctypes.POINTER(AfsTargetSequence), ctypes.c_double]
     lib.afs_target_sequence_samples.restype = ctypes.c_int64
     lib.afs_play_target_sequences.argtypes = [vp, vp, ctypes.c_int32, vp, ctypes.POINTER(AfsTargetSequence), vp,
-                                              ctypes.c_int32, vp, ctypes.POINTER(AfsReport)]
+                                              ctypes.c_int32, vp, vp, ctypes.POINTER(AfsReport)]
     for name in ("afs_create", "afs_set_stream", "afs_synchronize", "afs_synthesize",
                  "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_af_to_frames",
-                 "afs_to_int16", "afs_play_target_sequences"):
+                 "afs_to_int16", "afs_play_target_sequences", "afs_rng_draws", "afs_session_rng_draws"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib

@@ -15,7 +15,7 @@ LIB = os.path.join(HERE, "libafs.so")
 ARCH = os.environ.get("AFS_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["afs_capi.cpp", "afs_tables.cpp", "tds_lane.hip", "tds_tree.hip", "af_kernels.hip", "audio_kernels.hip"]
-HEADERS = ["afs_model.h", "afs_af.h", "afs_lane.h", "afs_tree.h", "afs_audio.h", "tree_core.h", "tree_kernel.h",
+HEADERS = ["afs_model.h", "afs_af.h", "afs_lane.h", "afs_tree.h", "afs_audio.h", "tree_core.h", "tree_plan.h", "tree_kernel.h",
            os.path.join("..", "..", "include", "afs.h")]
 # Per-source extra flags.  (Contracting a*b+c in the tree kernel was measured: ~1 % faster,
 # and it moves some chaotic utterances past the 1e-9 parity bound -- not used.)

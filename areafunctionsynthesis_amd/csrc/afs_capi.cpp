@@ -44,7 +44,13 @@ struct afs_ctx {
   size_t stage_seeds_bytes = 0;
   void *tgt = nullptr;  // target sequences: shape rows [Q][4][16] then frame_row [B]
   size_t tgt_bytes = 0;
+  void *plan = nullptr;   // tree solver: noise-source plans of one launch (tree_plan.h)
+  size_t plan_bytes = 0;
+  void *stage_nf = nullptr;  // per-utterance non-finite flags staged for a host array
+  size_t stage_nf_bytes = 0;
+  int32_t last_B = 0;        // batch of the last whole-trajectory call (afs_rng_draws)
   int32_t *dcount = nullptr;
+  int32_t *hcount = nullptr;  // pinned host copy of dcount
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -107,24 +113,39 @@ bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_T
 
 bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE; }
 
-// Launch the synthesis for frame transitions [k0, k1) in chunks that keep each kernel
-// well below a second (state is carried between launches).
-afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int k0, int k1, int hop,
+// Bytes of noise-source plans one tree launch may use; a launch covers at most
+// PLAN_BUDGET / (rows * 128 B) samples (4096 samples at 8192 rows).
+constexpr int64_t PLAN_BUDGET = (int64_t)4 << 30;
+
+// Launch the synthesis of frame transitions 1 .. ntrans (frames[row * fstride + k], k = 0 the
+// latched frame) in chunks that keep each kernel well below a second; state is carried
+// between launches.  rows: number of distinct frame rows (B, or the target sequences).
+afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int rows, int ntrans, int hop,
                       double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B,
                       const int32_t *frame_row = nullptr) {
-  const int64_t max_samples = tree(c) ? 65536 : 8192;
-  int per = (int)std::max<int64_t>(1, max_samples / std::max(1, hop));
-  for (int k = k0; k < k1; k += per) {
-    int ke = std::min(k1, k + per);
-    double *o = out + (int64_t)(k - k0) * hop;
-    if (tree(c)) {
-      afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, k, ke, hop, o, ostride, lanes, (double *)ws, B, c->host_tab.uni};
+  if (tree(c)) {
+    const int64_t S = (int64_t)ntrans * hop;
+    const int64_t per = std::max<int64_t>(1, std::min<int64_t>({S, 65536, PLAN_BUDGET / ((int64_t)rows * afs::PLAN_RECORD_BYTES)}));
+    afs_status st = ensure(c, &c->plan, &c->plan_bytes, (size_t)rows * (size_t)per * afs::PLAN_RECORD_BYTES);
+    if (st != AFS_OK) return st;
+    for (int64_t s0 = 0; s0 < S; s0 += per) {
+      const int64_t s1 = std::min(S, s0 + per);
+      afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)c->plan, per,
+                       c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0};
+      HIP_TRY(c, afs::launch_plan(pa, c->stream));
+      afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
+                      (const uint64_t *)c->plan, per, lanes, (double *)ws, B, c->host_tab.uni};
       HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
-    } else {
-      afs::LaneArgs a{c->dev_tab, frames, fstride, frame_row, k, ke, hop, o, ostride, (double *)ws, rng, bp, B,
-                      c->cfg.solver == AFS_SOLVER_SOR ? 1 : 0};
-      HIP_TRY(c, afs::launch_lane_synth(a, c->stream));
     }
+    return AFS_OK;
+  }
+  const int per = (int)std::max<int64_t>(1, 8192 / std::max(1, hop));
+  for (int k = 1; k <= ntrans; k += per) {
+    const int ke = std::min(ntrans + 1, k + per);
+    double *o = out + (int64_t)(k - 1) * hop;
+    afs::LaneArgs a{c->dev_tab, frames, fstride, frame_row, k, ke, hop, o, ostride, (double *)ws, rng, bp, B,
+                    c->cfg.solver == AFS_SOLVER_SOR ? 1 : 0};
+    HIP_TRY(c, afs::launch_lane_synth(a, c->stream));
   }
   return AFS_OK;
 }
@@ -146,13 +167,43 @@ afs_status reset_state(afs_ctx *c, void *ws, int32_t *rng, void *lanes, int64_t 
   return AFS_OK;
 }
 
-afs_status count_nonfinite(afs_ctx *c, void *ws, int64_t bp, int B, int32_t *out) {
+// Per-utterance non-finite flags (into `flags`, a host or device array of B bytes, or nowhere)
+// and their count (into the pinned c->hcount, read after the stream synchronises).  *host_sync
+// is set when the flags go to host memory (the call must synchronise before returning).
+afs_status nonfinite_report(afs_ctx *c, void *ws, int64_t bp, int B, uint8_t *flags, bool want_count,
+                            bool *host_sync) {
+  *host_sync = false;
+  if (!flags && !want_count) return AFS_OK;
+  uint8_t *dflags = flags;
+  if (flags && !is_device_ptr(flags)) {
+    afs_status s = ensure(c, &c->stage_nf, &c->stage_nf_bytes, (size_t)B);
+    if (s != AFS_OK) return s;
+    dflags = (uint8_t *)c->stage_nf;
+    *host_sync = true;
+  }
   HIP_TRY(c, hipMemsetAsync(c->dcount, 0, sizeof(int32_t), c->stream));
   if (tree(c))
-    HIP_TRY(c, afs::launch_tree_nonfinite((const double *)ws, B, c->dcount, c->stream));
+    HIP_TRY(c, afs::launch_tree_nonfinite((const double *)ws, B, c->dcount, dflags, c->stream));
   else
-    HIP_TRY(c, afs::launch_lane_nonfinite((const double *)ws, bp, B, c->dcount, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(out, c->dcount, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, afs::launch_lane_nonfinite((const double *)ws, bp, B, c->dcount, dflags, c->stream));
+  if (*host_sync) HIP_TRY(c, hipMemcpyAsync(flags, dflags, (size_t)B, hipMemcpyDeviceToHost, c->stream));
+  if (want_count) HIP_TRY(c, hipMemcpyAsync(c->hcount, c->dcount, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  return AFS_OK;
+}
+
+afs_status draws_of(afs_ctx *c, const void *ws, int B, int64_t *draws) {
+  if (!tree(c)) return fail(c, AFS_ERR_UNSUPPORTED, "rand() call counts are kept by the tree solver only");
+  int64_t *d = draws;
+  void *tmp = nullptr;
+  if (!is_device_ptr(draws)) {
+    HIP_TRY(c, hipMalloc(&tmp, (size_t)B * sizeof(int64_t)));
+    d = (int64_t *)tmp;
+  }
+  hipError_t e = afs::launch_tree_draws((const double *)ws, B, d, c->stream);
+  if (e == hipSuccess && tmp) e = hipMemcpyAsync(draws, d, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (tmp) (void)hipFree(tmp);
+  if (e != hipSuccess) return fail(c, AFS_ERR_HIP, "afs_rng_draws: %s", hipGetErrorString(e));
   return AFS_OK;
 }
 
@@ -209,6 +260,9 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   if (hipMemcpy(ctx->dev_tab, &ctx->host_tab, sizeof(afs::Tables), hipMemcpyHostToDevice) != hipSuccess)
     return bail(AFS_ERR_HIP);
   if (hipMalloc((void **)&ctx->dcount, sizeof(int32_t)) != hipSuccess) return bail(AFS_ERR_OUT_OF_MEMORY);
+  if (hipHostMalloc((void **)&ctx->hcount, sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
+    return bail(AFS_ERR_OUT_OF_MEMORY);
+  *ctx->hcount = 0;
   if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return bail(AFS_ERR_HIP);
   (void)st;
   *out = ctx;
@@ -226,7 +280,10 @@ void afs_destroy(afs_ctx *c) {
   if (c->stage_out) (void)hipFree(c->stage_out);
   if (c->stage_seeds) (void)hipFree(c->stage_seeds);
   if (c->tgt) (void)hipFree(c->tgt);
+  if (c->plan) (void)hipFree(c->plan);
+  if (c->stage_nf) (void)hipFree(c->stage_nf);
   if (c->dcount) (void)hipFree(c->dcount);
+  if (c->hcount) (void)hipHostFree(c->hcount);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -247,7 +304,7 @@ afs_status afs_synchronize(afs_ctx *c) {
 }
 
 afs_status afs_synthesize(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B,
-                          int32_t F, int32_t hop, double *out, afs_report *rep) {
+                          int32_t F, int32_t hop, double *out, uint8_t *nonfinite, afs_report *rep) {
   if (!c) return AFS_ERR_INVALID_ARGUMENT;
   if (!frames || !out || B <= 0 || F < 2 || hop < 1)
     return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_synthesize: need frames, out, batch>0, num_frames>=2, hop>=1");
@@ -281,22 +338,32 @@ afs_status afs_synthesize(afs_ctx *c, const afs_frame *frames, const uint32_t *s
   if (tree(c) && (s = ensure(c, &c->tree_lanes, &c->tree_lanes_bytes, lanes_bytes_for(c, bp))) != AFS_OK) return s;
   if ((s = reset_state(c, c->ws, c->rng, c->tree_lanes, bp, B, dseeds)) != AFS_OK) return s;
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-  if ((s = run_chunks(c, dframes, F, 1, F, hop, dout, T, c->ws, c->rng, c->tree_lanes, bp, B)) != AFS_OK) return s;
+  if ((s = run_chunks(c, dframes, F, B, F - 1, hop, dout, T, c->ws, c->rng, c->tree_lanes, bp, B)) != AFS_OK)
+    return s;
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
-  int32_t nonfinite = 0;
-  if ((s = count_nonfinite(c, c->ws, bp, B, &nonfinite)) != AFS_OK) return s;
+  c->last_B = B;
+  bool nf_sync = false;
+  if ((s = nonfinite_report(c, c->ws, bp, B, nonfinite, rep != nullptr, &nf_sync)) != AFS_OK) return s;
   if (host_out) HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)B * T * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  const bool sync = !(c->cfg.flags & AFS_ASYNC) || host_out || rep;
+  const bool sync = !(c->cfg.flags & AFS_ASYNC) || host_out || rep || nf_sync;
   if (sync) HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (rep) {
     float ms = 0.f;
     HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
     rep->device_ms = ms;
     rep->samples = (int64_t)B * T;
-    rep->nonfinite_utterances = nonfinite;
+    rep->nonfinite_utterances = *c->hcount;
     rep->kernel = c->cfg.solver;
   }
   return AFS_OK;
+}
+
+afs_status afs_rng_draws(afs_ctx *c, int32_t B, int64_t *draws) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (!draws || B <= 0 || B != c->last_B || !c->ws)
+    return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_rng_draws: need draws[B] with B = the last call's batch");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  return draws_of(c, c->ws, B, draws);
 }
 
 afs_status afs_session_create(afs_ctx *c, int32_t B, const uint32_t *seeds, afs_session **out) {
@@ -332,10 +399,9 @@ afs_status afs_session_reset(afs_session *s, const uint32_t *seeds) {
   if (seeds) {
     hipMemcpyKind k = is_device_ptr(seeds) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     HIP_TRY(c, hipMemcpyAsync(s->seeds, seeds, (size_t)s->B * 4, k, c->stream));
-  } else {
-    HIP_TRY(c, hipMemsetAsync(s->seeds, 0, (size_t)s->B * 4, c->stream));
   }
-  afs_status st = reset_state(c, s->ws, s->rng, s->tree_lanes, s->bp, s->B, s->seeds);
+  // (no seeds: the reset kernels seed voice u with u + 1)
+  afs_status st = reset_state(c, s->ws, s->rng, s->tree_lanes, s->bp, s->B, seeds ? s->seeds : nullptr);
   if (st != AFS_OK) return st;
   s->latched = false;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -353,7 +419,7 @@ void afs_session_destroy(afs_session *s) {
 }
 
 afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32_t n, double *out,
-                                  int32_t *produced, afs_report *rep) {
+                                  uint8_t *nonfinite, int32_t *produced, afs_report *rep) {
   if (!s || !frames) return AFS_ERR_INVALID_ARGUMENT;
   afs_ctx *c = s->ctx;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
@@ -380,13 +446,13 @@ afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32
     dout = (double *)c->stage_out;
   }
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-  if ((st = run_chunks(c, s->pair, 2, 1, 2, n, dout, n, s->ws, s->rng, s->tree_lanes, s->bp, B)) != AFS_OK) return st;
+  if ((st = run_chunks(c, s->pair, 2, B, 1, n, dout, n, s->ws, s->rng, s->tree_lanes, s->bp, B)) != AFS_OK) return st;
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   // prevTube = *newTube (Synthesizer.cpp:633-637)
   HIP_TRY(c, hipMemcpy2DAsync(s->pair, 2 * sizeof(afs_frame), s->pair + 1, 2 * sizeof(afs_frame),
                               sizeof(afs_frame), B, hipMemcpyDeviceToDevice, c->stream));
-  int32_t nonfinite = 0;
-  if ((st = count_nonfinite(c, s->ws, s->bp, B, &nonfinite)) != AFS_OK) return st;
+  bool nf_sync = false;
+  if ((st = nonfinite_report(c, s->ws, s->bp, B, nonfinite, rep != nullptr, &nf_sync)) != AFS_OK) return st;
   if (host_out) HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)B * n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (produced) *produced = n;
@@ -395,10 +461,17 @@ afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32
     HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
     rep->device_ms = ms;
     rep->samples = (int64_t)B * n;
-    rep->nonfinite_utterances = nonfinite;
+    rep->nonfinite_utterances = *c->hcount;
     rep->kernel = c->cfg.solver;
   }
   return AFS_OK;
+}
+
+afs_status afs_session_rng_draws(afs_session *s, int64_t *draws) {
+  if (!s || !draws) return AFS_ERR_INVALID_ARGUMENT;
+  afs_ctx *c = s->ctx;
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  return draws_of(c, s->ws, s->B, draws);
 }
 
 afs_status afs_af_to_frames(afs_ctx *c, const double *params, int64_t n, afs_frame *frames) {
@@ -492,7 +565,7 @@ int64_t afs_target_sequence_samples(const afs_target_sequence *ts, double fs) {
 
 afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t num_shapes, const int32_t *targets,
                                      const afs_target_sequence *ts, const uint32_t *seeds, int32_t B, double *out,
-                                     afs_report *rep) {
+                                     uint8_t *nonfinite, afs_report *rep) {
   if (!c) return AFS_ERR_INVALID_ARGUMENT;
   if (!shapes || num_shapes <= 0 || !targets || !ts || B <= 0 || !out)
     return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_play_target_sequences: need shapes, targets, timing, batch>0, out");
@@ -505,7 +578,13 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
     if (targets[k] < 0 || targets[k] >= num_shapes)
       return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_play_target_sequences: target %lld out of range", (long long)k);
   if (rep) std::memset(rep, 0, sizeof *rep);
-  if (T == 0) return AFS_OK;
+  if (T == 0) {
+    if (nonfinite) {
+      if (is_device_ptr(nonfinite)) HIP_TRY(c, hipMemset(nonfinite, 0, (size_t)B));
+      else std::memset(nonfinite, 0, (size_t)B);
+    }
+    return AFS_OK;
+  }
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   // one tube trajectory per distinct sequence of four shapes
   std::map<std::array<int32_t, 4>, int32_t> uniq;
@@ -569,22 +648,23 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
   for (int64_t k0 = 0; k0 < T; k0 += Tc) {
     const int nk = (int)std::min<int64_t>(Tc, T - k0);
     HIP_TRY(c, afs::launch_target_frames(dseq, Q, plan, k0, nk + 1, Tc + 1, dframes, c->stream));
-    if ((s = run_chunks(c, dframes, Tc + 1, 1, nk + 1, 1, dout + k0, T, c->ws, c->rng, c->tree_lanes, bp, B, drow)) !=
+    if ((s = run_chunks(c, dframes, Tc + 1, Q, nk, 1, dout + k0, T, c->ws, c->rng, c->tree_lanes, bp, B, drow)) !=
         AFS_OK)
       return s;
   }
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
-  int32_t nonfinite = 0;
-  if ((s = count_nonfinite(c, c->ws, bp, B, &nonfinite)) != AFS_OK) return s;
+  c->last_B = B;
+  bool nf_sync = false;
+  if ((s = nonfinite_report(c, c->ws, bp, B, nonfinite, rep != nullptr, &nf_sync)) != AFS_OK) return s;
   if (host_out) HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)B * T * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  const bool sync = !(c->cfg.flags & AFS_ASYNC) || host_out || rep;
+  const bool sync = !(c->cfg.flags & AFS_ASYNC) || host_out || rep || nf_sync;
   if (sync) HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (rep) {
     float ms = 0.f;
     HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
     rep->device_ms = ms;
     rep->samples = (int64_t)B * T;
-    rep->nonfinite_utterances = nonfinite;
+    rep->nonfinite_utterances = *c->hcount;
     rep->kernel = c->cfg.solver;
   }
   return AFS_OK;

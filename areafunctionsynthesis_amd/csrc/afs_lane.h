@@ -27,6 +27,6 @@ int64_t lane_ws_rows(const Tables &t);
 int64_t lane_persist_rows();
 hipError_t launch_lane_reset(double *ws, int32_t *rng, int64_t bp, int B, const uint32_t *seeds, hipStream_t st);
 hipError_t launch_lane_synth(const LaneArgs &a, hipStream_t st);
-hipError_t launch_lane_nonfinite(const double *ws, int64_t bp, int B, int32_t *count, hipStream_t st);
+hipError_t launch_lane_nonfinite(const double *ws, int64_t bp, int B, int32_t *count, uint8_t *flags, hipStream_t st);
 
 }  // namespace afs

@@ -7,19 +7,36 @@
 
 namespace afs {
 
+// Sample s (0-based) of a call plays frame transition k = 1 + s / hop (frames k-1, k of the
+// utterance's row) at ratio (s % hop) / hop; a launch covers samples [s_begin, s_end).
 struct TreeArgs {
   const Tables *tab;
   const afs_frame *frames;  // frames[row(u) * frame_stride + k]
   int64_t frame_stride;
   const int32_t *frame_row; // row(u) = frame_row[u], or u when null (shared trajectories)
-  int k_begin, k_end, hop;
-  double *out;              // out[u * out_stride + t]
+  int hop;
+  int64_t s_begin, s_end;
+  double *out;              // out[u * out_stride + s - s_begin]
   int64_t out_stride;
+  const uint64_t *plan;     // plan[(row(u) * plan_stride + s - s_begin) * 16 + w] (tree_plan.h)
+  int64_t plan_stride;
   void *lane_state;         // per-lane register state, B * TREE_W entries
   double *lds_state;        // per-utterance LDS block, B * tree_lds_doubles()
   int B;
   Uni uni;                  // copy of tab->uni: scalar kernel arguments
 };
+// K5: the noise-source plans of samples [s_begin, s_end) of `rows` frame rows.
+struct PlanArgs {
+  const Tables *tab;
+  const afs_frame *frames;
+  int64_t frame_stride;
+  int rows, hop;
+  int64_t s_begin, s_end;
+  uint64_t *plan;           // as TreeArgs::plan
+  int64_t plan_stride;
+  int two_mass;
+};
+constexpr int64_t PLAN_RECORD_BYTES = 128;
 
 #ifndef AFS_TREE_W
 #define AFS_TREE_W 16
@@ -36,6 +53,8 @@ int64_t tree_lane_bytes();
 int64_t tree_lds_doubles();
 hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const uint32_t *seeds, hipStream_t st);
 hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st);
-hipError_t launch_tree_nonfinite(const double *lds_state, int B, int32_t *count, hipStream_t st);
+hipError_t launch_tree_nonfinite(const double *lds_state, int B, int32_t *count, uint8_t *flags, hipStream_t st);
+hipError_t launch_tree_draws(const double *lds_state, int B, int64_t *draws, hipStream_t st);
+hipError_t launch_plan(const PlanArgs &a, hipStream_t st);
 
 }  // namespace afs

@@ -742,13 +742,14 @@ __device__ double sample_step(const Lane &Ln, const afs_frame *fl, const afs_fra
 
 }  // namespace
 
-// Reset the persistent state of utterances [0, B) and seed their generators.
+// Reset the persistent state of utterances [0, B) and seed their generators (seeds == nullptr:
+// utterance u is seeded u + 1, afs.h).
 __global__ void lane_reset_kernel(double *ws, int32_t *rng, int64_t bp, int B, const uint32_t *seeds) {
   int u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= B) return;
   for (int k = 0; k < Q_PERSIST; ++k) ws[(int64_t)k * bp + u] = 0.0;
   for (int d = 0; d < NDIP; ++d) ws[(int64_t)(Q_DCUT + d) * bp + u] = 3000.0;
-  seed_rng(rng + u, bp, seeds ? seeds[u] : 1u);
+  seed_rng(rng + u, bp, seeds ? seeds[u] : (uint32_t)u + 1u);
 }
 
 // Time loop over frame transitions k in [k_begin, k_end): pair (frames[k-1], frames[k]).
@@ -775,10 +776,12 @@ __global__ void __launch_bounds__(64) lane_synth_kernel(LaneArgs a) {
   NF[0] = bad;
 }
 
-__global__ void lane_nonfinite_kernel(const double *ws, int64_t bp, int B, int32_t *count) {
+__global__ void lane_nonfinite_kernel(const double *ws, int64_t bp, int B, int32_t *count, uint8_t *flags) {
   int u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= B) return;
-  if (ws[(int64_t)Q_NONFINITE * bp + u] != 0.0) atomicAdd(count, 1);
+  const bool nf = ws[(int64_t)Q_NONFINITE * bp + u] != 0.0;
+  if (flags) flags[u] = nf ? 1 : 0;
+  if (nf) atomicAdd(count, 1);
 }
 
 int64_t lane_ws_rows(const Tables &t) { return (int64_t)Q_FENV + t.env_total; }
@@ -800,9 +803,9 @@ hipError_t launch_lane_synth(const LaneArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_lane_nonfinite(const double *ws, int64_t bp, int B, int32_t *count, hipStream_t st) {
+hipError_t launch_lane_nonfinite(const double *ws, int64_t bp, int B, int32_t *count, uint8_t *flags, hipStream_t st) {
   if (B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(lane_nonfinite_kernel, dim3((B + 63) / 64), dim3(64), 0, st, ws, bp, B, count);
+  hipLaunchKernelGGL(lane_nonfinite_kernel, dim3((B + 63) / 64), dim3(64), 0, st, ws, bp, B, count, flags);
   return hipGetLastError();
 }
 

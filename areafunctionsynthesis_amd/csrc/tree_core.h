@@ -35,6 +35,7 @@ using std::sqrt;
 #endif
 
 #include "afs_model.h"
+#include "tree_plan.h"
 
 // Keeps the loads above it from being interleaved with the arithmetic below it (device).
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -66,14 +67,12 @@ enum : int {
   // (the dynamic arrays have NDYP slots: the ones past NDYNS are sinks of absent lane slots;
   // X_D has a sink at NS)
   X_E = X_P4 + 4, X_D = X_E + NDYP,                      // E: dynamic sections (s-23), D: all
-  X_L = X_D + NS + 1, X_R1 = X_L + NDYP, X_R0 = X_R1 + NDYP, X_AREA = X_R0 + NDYP,  // dynamic, s-23
-  X_RAD = X_AREA + NDYP,                                 // radius sqrt(A / pi) of the dynamic sections
-  X_GLEN = X_RAD + NDYP,                                 // glottis section lengths (2)
-  X_SMP = X_GLEN + 2,                                    // dipole samples (41)
+  X_L = X_D + NS + 1, X_R1 = X_L + NDYP, X_R0 = X_R1 + NDYP,  // dynamic, s-23
+  X_RAD = X_R0 + NDYP,                                   // radius sqrt(A / pi) of the dynamic sections
+  X_SMP = X_RAD + NDYP,                                  // dipole samples (41)
   X_UNION = X_SMP + NDIP,
-  //   noise scratch (n)
-  X_LEN = X_UNION, X_LAT = X_LEN + NPM, X_POS = X_LAT + NPM, X_TGT = X_POS + NPM,
-  X_CUTN = X_TGT + NDIP, X_ACT = X_CUTN + NDIP, X_NOISE_END = X_ACT + NDIP,
+  //   sink slots of the phases before the rows (n): stores of lanes / slots with nothing to store
+  X_ACT = X_UNION, X_NOISE_END = X_ACT + 16,
   //   solver
   //   (pivot / rhs with a sink slot at NC; edges with EDGE_ZERO and EDGE_SINK after TREE_NE)
   X_DIAG = X_UNION, X_RHS = X_DIAG + NC + 2, X_OFF = X_RHS + NC + 2, X_FILL = X_OFF + TREE_NE + 2,
@@ -88,9 +87,9 @@ enum : int {
   X_OUTF = X_TONE + 8,         // output Chebyshev: x1..x8, y1..y8
   X_PREVFLOW = X_OUTF + 16,
   X_NONFIN = X_PREVFLOW + 1,
-  X_ART = X_NONFIN + 1,        // 40 articulator bytes
-  X_RNG = X_ART + 5,           // rand(): value ring, prefix-sum ring (64 u32 each), head, pending (65 doubles)
-  X_GP = X_RNG + 65,           // interpolated glottis controls (6), teeth position, glottis dipole gain
+  X_NDRAW = X_NONFIN + 1,      // rand() calls so far (u64; diagnostics: afs_rng_draws)
+  X_RNG = X_NDRAW + 1,         // rand(): value ring, prefix-sum ring (64 u32 each), head, pending (65 doubles)
+  X_GP = X_RNG + 65,           // interpolated glottis controls (6), 2 spare
   X_TGLOT = X_GP + 8,          // transglottal-pressure filter x1..x4, y1..y4 (variable entrance loss)
   X_TVEL = X_TGLOT + 8,        // transvelar coupling filters H1, H2: x1..x4, y1..y4 each
   X_TVP = X_TVEL + 16,         // p[43], p[67] after the last update (transvelar filter inputs)
@@ -105,8 +104,7 @@ static_assert(X_STRIDE % 32 == 16, "utterance blocks offset by half a bank row")
 
 // Phase ids for Exec::mark (cycle accounting in tools/phase_prof; a no-op otherwise).
 enum : int {
-  PH_GEOMETRY, PH_NETWORK, PH_CONSTRICTIONS, PH_NOISE,
-  PH_C_POS, PH_C_T1, PH_C_T2, PH_C_LIP, PH_N_AMP, PH_N_RNG,
+  PH_GEOMETRY, PH_NETWORK, PH_NOISE, PH_N_AMP, PH_N_RNG,
   PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_COUNT
 };
 
@@ -203,12 +201,12 @@ struct Lane {
   using S = Shape<W>;
   double p[S::NSL], pr[S::NSL], w[S::NSL], wr[S::NSL], wr2[S::NSL];  // sections
   double u[S::NSL], ur[S::NSL], un[S::NSL];                          // their in-currents
-  double aL[S::ND], aR[S::ND], lL[S::ND], lR[S::ND], tL[S::ND], tR[S::ND];  // frame cache
+  double aL[S::ND], aR[S::ND], lL[S::ND], lR[S::ND];                 // frame cache
   double al[S::ND], be[S::ND];                                        // dynamic wall terms
   double damp[S::NDP], dout[S::NDP], dcut[S::NDP];                   // dipoles gl + k W
   double rad_u[2], rad_ur[2], rad_un[2];                             // owner of 64 / 83
   double sample;                                                     // lane 0
-  int art[S::ND];
+  uint64_t planw;                                                    // word gl of this sample's plan (tree_plan.h)
   uint32_t racc[S::NDP];                                             // rand() sums of owned dipoles
   uint32_t rtmp[3];                                                  // rand() block scratch
   SolveCarry sc;                                                     // chain lanes, during the solve
@@ -301,10 +299,6 @@ AFS_HD inline GlotOut two_mass_glottis(double *X, const Consts &C, const double 
   double chink = passive * TM_CHINK_LEN + gp[4];
   if (chink < 0.0) chink = 0.0;
   GlotOut go{clampA(2.0 * len * a0 + chink), clampA(2.0 * len * a1 + chink), th0, th1};
-  X[X_AREA + 0] = go.a0;
-  X[X_AREA + 1] = go.a1;
-  X[X_GLEN + 0] = th0;
-  X[X_GLEN + 1] = th1;
   // incTime
   const double crit = 0.5 * TM_CRIT_WIDTH;
   const double min0 = crit - rest0, min1 = crit - rest1;
@@ -457,9 +451,9 @@ AFS_HD inline void reset_lane(int gl, Lane<W> &R) {
   }
 #pragma unroll
   for (int j = 0; j < S::ND; ++j) {
-    R.aL[j] = R.aR[j] = R.lL[j] = R.lR[j] = R.tL[j] = R.tR[j] = R.al[j] = R.be[j] = 0.0;
-    R.art[j] = OTHER;
+    R.aL[j] = R.aR[j] = R.lL[j] = R.lR[j] = R.al[j] = R.be[j] = 0.0;
   }
+  R.planw = 0;
 #pragma unroll
   for (int k = 0; k < S::NDP; ++k) { R.damp[k] = 0.0; R.dout[k] = 0.0; R.dcut[k] = 3000.0; }
   for (int k = 0; k < 2; ++k) R.rad_u[k] = R.rad_ur[k] = R.rad_un[k] = 0.0;
@@ -488,11 +482,9 @@ AFS_HD inline void frame_load(int gl, Lane<W> &R, double *X, const afs_frame *fl
       R.aR[j] = clampA(fr->area_cm2[m]);
       R.lL[j] = fl->length_cm[m];
       R.lR[j] = fr->length_cm[m];
-      R.tL[j] = fl->laterality[m];
-      R.tR[j] = fr->laterality[m];
-      R.art[j] = fl->articulator[m];       // articulator comes from the left tube (Tube.cpp:452)
     }
   }
+  // (laterality, articulators and teeth position only steer the noise sources: tree_plan.h)
   if (gl == 0) {
     X[X_FRAME + 0] = fl->teeth_position_cm;
     X[X_FRAME + 1] = fr->teeth_position_cm;
@@ -502,8 +494,6 @@ AFS_HD inline void frame_load(int gl, Lane<W> &R, double *X, const afs_frame *fl
       X[X_FRAME + 4 + k] = fl->glottis[k];
       X[X_FRAME + 10 + k] = fr->glottis[k];
     }
-    unsigned char *art = (unsigned char *)(X + X_ART);
-    for (int m = 0; m < NPM; ++m) art[m] = fl->articulator[m];
   }
 }
 
@@ -514,9 +504,12 @@ template <int W>
 AFS_HD inline void phase_interpolate(int gl, Lane<W> &R, double *X, const Consts &C, double ratio) {
   // Branch-free over the lane's slots: pharynx/mouth sections interpolate area, length and
   // laterality, the nose sections 65..68 take the velum taper (Tube.cpp:402-416); other slots
-  // (glottis, absent) store into sinks.  The area and length stay in the lane (acur, lcur)
-  // for the network phase of the same block.
+  // (glottis, absent) compute on stand-ins.  The area and length stay in the lane (acur,
+  // lcur) for the network phase of the same block.  (The constriction scans that read the
+  // interpolated geometry of all sections run ahead of the time loop: tree_plan.h.)
   using S = Shape<W>;
+  (void)gl;
+  (void)X;
   const double r1 = 1.0 - ratio;
   const double open = r1 * X[X_FRAME + 2] + ratio * X[X_FRAME + 3];
 #pragma unroll
@@ -527,20 +520,11 @@ AFS_HD inline void phase_interpolate(int gl, Lane<W> &R, double *X, const Consts
     const bool nose = s >= S_NOSE0 && k < NDYNS;
     const double apm = clampA(r1 * R.aL[j] + ratio * R.aR[j]);
     const double lpm = r1 * R.lL[j] + ratio * R.lR[j];
-    const double tpm = r1 * R.tL[j] + ratio * R.tR[j];
     const int i = s - S_NOSE0;
     const double anose = clampA(open + ((double)(i * i) * (C.h.nose4_area - open)) * (1.0 / 16));
     const double a = pm ? apm : (nose ? anose : 1.0);
     R.acur[j] = a;
     R.lcur[j] = pm ? lpm : C.h.len_nose0;
-    if constexpr (S::ND * W <= NDYP) {
-      X[X_AREA + ((pm || nose) ? k : NDYNS)] = a;
-      X[pm ? X_LEN + s - S_PHARYNX0 : X_ACT] = lpm;
-      X[pm ? X_LAT + s - S_PHARYNX0 : X_ACT] = tpm;
-    } else {  // wider utterances (CPU emulator only)
-      if (pm || nose) X[X_AREA + k] = a;
-      if (pm) { X[X_LEN + s - S_PHARYNX0] = lpm; X[X_LAT + s - S_PHARYNX0] = tpm; }
-    }
   }
 }
 
@@ -556,8 +540,6 @@ AFS_HD inline GlotOut phase_glottis(double *X, const Consts &C, double ratio) {
       X[X_GP + k] = gp[k];
     }
     X[X_GP + 5] = GLOTTIS_DEFAULT_ASPIRATION_DB;  // X_GP + 5 is read as the aspiration strength
-    X[X_GP + 6] = r1 * X[X_FRAME + 0] + ratio * X[X_FRAME + 1];
-    X[X_GP + 7] = glottis_dipole_gain(GLOTTIS_DEFAULT_ASPIRATION_DB);
     return two_mass_glottis(X, C, gp);
   } else {
     double gp[6];
@@ -565,8 +547,6 @@ AFS_HD inline GlotOut phase_glottis(double *X, const Consts &C, double ratio) {
       gp[k] = r1 * X[X_FRAME + 4 + k] + ratio * X[X_FRAME + 10 + k];
       X[X_GP + k] = gp[k];
     }
-    X[X_GP + 6] = r1 * X[X_FRAME + 0] + ratio * X[X_FRAME + 1];
-    X[X_GP + 7] = glottis_dipole_gain(gp[5]);
     double rel0 = X[X_RELX + 0], rel1 = X[X_RELX + 1];
     // calcGeometry + getTubeData + Tube::setGlottisGeometry (TriangularGlottis.cpp:338-411)
     // (divisions sharing a denominator use one reciprocal; sqrt(m k) is a constant since
@@ -581,10 +561,6 @@ AFS_HD inline GlotOut phase_glottis(double *X, const Consts &C, double ratio) {
     double olen[2], clen[2], ow[2], cz[2];
     glottis_open_close(gp, cord, rel0, rel1, olen, clen, ow, cz);
     const GlotOut go{clampA(olen[0] * ow[0] + chink), clampA(olen[1] * ow[1] + chink), th0, th1};
-    X[X_AREA + 0] = go.a0;
-    X[X_AREA + 1] = go.a1;
-    X[X_GLEN + 0] = th0;
-    X[X_GLEN + 1] = th1;
     // incTime (TriangularGlottis.cpp:154-330) with the previous sample's pressures
     const double Tt = C.h.Tt;
     const double p0 = X[X_P4 + 0], p1 = X[X_P4 + 1], p2 = X[X_P4 + 2], p3 = X[X_P4 + 3];
@@ -629,20 +605,6 @@ AFS_HD inline double static_beta(const Lane<W> &R, int j, const Uni &U, const Co
   // (evaluated either way and selected: a branch here would split the slot block)
   const double v = k[ST_ALPHA] * (R.w[j] * k[ST_WC1] + R.wr[j] * k[ST_WC2] + R.wr2[j] * k[ST_LW] * (TH1 / TH));
   return U.opt.soft_walls ? v : 0.0;
-}
-
-// Section positions (Tube::calcPositions, Tube.cpp:611-622): one sequential sum, as in the
-// reference (the comparisons against obstacle positions depend on its rounding).  Every lane
-// of the utterance evaluates it (same values, same stores) inside the network phase, where
-// the scheduler interleaves the chain of dependent adds with the per-section arithmetic.
-AFS_HD inline void phase_positions(double *X) {
-  double p = 0.0;
-#pragma unroll
-  for (int m = 0; m < NPM; ++m) {
-    const double l = X[X_LEN + m];
-    X[X_POS + m] = p;
-    p += l;
-  }
 }
 
 template <int W, bool VARLOSS>
@@ -807,225 +769,96 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
            iir_run<4>(X + X_TVEL + 8, C.h.tvel2_a, C.h.tone_b, X[X_TVP + 1]);
     X[X_D + S_NOSE0 + 2] = R.p[JTV] + C.h.dtTH1 * R.pr[JTV] - Eg[JTV] * (betag[JTV] - src);
   }
-  // reset the dipole targets this lane owns (calcNoiseSources, TdsModel.cpp:1203-1208)
-#pragma unroll
-  for (int k = 0; k < S::NDP; ++k) {
-    int d = gl + k * W;
-    if (d < NDIP) { X[X_TGT + d] = 0.0; X[X_CUTN + d] = 0.0; }
-  }
 }
 
 // ---------------------------------------------------------------------------
-// Phase C: constriction detection and dipole targets (TdsModel.cpp:1188-1604).
-// The reference scans the 40 pharynx/mouth sections one after another; here every lane
-// tests the sections it owns and the scans become ballots (bit masks over the 40 sections)
-// and min/max reductions over the W lanes.  All decisions are uniform per utterance.
+// Phase T: dipole targets and amplitude smoothing (TdsModel.cpp:1456-1604, 1630-1643).
+// The geometry half of calcNoiseSources -- which constrictions exist and which two dipole
+// sources each drives with which weights -- comes from this sample's plan (tree_plan.h,
+// computed ahead of the time loop).  What is left depends on the state: the flow through
+// each narrowest section (the noise-smoothed flows of the previous sample), the particle
+// velocity, the full amplitude and the cutoff.  Every lane evaluates the four constrictions
+// (lane-uniform values) and keeps the targets of the dipoles it owns, in the reference's
+// store order (glottis, tongue 1, tongue 2, lip; the downstream source after the upstream
+// one), then smooths their amplitudes -- all inside the network block, no LDS round trip.
 // ---------------------------------------------------------------------------
-struct Cons { int first, last, narrow, art; double obst, lat; };
+struct Target { uint32_t up; double tup, tdn, fc; bool on; };
 
-// Bit m (0..39) = pred(R, j, m) evaluated by the owner of mouth section 25 + m
-// (dynamic slot j of lane gl holds section 23 + jW + gl).
-template <int W, class Xc, class P>
-AFS_HD inline uint64_t mouth_mask(Xc &x, P pred) {
-  using S = Shape<W>;
-  // (pred is evaluated for every slot, on section 25 for slots outside the pharynx/mouth, so
-  // that its LDS loads are not under a short-circuit branch)
-  uint64_t M = 0;
-#pragma unroll
-  for (int j = 0; j < S::ND; ++j)
-    M |= x.ballot([&](int gl, Lane<W> &R) {
-      const int m = j * W + gl - 2;
-      const bool in = m >= 0 && m < NPM;
-      const bool p = pred(R, j, in ? m : 0);
-      return in && p;
-    }) << (j * W);
-  return (M >> 2) & ((1ull << NPM) - 1);
-}
-
-// First minimum of the area over the mouth sections with pred (the reference's ascending
-// scan with a strict "<"); {1e6, -1} when there is none.
-template <int W, class Xc, class P>
-AFS_HD inline MinIdx mouth_min(Xc &x, const double *X, P pred) {
-  using S = Shape<W>;
-  return x.min_index([&](int gl, Lane<W> &R) {
-    MinIdx b{1000000.0, -1};
-#pragma unroll
-    for (int j = 0; j < S::ND; ++j) {
-      const int m = j * W + gl - 2;
-      const bool in = m >= 0 && m < NPM;
-      const int mm = in ? m : 0;
-      const bool p = pred(R, j, mm);
-      const double a = X[X_AREA + mm + 2];  // (loaded for every slot: no branch around it)
-      if (in && p && a < b.v) b = MinIdx{a, m};
-    }
-    return b;
-  });
-}
-
-// Dipole targets of one constriction (TdsModel.cpp:1456-1602), in two steps: the first
-// section that contains the obstacle (a ballot over the owners, obstacle_mask) and the
-// arithmetic (dipole_target<ART>), so that the constrictions of a sample run as independent
-// chains; store_target writes them in the reference's order.
-struct DipTarget { int up, dn; double tup, tdn, fc; };
-
-template <int W, class Xc>
-AFS_HD inline uint64_t obstacle_mask(Xc &x, const double *X, double obst) {
-  return mouth_mask<W>(x, [&](Lane<W> &R, int j, int m) {
-    (void)R; (void)j;
-    const double pos = X[X_POS + m], len = X[X_LEN + m];  // (both loads unconditional)
-    const bool lo = pos <= obst;
-    const bool hi = pos + len >= obst;
-    return lo && hi;
-  });
-}
-
-// M == 0 (no section contains the obstacle): the result is not stored.
-template <int ART>
-AFS_HD inline DipTarget dipole_target(const double *X, const Consts &C, double teeth, const Cons &c, uint64_t M) {
-  DipTarget t;
-  t.up = M ? __builtin_ctzll(M) : 0;  // the first section that contains the obstacle
-  t.dn = (t.up < NPM - 1) ? t.up + 1 : DIP_LIPS;
-  double fdn = fast_div(c.obst - X[X_POS + t.up], X[X_LEN + t.up]);
-  double fup = 1.0 - fdn;
-  double A = X[X_AREA + c.narrow - DYN0];
-  if (A < 0.1) A = 0.1;
-  const double inv_A = fast_rcp(A);
+AFS_HD inline double narrow_flow(const double *X, uint32_t o0, uint32_t o1) {
   double flow = 0.0;
-  const SecRec &q = C.sec[c.narrow];  // (an absent output reads the zero slot)
-  flow += xat(X, q.x_uo0);
-  flow += xat(X, q.x_uo1);
-  if (flow < 0.0) flow = 0.0;
-  double v = flow * inv_A;
-  double fc = 6000.0, gain = 0.0;
-  if (ART == LOWER_LIP) {
-    gain = 2.0e-7;
-  } else if (ART == VOCAL_FOLDS) {
-    gain = X[X_GP + 7];  // 0.5e-7 * 10^(aspiration dB / 20), from the glottis phase
-  } else {
-    fc = 0.15 * v * fast_sqrt((PI / 4.0) * inv_A);  // 0.15 v / d, d = sqrt(4 A / pi)
-    gain = (fabs(c.obst - teeth) < 0.0001) ? 10.0e-7 : 5.0e-7;
-  }
-  double full = gain * fabs(v) * v * v * fast_sqrt(A);
-  if (c.lat > 0.1) full = 0.0;
+  flow += xat(X, o0);  // (an absent output reads the zero slot)
+  flow += xat(X, o1);
+  return flow < 0.0 ? 0.0 : flow;  // only outgoing flow (:1512-1517)
+}
+
+AFS_HD inline double clamp_fc(double fc) {
   if (fc < 50.0) fc = 50.0;
   if (fc > 2000.0) fc = 2000.0;
-  t.tup = fup * full;
-  t.tdn = fdn * full;
-  t.fc = fc;
-  return t;
-}
-
-// Every lane of the utterance stores the same values (no exec-mask branch); a target that is
-// not stored (on == false) goes to the sink slots X_ACT, X_ACT + 1.
-template <int W, class Xc>
-AFS_HD inline void store_target(Xc &x, double *X, const DipTarget &t, bool on) {
-  x.par([&](int gl, Lane<W> &R) {
-    (void)gl; (void)R;
-    const int tu = on ? X_TGT + t.up : X_ACT, cu = on ? X_CUTN + t.up : X_ACT + 1;
-    const int td = on ? X_TGT + t.dn : X_ACT, cd = on ? X_CUTN + t.dn : X_ACT + 1;
-    X[tu] = t.tup; X[cu] = t.fc;
-    X[td] = t.tdn; X[cd] = t.fc;
-  });
+  return fc;
 }
 
 template <int W, class Xc>
-AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Consts &C) {
+AFS_HD inline void phase_targets(Xc &x, int gl, Lane<W> &R, const double *X, const Consts &C, double a_glot_up) {
   using S = Shape<W>;
-  // section positions: every lane evaluates the chain (same values, same stores), in the
-  // block of the first scans, which do not need them
-  x.par([&](int gl, Lane<W> &R) { (void)gl; (void)R; phase_positions(X); });
-  x.mark(PH_C_POS);
-  const double teeth = X[X_GP + 6];
-  // Extend a constriction over the neighbours with area < amin + 0.2 and the same
-  // articulator (TdsModel.cpp:1247-1262), including the reference's stop rules at the ends.
-  auto grow = [&](Cons &c, double amin, int a) {
-    const double amax = amin + 0.2;
-    const uint64_t M = mouth_mask<W>(x, [&](Lane<W> &R, int j, int m) { return X[X_AREA + m + 2] < amax && R.art[j] == a; });
-    const int lo = c.narrow - S_PHARYNX0;
-    const uint64_t dn = (~M | 1ull) & ((2ull << lo) - 1);
-    const uint64_t up = (~M | (1ull << (NPM - 1))) & ~((1ull << lo) - 1);
-    c.first = S_PHARYNX0 + (63 - __builtin_clzll(dn)) + 1;
-    c.last = S_PHARYNX0 + __builtin_ctzll(up) - 1;
-  };
-  auto tongue_obstacle = [&](Cons &c, double &min_teeth) {
-    const int f = c.first - S_PHARYNX0, l = c.last - S_PHARYNX0;
-    c.lat = x.max_value([&](int gl, Lane<W> &R) {
-      (void)R;
-      double b = 0.0;
+  const uint64_t hdr = x.template rec<PW_HDR>(), uo = x.template rec<PW_UO>(), uol = x.template rec<PW_UOL>();
+  const uint32_t fl = (uint32_t)hdr & 0xffu;
+  Target t[4];
+  {  // glottis: A = the upper glottis section's area (this sample's glottis), clamped at 0.1
+    const SecRec &q = C.sec[S_GLOT_UP];
+    const double A = a_glot_up < 0.1 ? 0.1 : a_glot_up;
+    const double v = narrow_flow(X, q.x_uo0, q.x_uo1) * fast_rcp(A);
+    const double full = plan_double(x.template rec<PW_GAIN_G>()) * fabs(v) * v * v * fast_sqrt(A);
+    const double fdn = plan_double(x.template rec<PW_FDN + 0>());
+    t[0] = Target{(uint32_t)(hdr >> 8) & 0xffu, (1.0 - fdn) * full, fdn * full, 2000.0, (fl & PF_G) != 0};
+  }
 #pragma unroll
-      for (int j = 0; j < S::ND; ++j) {
-        const int m = j * W + gl - 2;
-        const bool in = m >= 0 && m < NPM && m >= f && m <= l;
-        const double lat = X[X_LAT + (m >= 0 && m < NPM ? m : 0)];  // (unconditional load)
-        if (in) b = max_combine(b, lat);
-      }
-      return b;
-    });
-    const double jet = X[X_POS + l] + X[X_LEN + l];
-    // (all loads first, then selects)
-    const double an = X[X_AREA + c.narrow - DYN0];
-    const double ob = X[X_POS + l + 1] + 0.5 * X[X_LEN + l + 1];
-    const bool at_teeth = teeth - jet < 2.0;
-    c.obst = at_teeth ? teeth : ob;
-    min_teeth = at_teeth ? an : min_teeth;
-  };
-  // Up to four constrictions in the reference's order: glottis, tongue, second tongue, lip.
-  // Every step runs for every utterance (no branch: a wave serves four utterances); an absent
-  // constriction works on a stand-in section with valid indices, and the has_* flags decide
-  // what is used and stored.
-  const Cons cg = Cons{S_GLOT_LO, S_GLOT_UP, S_GLOT_UP, VOCAL_FOLDS, 1.5, 0.0};
-  // the tongue and the lip minimum: independent scans
-  const MinIdx t1 = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) { (void)m; return R.art[j] == TONGUE; });
-  const MinIdx lp = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) { (void)m; return R.art[j] == LOWER_LIP; });
-  const bool has_lp = lp.v < 1.0, has_t1 = t1.v < 1.0;
-  // the lip constriction's extent (used if it is narrower than a tongue at the teeth)
-  const int sl = S_PHARYNX0 + (has_lp ? lp.i : 0);
-  Cons cl = Cons{sl, sl, sl, LOWER_LIP, 0.0, 0.0};
-  grow(cl, lp.v, LOWER_LIP);
-  cl.obst = X[X_POS + cl.last + 1 - S_PHARYNX0];
-  // the first tongue constriction
-  const int st1 = S_PHARYNX0 + (has_t1 ? t1.i : 0);
-  Cons ct1 = Cons{st1, st1, st1, TONGUE, 0.0, 0.0};
-  grow(ct1, t1.v, TONGUE);
-  double mt1 = 1000000.0, mt2 = 1000000.0;
-  tongue_obstacle(ct1, mt1);
-  const int pf = ct1.first, pl = ct1.last;
-  const MinIdx t2 = mouth_min<W>(x, X, [&](Lane<W> &R, int j, int m) {
-    const int sm = S_PHARYNX0 + m;
-    return R.art[j] == TONGUE && (sm < pf || sm > pl);
-  });
-  x.mark(PH_C_T1);
-  // the second one (kept if it does not touch the first)
-  const bool cand_t2 = has_t1 && t2.v < 1.0;
-  const int st2 = S_PHARYNX0 + (cand_t2 ? t2.i : 0);
-  Cons ct2 = Cons{st2, st2, st2, TONGUE, 0.0, 0.0};
-  grow(ct2, t2.v, TONGUE);
-  const bool has_t2 = cand_t2 && (ct2.first > pl + 1 || ct2.last < pf - 1);
-  tongue_obstacle(ct2, mt2);
-  double min_teeth = has_t1 ? mt1 : 1000000.0;
-  min_teeth = (has_t2 && mt2 < 1000000.0) ? mt2 : min_teeth;
-  x.mark(PH_C_T2);
-  const bool has_l = lp.v < 1.0 && lp.v < min_teeth;
-  x.mark(PH_C_LIP);
-  // The four targets as independent chains, all evaluated (absent constrictions hold dummies
-  // with valid indices), stored in the reference's order; a target that is not stored writes
-  // the sink slots (X_ACT), so the phase has no branch.
-  const uint64_t Mg = obstacle_mask<W>(x, X, cg.obst);
-  const uint64_t M1 = obstacle_mask<W>(x, X, ct1.obst);
-  const uint64_t M2 = obstacle_mask<W>(x, X, ct2.obst);
-  const uint64_t Ml = obstacle_mask<W>(x, X, cl.obst);
-  const DipTarget tg = dipole_target<VOCAL_FOLDS>(X, C, teeth, cg, Mg);
-  const DipTarget tt1 = dipole_target<TONGUE>(X, C, teeth, ct1, M1);
-  const DipTarget tt2 = dipole_target<TONGUE>(X, C, teeth, ct2, M2);
-  const DipTarget tl = dipole_target<LOWER_LIP>(X, C, teeth, cl, Ml);
-  store_target<W>(x, X, tg, Mg != 0);
-  store_target<W>(x, X, tt1, has_t1 && M1 != 0);
-  store_target<W>(x, X, tt2, has_t2 && M2 != 0);
-  store_target<W>(x, X, tl, has_l && Ml != 0);
+  for (int c = 0; c < 2; ++c) {  // tongue constrictions: "normal" fricatives (:1547-1563)
+    const uint32_t o = (uint32_t)(uo >> (32 * c));
+    const double invA = plan_double(c ? x.template rec<PW_T2 + 0>() : x.template rec<PW_T1 + 0>());
+    const double sqA = plan_double(c ? x.template rec<PW_T2 + 1>() : x.template rec<PW_T1 + 1>());
+    const double invd = plan_double(c ? x.template rec<PW_T2 + 2>() : x.template rec<PW_T1 + 2>());
+    const double fdn = plan_double(c ? x.template rec<PW_FDN + 2>() : x.template rec<PW_FDN + 1>());
+    const double v = narrow_flow(X, o & 0xffffu, o >> 16) * invA;
+    const double fc = 0.15 * v * invd;
+    const double gain = (fl & (c ? PF_T2_TEETH : PF_T1_TEETH)) ? 10.0e-7 : 5.0e-7;
+    double full = gain * fabs(v) * v * v * sqA;
+    if (fl & (c ? PF_T2_LAT : PF_T1_LAT)) full = 0.0;
+    t[1 + c] = Target{(uint32_t)(hdr >> (16 + 8 * c)) & 0xffu, (1.0 - fdn) * full, fdn * full, clamp_fc(fc),
+                      (fl & (c ? PF_T2 : PF_T1)) != 0};
+  }
+  {  // lower lip: flat spectrum, gain 2e-7 (:1523-1529)
+    const double v = narrow_flow(X, (uint32_t)uol & 0xffffu, (uint32_t)(uol >> 16) & 0xffffu) *
+                     plan_double(x.template rec<PW_L + 0>());
+    const double full = 2.0e-7 * fabs(v) * v * v * plan_double(x.template rec<PW_L + 1>());
+    const double fdn = plan_double(x.template rec<PW_FDN + 3>());
+    t[3] = Target{(uint32_t)(hdr >> 32) & 0xffu, (1.0 - fdn) * full, fdn * full, 2000.0, (fl & PF_L) != 0};
+  }
+  // the owned dipoles: targets in store order, then the 40 Hz amplitude smoother
+  // (branch-free over the slots; a slot past the 41 dipoles is never targeted and never active)
+#pragma unroll
+  for (int k = 0; k < S::NDP; ++k) {
+    const uint32_t d = (uint32_t)(gl + k * W);
+    double tgt = 0.0, cut = 0.0;  // targetAmp reset (:1203-1208); cut 0: not targeted
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t dn = t[c].up < (uint32_t)(NPM - 1) ? t[c].up + 1 : (uint32_t)DIP_LIPS;
+      const bool hu = t[c].on && t[c].up == d, hd = t[c].on && dn == d;
+      tgt = hu ? t[c].tup : tgt;
+      cut = hu ? t[c].fc : cut;
+      tgt = hd ? t[c].tdn : tgt;
+      cut = hd ? t[c].fc : cut;
+    }
+    R.dcut[k] = cut != 0.0 ? cut : R.dcut[k];  // targeted this step: cutoff (re)assigned
+    const double old = R.damp[k];
+    const double amp = old + C.h.noise_amp_F * (tgt - old);
+    R.damp[k] = amp;
+    R.dout[k] = (old >= THR && amp < THR) ? 0.0 : R.dout[k];
+    R.racc[k] = 0u;
+  }
 }
 
-// Phase N: noise sources (TdsModel.cpp:1630-1708).  Amplitude smoothing of the owned
-// dipoles, then the rand() draws: source d, the q-th active one in source order, takes
+// Phase N: noise sources (TdsModel.cpp:1630-1708), after phase_targets smoothed the
+// amplitudes: the rand() draws: source d, the q-th active one in source order, takes
 // draws 12q .. 12q+11 of this sample; the lanes generate the stream 30 values at a time
 // (lane scans instead of one draw after another) and each source's sum of 12 draws is a
 // difference of two output prefix sums.  Then the one-pole shaping filter of the owned
@@ -1033,22 +866,6 @@ AFS_HD inline void phase_constrictions(Xc &x, double *X, const Uni &U, const Con
 template <int W, class Xc>
 AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
-  // (branch-free over the lane's dipole slots: a slot past the 41 dipoles reads dipole 0's
-  // values into its own, never used, state)
-  x.par([&](int gl, Lane<W> &R) {
-#pragma unroll
-    for (int k = 0; k < S::NDP; ++k) {
-      const int d0 = gl + k * W;
-      const int d = d0 < NDIP ? d0 : 0;
-      double cn = X[X_CUTN + d];
-      if (cn != 0.0) R.dcut[k] = cn;  // targeted this step: cutoff was (re)assigned
-      double old = R.damp[k];
-      double amp = old + C.h.noise_amp_F * (X[X_TGT + d] - old);
-      R.damp[k] = amp;
-      if (old >= THR && amp < THR) R.dout[k] = 0.0;
-      R.racc[k] = 0u;
-    }
-  });
   x.mark(PH_N_AMP);
   uint64_t act = 0;
 #pragma unroll
@@ -1140,11 +957,13 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
   x.mark(PH_N_RNG);
   // (every lane stores the same ring head / pending count; the shaping filter is branch-free
   // over the slots except for the exponential of a cutoff other than the clamped 2000 Hz)
+  const uint64_t ndraw = *(const uint64_t *)(X + X_NDRAW) + (uint64_t)need;
   x.par([&](int gl, Lane<W> &R) {
     (void)gl; (void)R;
     int32_t *c = (int32_t *)g;
     c[RNG_HEAD] = head;
     c[RNG_PEND] = avail - need;
+    *(uint64_t *)(X + X_NDRAW) = ndraw;  // (every lane stores the same count)
   });
   x.par([&](int gl, Lane<W> &R) {
 #pragma unroll
@@ -1262,7 +1081,6 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     const double *ks = C.stat[static_index(s)];
     const double LB = dyn ? X[X_L + s - DYN0] : ks[ST_L];
     const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
-    const double AB = dyn ? X[X_AREA + s - DYN0] : C.h.area_last_nose;
     const double EB = dyn ? X[X_E + s - DYN0] : ks[ST_E], DB = X[X_D + s];
     const SecRec &q = rec[j];
     const int rc = q.x_rad[0] / 8 - X_U, lc = q.x_rad[1] / 8 - X_U;
@@ -1270,7 +1088,6 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
     R.rad_un[0] = xat(X, q.x_rad[4]); R.rad_un[1] = xat(X, q.x_rad[5]);
     const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
-    (void)AB;
     {
       const double Rrad = dyn ? X[X_RRAD] : C.h.rrad_nose;  // (network phase / tables)
       double F = LA2 * idt + RA2 + Rrad;
@@ -1556,7 +1373,10 @@ AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts
   x.par_uniform([&](int gl, Lane<W> &R) { phase_interpolate<W>(gl, R, X, C, ratio); },
                 [&](Lane<W> &R) { (void)R; go = phase_glottis<MODEL>(X, C, ratio); });
   x.dyn_neighbors();
-  x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS>(gl, R, X, U, C, go); });
+  x.par([&](int gl, Lane<W> &R) {
+    phase_network<W, VARLOSS>(gl, R, X, U, C, go);
+    phase_targets<W>(x, gl, R, X, C, go.a1);
+  });
 }
 
 template <int W, class Xc>
@@ -1579,9 +1399,6 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.mark(PH_GEOMETRY);
   x.mark(PH_NETWORK);
   if (U.opt.generate_noise_sources) {
-    phase_constrictions<W>(x, X, U, C);
-    x.sync();
-    x.mark(PH_CONSTRICTIONS);
     phase_noise<W>(x, X, U, C);
   } else {
     x.par([&](int gl, Lane<W> &R) {

@@ -127,6 +127,14 @@ struct GpuExec {
     }
     g(gl, *R, v);
   }
+  // Word K of this sample's plan (tree_plan.h): lane K of each 16-lane row holds it
+  // (R.planw), DPP row_newbcast hands it to the whole row.
+  template <int K> __device__ __forceinline__ uint64_t rec() {
+    const uint64_t v = R->planw;
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x150 + K, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x150 + K, 0xF, 0xF, false);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+  }
   __device__ __forceinline__ void mark(int ph) {
     if constexpr (PROF) {
       uint64_t t = __builtin_amdgcn_s_memtime();
@@ -165,27 +173,38 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   const Consts &C = lds.C;
   GpuExec<PROF> ex{gl, &R};
   if constexpr (PROF) ex.last = __builtin_amdgcn_s_memtime();
-  const afs_frame *fu = a.frames + (int64_t)(a.frame_row ? a.frame_row[ue] : ue) * a.frame_stride;
+  const int64_t row = a.frame_row ? a.frame_row[ue] : ue;
+  const afs_frame *fu = a.frames + row * a.frame_stride;
   double *o = a.out + (int64_t)ue * a.out_stride;
-  int64_t t = 0;
+  // this utterance's plan records, word gl % 16 of each (tree_plan.h)
+  const uint64_t *pl = a.plan + row * a.plan_stride * PLAN_WORDS + (gl & (PLAN_WORDS - 1));
+  const int hop = a.hop;
+  const int64_t n = a.s_end - a.s_begin;
+  int k = (int)(a.s_begin / hop) + 1, i = (int)(a.s_begin % hop);
   // long hops: the output filter runs over each hop's flows once the hop is done (lane 0
-  // re-reads the flows it stored; the filter does not feed back into the tube)
-  const bool defer = a.hop >= OUT_DEFER_MIN_HOP;
-  for (int k = a.k_begin; k < a.k_end; ++k) {
-    frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
-    ex.sync();
-    const int64_t t0 = t;
-    for (int i = 0; i < a.hop; ++i) {
-      const double ratio = (double)i / (double)a.hop;
-      sample_step<TW>(ex, X, a.uni, C, ratio, defer);
-      if (valid && gl == 0) o[t] = R.sample;
-      ++t;
+  // re-reads the flows it stored; the filter does not feed back into the tube); a launch
+  // that ends inside a hop filters the part it has
+  const bool defer = hop >= OUT_DEFER_MIN_HOP;
+  frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
+  ex.sync();
+  uint64_t next = pl[0];
+  int64_t t0 = 0;
+  for (int64_t t = 0; t < n; ++t) {
+    R.planw = next;
+    next = pl[(t + 1 < n ? t + 1 : t) * PLAN_WORDS];  // the next sample's word, a sample ahead
+    const double ratio = (double)i / (double)hop;
+    sample_step<TW>(ex, X, a.uni, C, ratio, defer);
+    if (valid && gl == 0) o[t] = R.sample;
+    if (++i == hop) {
+      if (defer && valid && gl == 0) output_filter_run(X, C, o + t0, (int)(t + 1 - t0));
+      t0 = t + 1;
+      i = 0;
+      ++k;
+      if (t + 1 < n) frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
+      ex.sync();
     }
-    if (defer && gl == 0) {
-      if (valid) output_filter_run(X, C, o + t0, a.hop);
-    }
-    ex.sync();
   }
+  if (defer && valid && gl == 0 && t0 < n) output_filter_run(X, C, o + t0, (int)(n - t0));
   ex.sync();
   if (valid) {
     // (the per-sample fields carry nothing to the next launch; zero them so that their

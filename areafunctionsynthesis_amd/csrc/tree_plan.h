@@ -1,0 +1,228 @@
+// tree_plan.h -- the noise-source plan of one audio sample (kernel K5, tds_plan.hip).
+//
+// Everything calcNoiseSources (src/Backend/TdsModel.cpp:1188-1604) decides from the tube
+// GEOMETRY alone -- which constrictions exist (glottis, up to two tongue constrictions, the
+// lower lip), their extent, laterality, obstacle position, the two dipole sources each one
+// drives, the source weights and the area terms of the narrowest section -- depends only on
+// the interpolated frame of that sample (Tube::interpolate, Tube.cpp:438-505, and
+// Tube::calcPositions, :579-654), not on the acoustic state.  K5 evaluates it for every
+// utterance-sample ahead of the time loop, one thread per sample, with the reference's own
+// sequential scans; the cooperative synthesis kernel then reads 128 bytes per sample and
+// only combines them with the state-dependent flows (TdsModel.cpp:1507-1602).  This takes
+// the constriction scans -- ballots and lane reductions over the 40 pharynx/mouth sections,
+// a quarter of the per-sample latency chain -- out of the recurrence.
+//
+// The same function runs on the host (tests/emu), so the CPU emulator checks the split
+// against the oracle.
+#pragma once
+
+#include <cstdint>
+
+#include "afs_model.h"
+
+#if !defined(__HIPCC__)
+#include <cmath>
+#endif
+
+namespace afs {
+namespace tree {
+
+// One record = 16 u64 words; word w is held by lane w of the utterance in the synthesis
+// kernel and broadcast to the other lanes (DPP row_newbcast) where it is used.
+enum : int {
+  PW_HDR = 0,     // bytes 0..4: flags, up of glottis / tongue 1 / tongue 2 / lip (0..39)
+  PW_UO = 1,      // u16 x 4: X_UN byte offsets of the outputs of the narrowest section, tongue 1, 2
+  PW_UOL = 2,     // u16 x 2: the same for the lip constriction
+  PW_FDN = 3,     // 4 words: downstream factor of glottis, tongue 1, tongue 2, lip
+  PW_T1 = 7,      // 3 words: 1/A, sqrt(A), 1/d of the narrowest section (A >= 0.1, d = sqrt(4A/pi))
+  PW_T2 = 10,     // 3 words: the same for tongue 2
+  PW_L = 13,      // 2 words: 1/A, sqrt(A) of the lip constriction
+  PW_GAIN_G = 15, // glottis dipole gain 0.5e-7 * 10^(aspiration dB / 20) (TdsModel.cpp:1546)
+  PLAN_WORDS = 16
+};
+enum : uint32_t {
+  PF_G = 1, PF_T1 = 2, PF_T2 = 4, PF_L = 8,  // constriction present and its obstacle section found
+  PF_T1_LAT = 16, PF_T2_LAT = 32,           // laterality > 0.1: full amplitude 0 (:1567-1571)
+  PF_T1_TEETH = 64, PF_T2_TEETH = 128       // obstacle at the teeth: gain 10e-7, else 5e-7 (:1549-1562)
+};
+
+AFS_HD inline uint64_t plan_bits(double v) {
+#if defined(__HIPCC__)
+  return __builtin_bit_cast(uint64_t, v);
+#else
+  uint64_t b;
+  __builtin_memcpy(&b, &v, 8);
+  return b;
+#endif
+}
+AFS_HD inline double plan_double(uint64_t b) {
+#if defined(__HIPCC__)
+  return __builtin_bit_cast(double, b);
+#else
+  double v;
+  __builtin_memcpy(&v, &b, 8);
+  return v;
+#endif
+}
+
+AFS_HD inline double plan_clampA(double a) { return a < AMIN ? AMIN : a; }
+
+// The interpolated pharynx/mouth geometry of one sample, evaluated on demand (no per-thread
+// arrays: K5 keeps its registers for occupancy).  Every value is computed with the operations
+// of tree_core.h phase_interpolate and Tube::calcPositions, so it is bit-identical however
+// often it is re-evaluated.
+struct PlanGeom {
+  const afs_frame *fl, *fr;
+  double r1, ratio;
+  AFS_HD double area(int m) const {
+    return plan_clampA(r1 * plan_clampA(fl->area_cm2[m]) + ratio * plan_clampA(fr->area_cm2[m]));
+  }
+  AFS_HD double len(int m) const { return r1 * fl->length_cm[m] + ratio * fr->length_cm[m]; }
+  AFS_HD double lat(int m) const { return r1 * fl->laterality[m] + ratio * fr->laterality[m]; }
+  AFS_HD int art(int m) const { return fl->articulator[m]; }  // the left tube's (Tube.cpp:452)
+  // position of section m: the sequential sum of Tube::calcPositions (:611-622)
+  AFS_HD double pos(int m) const {
+    double p = 0.0;
+    for (int i = 0; i < m; ++i) p += len(i);
+    return p;
+  }
+  // first section with the articulator and the smallest area (strict "<", from 1e6), -1: none
+  AFS_HD int argmin(int a, double &amin, int skip_lo = 1, int skip_hi = 0) const {
+    int n = -1;
+    amin = 1000000.0;
+    for (int m = 0; m < NPM; ++m) {
+      const double A = area(m);
+      if (art(m) == a && A < amin && (m < skip_lo || m > skip_hi)) { amin = A; n = m; }
+    }
+    return n;
+  }
+  // the reference's constriction extent (TdsModel.cpp:1247-1262): from the narrowest section
+  // outwards while the area stays below amin + 0.2 with the same articulator, then one back
+  AFS_HD void grow(int narrow, double amin, int a, int &first, int &last) const {
+    const double maxA = amin + 0.2;
+    first = narrow;
+    last = narrow;
+    while (area(first) < maxA && art(first) == a && first > 0) --first;
+    while (area(last) < maxA && art(last) == a && last < NPM - 1) ++last;
+    ++first;
+    --last;
+  }
+  AFS_HD double max_lat(int first, int last) const {
+    double l = 0.0;
+    for (int m = first; m <= last; ++m)
+      if (lat(m) > l) l = lat(m);
+    return l;
+  }
+  // first section whose extent contains the obstacle (:1462-1471), -1: none; *p its position
+  AFS_HD int obstacle(double obst, double *p_out) const {
+    double p = 0.0;
+    for (int m = 0; m < NPM; ++m) {
+      const double l = len(m);
+      if (p <= obst && p + l >= obst) { *p_out = p; return m; }
+      p += l;
+    }
+    return -1;
+  }
+};
+
+// The plan of the sample at `ratio` between frames fl and fr.  sec: the kernel tables' section
+// records (X_UN offsets of the section outputs).  two_mass: the glottis is the TwoMassModel,
+// whose aspiration strength is Glottis::DEFAULT_ASPIRATION_STRENGTH_DB.
+AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double ratio, const SecRec *sec,
+                               bool two_mass, uint64_t *w) {
+  const PlanGeom g{fl, fr, 1.0 - ratio, ratio};
+  const double teeth = g.r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm;
+  const double asp_db = two_mass ? GLOTTIS_DEFAULT_ASPIRATION_DB : g.r1 * fl->glottis[5] + ratio * fr->glottis[5];
+  // position of the obstacle of a tongue constriction ending at `last` (:1283-1299)
+  auto tongue_obstacle = [&](int last, int narrow, double &min_teeth) {
+    const double pl = g.pos(last);
+    const double jet = pl + g.len(last);
+    if (teeth - jet < 2.0) {
+      min_teeth = g.area(narrow);
+      return teeth;
+    }
+    return (pl + g.len(last)) + 0.5 * g.len(last + 1);  // pos[last + 1] + 0.5 len[last + 1]
+  };
+
+  // tongue constriction 1 (:1228-1302)
+  double min_teeth = 1000000.0, amin1;
+  const int n1 = g.argmin(TONGUE, amin1);
+  const bool has_t1 = amin1 < 1.0;
+  int f1 = 0, l1 = -1;
+  double lat1 = 0.0, obst1 = 0.0;
+  if (has_t1) {
+    g.grow(n1, amin1, TONGUE, f1, l1);
+    lat1 = g.max_lat(f1, l1);
+    obst1 = tongue_obstacle(l1, n1, min_teeth);
+  }
+  // tongue constriction 2 (:1309-1392), kept when it does not touch the first
+  bool has_t2 = false;
+  int n2 = -1;
+  double lat2 = 0.0, obst2 = 0.0;
+  if (has_t1) {
+    double amin2;
+    n2 = g.argmin(TONGUE, amin2, f1, l1);
+    if (amin2 < 1.0) {
+      int f2, l2;
+      g.grow(n2, amin2, TONGUE, f2, l2);
+      if (f2 > l1 + 1 || l2 < f1 - 1) {
+        has_t2 = true;
+        lat2 = g.max_lat(f2, l2);
+        obst2 = tongue_obstacle(l2, n2, min_teeth);
+      }
+    }
+  }
+  // lower lip (:1399-1444): narrower than a tongue constriction at the teeth
+  double aminl;
+  const int nl = g.argmin(LOWER_LIP, aminl);
+  const bool has_l = aminl < 1.0 && aminl < min_teeth;
+  double obstl = 0.0;
+  if (has_l) {
+    int fl_, ll;
+    g.grow(nl, aminl, LOWER_LIP, fl_, ll);
+    obstl = g.pos(ll + 1);
+  }
+
+  // obstacle sections and source weights (:1456-1499)
+  const double obst[4] = {1.5, obst1, obst2, obstl};
+  const bool has[4] = {true, has_t1, has_t2, has_l};
+  uint32_t flags = 0, up[4] = {0, 0, 0, 0};
+  double fdn[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int c = 0; c < 4; ++c) {
+    if (!has[c]) continue;
+    double p = 0.0;
+    const int m = g.obstacle(obst[c], &p);
+    if (m < 0) continue;
+    flags |= 1u << c;
+    up[c] = (uint32_t)m;
+    fdn[c] = (obst[c] - p) / g.len(m);
+  }
+  if (lat1 > 0.1) flags |= PF_T1_LAT;
+  if (lat2 > 0.1) flags |= PF_T2_LAT;
+  if (fabs(obst1 - teeth) < 0.0001) flags |= PF_T1_TEETH;
+  if (fabs(obst2 - teeth) < 0.0001) flags |= PF_T2_TEETH;
+
+  w[PW_HDR] = (uint64_t)flags | ((uint64_t)up[0] << 8) | ((uint64_t)up[1] << 16) | ((uint64_t)up[2] << 24) |
+              ((uint64_t)up[3] << 32);
+  // the outputs of the narrowest sections (an absent constriction points at section 25's)
+  const SecRec &q1 = sec[S_PHARYNX0 + (n1 < 0 ? 0 : n1)], &q2 = sec[S_PHARYNX0 + (n2 < 0 ? 0 : n2)];
+  const SecRec &ql = sec[S_PHARYNX0 + (nl < 0 ? 0 : nl)];
+  w[PW_UO] = (uint64_t)q1.x_uo0 | ((uint64_t)q1.x_uo1 << 16) | ((uint64_t)q2.x_uo0 << 32) | ((uint64_t)q2.x_uo1 << 48);
+  w[PW_UOL] = (uint64_t)ql.x_uo0 | ((uint64_t)ql.x_uo1 << 16);
+  for (int c = 0; c < 4; ++c) w[PW_FDN + c] = plan_bits(fdn[c]);
+  // area terms of the narrowest sections, A clamped to 0.1 cm^2 (:1502-1508)
+  const int na[3] = {n1, n2, nl};
+  const int base[3] = {PW_T1, PW_T2, PW_L};
+  for (int c = 0; c < 3; ++c) {
+    double a = na[c] < 0 ? 1.0 : g.area(na[c]);
+    if (a < 0.1) a = 0.1;
+    w[base[c] + 0] = plan_bits(1.0 / a);
+    w[base[c] + 1] = plan_bits(sqrt(a));
+    if (c < 2) w[base[c] + 2] = plan_bits(1.0 / sqrt(4.0 * a / PI));
+  }
+  w[PW_L + 2] = 0;
+  w[PW_GAIN_G] = plan_bits(0.5e-7 * pow(10.0, asp_db / 20.0));
+}
+
+}  // namespace tree
+}  // namespace afs

@@ -97,9 +97,11 @@ class Context:
     def synchronize(self) -> None:
         _native.check(self._lib.afs_synchronize(self._h), self._h, "afs_synchronize")
 
-    def synthesize(self, frames, hop: int, seeds=None, out=None, report: bool = False):
+    def synthesize(self, frames, hop: int, seeds=None, out=None, report: bool = False, nonfinite=None):
         """frames[B, F] (FRAME_DTYPE array, or a uint8 torch tensor [B, F, 1072] on the GPU)
-        -> audio[B, (F-1)*hop] float64."""
+        -> audio[B, (F-1)*hop] float64.  ``seeds=None``: 1 .. B.  ``nonfinite``: optional uint8
+        array / tensor of B flags (1 = the utterance's audio holds NaN/Inf); with ``report``
+        the returned dict carries them under ``nonfinite`` too."""
         if isinstance(frames, np.ndarray):
             if frames.dtype != FRAME_DTYPE or frames.ndim != 2:
                 raise ValueError("frames must be a 2-D FRAME_DTYPE array [B, F]")
@@ -118,14 +120,26 @@ class Context:
             out = np.zeros((B, T), dtype=np.float64)
         if _nbytes(out) != B * T * 8:
             raise ValueError("out must hold B*(F-1)*hop doubles")
+        if nonfinite is None and report:
+            nonfinite = np.zeros(B, dtype=np.uint8)
+        if nonfinite is not None and _nbytes(nonfinite) != B:
+            raise ValueError("nonfinite must hold B bytes")
         rep = _native.AfsReport()
         st = self._lib.afs_synthesize(self._h, _vp(_addr(frames)), _vp(_addr(seeds)), B, F, hop,
-                                      _vp(_addr(out)), ctypes.byref(rep))
+                                      _vp(_addr(out)), _vp(_addr(nonfinite)), ctypes.byref(rep))
         _native.check(st, self._h, "afs_synthesize")
         if report:
             return out, {"device_ms": rep.device_ms, "samples": rep.samples,
-                         "nonfinite_utterances": rep.nonfinite_utterances, "kernel": rep.kernel}
+                         "nonfinite_utterances": rep.nonfinite_utterances, "kernel": rep.kernel,
+                         "nonfinite": nonfinite}
         return out
+
+    def rng_draws(self, batch: int) -> np.ndarray:
+        """rand() calls per utterance of the last synthesize / play_target_sequences call
+        (tree solver; the reference's count is what a wrapped rand() would count)."""
+        d = np.zeros(int(batch), dtype=np.int64)
+        _native.check(self._lib.afs_rng_draws(self._h, int(batch), _vp(_addr(d))), self._h, "afs_rng_draws")
+        return d
 
     def af_to_frames(self, params, frames=None):
         """OneDimAreaFunction::calculateOneDimTubeFunction on the GPU.
@@ -169,14 +183,15 @@ class Context:
             out = np.zeros((B, T), dtype=np.float64)
         if _nbytes(out) != B * T * 8:
             raise ValueError("out must hold B*T doubles")
+        nonfinite = np.zeros(B, dtype=np.uint8) if report else None
         rep = _native.AfsReport()
         st = self._lib.afs_play_target_sequences(self._h, _vp(_addr(shapes)), shapes.shape[0], _vp(_addr(targets)),
                                                  ctypes.byref(ts), _vp(_addr(seeds)), B, _vp(_addr(out)),
-                                                 ctypes.byref(rep))
+                                                 _vp(_addr(nonfinite)), ctypes.byref(rep))
         _native.check(st, self._h, "afs_play_target_sequences")
         if report:
             return out, {"device_ms": rep.device_ms, "samples": rep.samples,
-                         "nonfinite_utterances": rep.nonfinite_utterances}
+                         "nonfinite_utterances": rep.nonfinite_utterances, "nonfinite": nonfinite}
         return out
 
     def to_int16(self, samples, out=None):
@@ -247,10 +262,17 @@ class Synthesizer:
         n = max(int(num_samples), 1)
         out = np.zeros((self.batch, n), dtype=np.float64)
         produced = ctypes.c_int32(0)
-        st = self._lib.afs_session_synthesize(self._h, _vp(_addr(fr)), int(num_samples), _vp(_addr(out)),
+        st = self._lib.afs_session_synthesize(self._h, _vp(_addr(fr)), int(num_samples), _vp(_addr(out)), None,
                                               ctypes.byref(produced), None)
         _native.check(st, self.ctx.handle, "afs_session_synthesize")
         return out[:, : produced.value]
+
+    def rng_draws(self) -> np.ndarray:
+        """rand() calls of every voice since construction / the last reset (tree solver)."""
+        d = np.zeros(self.batch, dtype=np.int64)
+        _native.check(self._lib.afs_session_rng_draws(self._h, _vp(_addr(d))), self.ctx.handle,
+                      "afs_session_rng_draws")
+        return d
 
     # reference spelling
     synthesizeSignalTds = synthesize_signal_tds

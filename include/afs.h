@@ -27,8 +27,11 @@
  * Errors: the reference prints and continues (TdsModel.cpp:1832,1849,1898,2267); here every
  * call returns an afs_status and afs_last_error() holds a message.  Inputs are clamped exactly
  * as the reference clamps them (areas >= 0.001 cm^2, Tube.cpp:337/371/413).  Non-finite audio
- * (the reference's "matrix is not positive definite" path) is reported per call in
+ * (the reference's "matrix is not positive definite" path, TdsModel.cpp:2267) is reported per
+ * utterance in the optional `nonfinite` flag array of the synthesis calls and counted in
  * afs_report.nonfinite_utterances.
+ *
+ * Seeds: srand() seed per utterance / voice; a NULL seed array seeds utterance u with u + 1.
  *
  * Memory: frames / seeds / out may be host or device (hipMalloc) pointers; the library
  * detects which.  Device state lives in the session.  One context per host thread.
@@ -45,7 +48,7 @@
 extern "C" {
 #endif
 
-#define AFS_ABI_VERSION 2
+#define AFS_ABI_VERSION 3
 #define AFS_NUM_TUBE_SECTIONS 40   /* Tube::NUM_PHARYNX_MOUTH_SECTIONS (Tube.h:56-58) */
 #define AFS_NUM_GLOTTIS_PARAMS 6   /* TriangularGlottis::NUM_CONTROL_PARAMS (TriangularGlottis.h:26-35) */
 #define AFS_NUM_AF_PARAMS 16       /* OneDimAreaFunction::NUM_AF_PARAMS (OneDimAreaFunction.h:34-43) */
@@ -145,10 +148,17 @@ afs_status afs_set_stream(afs_ctx *ctx, void *hip_stream);
 afs_status afs_synchronize(afs_ctx *ctx);
 
 /* Whole trajectories.  frames[batch][num_frames], seeds[batch] (srand() seed per utterance,
- * 0 behaves as 1 like glibc), out[batch][(num_frames-1)*hop] doubles in [-1,1]. */
+ * 0 behaves as 1 like glibc; NULL: u + 1), out[batch][(num_frames-1)*hop] doubles in [-1,1].
+ * nonfinite: NULL or batch bytes (host or device), set to 1 for the utterances whose audio
+ * holds a NaN or an infinity, else 0. */
 afs_status afs_synthesize(afs_ctx *ctx, const afs_frame *frames, const uint32_t *seeds,
                           int32_t batch, int32_t num_frames, int32_t hop, double *out,
-                          afs_report *report);
+                          uint8_t *nonfinite, afs_report *report);
+/* Diagnostics: the number of rand() calls (TdsModel.cpp:1690-1692) each utterance of the last
+ * afs_synthesize / afs_play_target_sequences call made, draws[batch] (host or device).  A
+ * count that differs from the reference's means a noise source switched on or off at a
+ * different sample (TdsModel.cpp:1647-1666).  Tree solver only (else AFS_ERR_UNSUPPORTED). */
+afs_status afs_rng_draws(afs_ctx *ctx, int32_t batch, int64_t *draws);
 
 /* Stateful sessions: B independent Synthesizer instances living on the device. */
 afs_status afs_session_create(afs_ctx *ctx, int32_t batch, const uint32_t *seeds, afs_session **s);
@@ -156,8 +166,10 @@ afs_status afs_session_create(afs_ctx *ctx, int32_t batch, const uint32_t *seeds
  * utterance: frames[batch], out[batch][max(num_samples,1)].  The first call after create/reset
  * only latches the frames and produces no samples (*produced = 0). */
 afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32_t num_samples,
-                                  double *out, int32_t *produced, afs_report *report);
+                                  double *out, uint8_t *nonfinite, int32_t *produced, afs_report *report);
 afs_status afs_session_reset(afs_session *s, const uint32_t *seeds);
+/* rand() calls of every voice since the last reset (see afs_rng_draws). */
+afs_status afs_session_rng_draws(afs_session *s, int64_t *draws);
 void afs_session_destroy(afs_session *s);
 
 /* Area-function model -> tube frames (pharynx/mouth part, teeth).  params[n][16] in
@@ -196,7 +208,8 @@ int64_t afs_target_sequence_samples(const afs_target_sequence *ts, double sampli
  * on the GPU once per distinct target sequence and streamed in time chunks. */
 afs_status afs_play_target_sequences(afs_ctx *ctx, const double *shapes, int32_t num_shapes,
                                      const int32_t *targets, const afs_target_sequence *ts,
-                                     const uint32_t *seeds, int32_t B, double *out, afs_report *report);
+                                     const uint32_t *seeds, int32_t B, double *out, uint8_t *nonfinite,
+                                     afs_report *report);
 
 #ifdef __cplusplus
 }

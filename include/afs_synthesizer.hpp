@@ -117,7 +117,7 @@ class TdsVoices {
     const int n = numNewSamples < 1 ? 1 : numNewSamples;
     out_.resize((size_t)batch_ * (size_t)n);
     int32_t produced = 0;
-    check(afs_session_synthesize(s_, frames_.data(), numNewSamples, out_.data(), &produced, nullptr), ctx_.get(),
+    check(afs_session_synthesize(s_, frames_.data(), numNewSamples, out_.data(), nullptr, &produced, nullptr), ctx_.get(),
           "afs_session_synthesize");
     for (int b = 0; b < batch_; ++b)
       if (newSignals[b] && produced > 0)

@@ -33,6 +33,7 @@ struct CpuExec {
   }
   void sync() {}
   void mark(int) {}
+  template <int K> uint64_t rec() { return R[K].planw; }  // lane K holds plan word K
   template <class F> uint64_t ballot(F f) {
     uint64_t m = 0;
     for (int gl = 0; gl < W; ++gl)
@@ -79,6 +80,9 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
     const long t0 = t;
     for (int i = 0; i < hop; ++i) {
       double ratio = (double)i / (double)hop;
+      uint64_t w[PLAN_WORDS];  // K5's record of this sample (tree_plan.h)
+      plan_sample(frames + k - 1, frames + k, ratio, T.consts.sec, opt.glottis_model == AFS_GLOTTIS_TWO_MASS, w);
+      for (int gl = 0; gl < W; ++gl) R[gl].planw = w[gl % PLAN_WORDS];
       sample_step<W>(ex, X.data(), T.uni, T.consts, ratio, defer);
       out[t] = R[0].sample;
       if (t < ndump) {

@@ -167,6 +167,16 @@ class Oracle:
             out[u] = self.utterance(frames[u], hop, int(seeds[u]), fs)
         return out
 
+    def utterance_draws(self, frames: np.ndarray, hop: int, seed: int, fs: float):
+        """(audio, rand() calls) of one utterance: the latch then F-1 calls of hop samples."""
+        frames = np.ascontiguousarray(frames, dtype=FRAME_DTYPE)
+        h = self.lib.ao_create(fs, seed, None)
+        try:
+            parts = [self.call(h, frames[k], hop) for k in range(frames.shape[0])]
+            return np.concatenate(parts), int(self.lib.ao_rng_calls(h))
+        finally:
+            self.lib.ao_destroy(h)
+
     def rand_stream(self, seed: int, n: int) -> np.ndarray:
         buf = ctypes.create_string_buffer(31 * 4 + 8)
         self.lib.ao_rng_seed(buf, seed)
@@ -306,3 +316,23 @@ class RefLib:
 
 def ref_available() -> bool:
     return os.path.exists(REF_SO) or os.path.isdir("/root/reference/src/Backend")
+
+
+def _draws_job(args):
+    frames, hop, seed, fs = args
+    return Oracle().utterance_draws(frames, hop, seed, fs)
+
+
+def oracle_parallel(frames: np.ndarray, hop: int, seeds, fs: float, workers: int = 0):
+    """The oracle over rows of frames[B, F] in worker processes (one utterance per task).
+    Returns (audio[B, T], rand() calls[B])."""
+    import multiprocessing as mp
+    B = frames.shape[0]
+    jobs = [(np.ascontiguousarray(frames[u]), int(hop), int(seeds[u]), float(fs)) for u in range(B)]
+    workers = workers or max(1, min(16, (os.cpu_count() or 1), B))
+    if workers == 1:
+        res = [_draws_job(j) for j in jobs]
+    else:
+        with mp.get_context("spawn").Pool(workers) as pool:
+            res = pool.map(_draws_job, jobs)
+    return np.stack([r[0] for r in res]), np.array([r[1] for r in res], dtype=np.int64)

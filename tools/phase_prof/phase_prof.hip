@@ -57,7 +57,12 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   CK(hipMalloc(&dlanes, (size_t)B * TW * tree_lane_bytes()));
   CK(hipMalloc(&dprof, sizeof(uint64_t) * waves * PH_COUNT));
   CK(launch_tree_reset(dlanes, dlds, B, ds, nullptr));
-  TreeArgs a{dt, df, F, nullptr, 1, F, hop, dout, (int64_t)(F - 1) * hop, dlanes, dlds, B, ht->uni};
+  const int64_t T = (int64_t)(F - 1) * hop;
+  uint64_t *dplan;
+  CK(hipMalloc(&dplan, (size_t)B * T * PLAN_RECORD_BYTES));
+  PlanArgs pa{dt, df, F, B, hop, 0, T, dplan, T, 0};
+  CK(launch_plan(pa, nullptr));
+  TreeArgs a{dt, df, F, nullptr, hop, 0, T, dout, T, dplan, T, dlanes, dlds, B, ht->uni};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -79,7 +84,7 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
       g_wave[w] += h[(size_t)w * PH_COUNT + p];
     }
   (void)hipFree(dt); (void)hipFree(df); (void)hipFree(ds); (void)hipFree(dout);
-  (void)hipFree(dlds); (void)hipFree(dlanes); (void)hipFree(dprof);
+  (void)hipFree(dlds); (void)hipFree(dlanes); (void)hipFree(dprof); (void)hipFree(dplan);
   delete ht;
   return waves;
 }

@@ -12,8 +12,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", ".."))
 
-PHASES = ["geometry", "network", "c:targets", "n:filter", "c:positions", "c:tongue1", "c:tongue2", "c:lip",
-          "n:amp", "n:rng", "rows", "forward", "backward", "update", "output"]
+PHASES = ["geometry+targets", "network", "n:filter", "n:act", "n:rng", "rows", "forward", "backward", "update",
+          "output"]
 
 
 def main():
