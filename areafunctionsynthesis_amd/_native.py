@@ -20,6 +20,8 @@ AFS_SOLVER_TREE = 1
 AFS_SOLVER_SOR = 2
 AFS_FP64 = 0
 AFS_ASYNC = 0x1
+AFS_PROFILE = 0x2
+AFS_COMM_ID_BYTES = 128
 
 # Every symbol include/afs.h declares.
 EXPORTED = (
@@ -27,7 +29,9 @@ EXPORTED = (
     "afs_last_error", "afs_set_stream", "afs_synchronize", "afs_synthesize",
     "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_session_destroy",
     "afs_af_to_frames", "afs_to_int16", "afs_target_sequence_default", "afs_target_sequence_samples",
-    "afs_play_target_sequences", "afs_rng_draws", "afs_session_rng_draws",
+    "afs_play_target_sequences", "afs_rng_draws", "afs_session_rng_draws", "afs_kernel_times",
+    "afs_shard_range", "afs_comm_unique_id", "afs_comm_create", "afs_comm_create_all", "afs_comm_destroy",
+    "afs_gather_pcm", "afs_comm_fence", "afs_comm_synchronize", "afs_multi_synthesize",
 )
 
 
@@ -102,9 +106,25 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.afs_target_sequence_samples.restype = ctypes.c_int64
     lib.afs_play_target_sequences.argtypes = [vp, vp, ctypes.c_int32, vp, ctypes.POINTER(AfsTargetSequence), vp,
                                               ctypes.c_int32, vp, vp, ctypes.POINTER(AfsReport)]
+    i32p, i64p, dp = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)
+    lib.afs_kernel_times.argtypes = [vp, dp, i32p, dp, i32p]
+    lib.afs_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, i64p, i64p]
+    lib.afs_shard_range.restype = None
+    lib.afs_comm_unique_id.argtypes = [vp]
+    lib.afs_comm_create.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(vp)]
+    lib.afs_comm_create_all.argtypes = [vp, ctypes.c_int32, vp]
+    lib.afs_comm_destroy.argtypes = [vp]
+    lib.afs_comm_destroy.restype = None
+    lib.afs_gather_pcm.argtypes = [vp, vp, ctypes.c_int64, vp, vp]
+    lib.afs_comm_fence.argtypes = [vp]
+    lib.afs_comm_synchronize.argtypes = [vp]
+    lib.afs_multi_synthesize.argtypes = [vp, vp, ctypes.c_int32, vp, vp, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32, vp, vp, ctypes.POINTER(AfsReport)]
     for name in ("afs_create", "afs_set_stream", "afs_synchronize", "afs_synthesize",
                  "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_af_to_frames",
-                 "afs_to_int16", "afs_play_target_sequences", "afs_rng_draws", "afs_session_rng_draws"):
+                 "afs_to_int16", "afs_play_target_sequences", "afs_rng_draws", "afs_session_rng_draws",
+                 "afs_kernel_times", "afs_comm_unique_id", "afs_comm_create", "afs_comm_create_all",
+                 "afs_gather_pcm", "afs_comm_fence", "afs_comm_synchronize", "afs_multi_synthesize"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib

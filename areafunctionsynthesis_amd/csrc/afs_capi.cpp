@@ -18,55 +18,13 @@
 #include "afs_af.h"
 #include "afs_lane.h"
 #include "afs_audio.h"
+#include "afs_ctx.h"
 #include "afs_model.h"
 #include "afs_tree.h"
 
 static_assert(sizeof(afs_frame) == 1072, "afs_frame layout");
 
-struct afs_ctx {
-  afs_config cfg{};
-  hipStream_t stream = nullptr;
-  afs::Tables host_tab{};
-  afs::Tables *dev_tab = nullptr;
-  std::string err;
-  // reusable device buffers for whole-trajectory calls
-  void *ws = nullptr;
-  size_t ws_bytes = 0;
-  int32_t *rng = nullptr;
-  size_t rng_bytes = 0;
-  void *tree_lanes = nullptr;
-  size_t tree_lanes_bytes = 0;
-  void *stage_in = nullptr;
-  size_t stage_in_bytes = 0;
-  void *stage_out = nullptr;
-  size_t stage_out_bytes = 0;
-  void *stage_seeds = nullptr;
-  size_t stage_seeds_bytes = 0;
-  void *tgt = nullptr;  // target sequences: shape rows [Q][4][16] then frame_row [B]
-  size_t tgt_bytes = 0;
-  void *plan = nullptr;   // tree solver: noise-source plans of one launch (tree_plan.h)
-  size_t plan_bytes = 0;
-  void *stage_nf = nullptr;  // per-utterance non-finite flags staged for a host array
-  size_t stage_nf_bytes = 0;
-  int32_t last_B = 0;        // batch of the last whole-trajectory call (afs_rng_draws)
-  int32_t *dcount = nullptr;
-  int32_t *hcount = nullptr;  // pinned host copy of dcount
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-};
-
-struct afs_session {
-  afs_ctx *ctx = nullptr;
-  int B = 0;
-  int64_t bp = 0;
-  void *ws = nullptr;          // lane solver: SoA workspace; tree solver: per-utterance LDS blocks
-  int32_t *rng = nullptr;      // lane solver: generator state; tree solver: unused
-  void *tree_lanes = nullptr;  // tree solver: per-lane register state
-  afs_frame *pair = nullptr;   // [B][2]: previous frame, new frame
-  uint32_t *seeds = nullptr;   // device copy
-  bool latched = false;
-};
-
-namespace {
+namespace afs {
 
 afs_status fail(afs_ctx *c, afs_status s, const char *fmt, ...) {
   char buf[512];
@@ -77,14 +35,6 @@ afs_status fail(afs_ctx *c, afs_status s, const char *fmt, ...) {
   if (c) c->err = buf;
   return s;
 }
-
-#define HIP_TRY(ctx, call)                                                                   \
-  do {                                                                                       \
-    hipError_t e_ = (call);                                                                  \
-    if (e_ != hipSuccess)                                                                    \
-      return fail((ctx), e_ == hipErrorOutOfMemory ? AFS_ERR_OUT_OF_MEMORY : AFS_ERR_HIP,    \
-                  "%s failed: %s", #call, hipGetErrorString(e_));                            \
-  } while (0)
 
 bool is_device_ptr(const void *p) {
   if (!p) return false;
@@ -107,6 +57,14 @@ afs_status ensure(afs_ctx *c, void **buf, size_t *cap, size_t bytes) {
   return AFS_OK;
 }
 
+}  // namespace afs
+
+using afs::ensure;
+using afs::fail;
+using afs::is_device_ptr;
+
+namespace {
+
 int64_t pad64(int64_t b) { return (b + 63) / 64 * 64; }
 
 bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_TREE || s == AFS_SOLVER_SOR; }
@@ -120,6 +78,27 @@ constexpr int64_t PLAN_BUDGET = (int64_t)4 << 30;
 // Launch the synthesis of frame transitions 1 .. ntrans (frames[row * fstride + k], k = 0 the
 // latched frame) in chunks that keep each kernel well below a second; state is carried
 // between launches.  rows: number of distinct frame rows (B, or the target sequences).
+// AFS_PROFILE: record an event on the context's stream (a pooled one; recording stops past
+// the pool's cap until afs_kernel_times drains it).
+hipEvent_t prof_event(afs_ctx *c) {
+  if (!(c->cfg.flags & AFS_PROFILE)) return nullptr;
+  constexpr size_t CAP = 1 << 14;
+  if (c->pev_used == c->pev.size()) {
+    hipEvent_t e = nullptr;
+    if (c->pev.size() >= CAP || hipEventCreate(&e) != hipSuccess) {
+      c->timed_overflow = true;
+      return nullptr;
+    }
+    c->pev.push_back(e);
+  }
+  hipEvent_t e = c->pev[c->pev_used++];
+  if (hipEventRecord(e, c->stream) != hipSuccess) return nullptr;
+  return e;
+}
+void prof_pair(afs_ctx *c, hipEvent_t a, hipEvent_t b, int kind) {
+  if (a && b) c->timed.push_back({a, b, kind});
+}
+
 afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int rows, int ntrans, int hop,
                       double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B,
                       const int32_t *frame_row = nullptr) {
@@ -132,10 +111,15 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       const int64_t s1 = std::min(S, s0 + per);
       afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)c->plan, per,
                        c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0};
+      hipEvent_t e0 = prof_event(c);
       HIP_TRY(c, afs::launch_plan(pa, c->stream));
+      hipEvent_t e1 = prof_event(c);
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
                       (const uint64_t *)c->plan, per, lanes, (double *)ws, B, c->host_tab.uni};
       HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
+      hipEvent_t e2 = prof_event(c);
+      prof_pair(c, e0, e1, 1);
+      prof_pair(c, e1, e2, 0);
     }
     return AFS_OK;
   }
@@ -145,7 +129,9 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     double *o = out + (int64_t)(k - 1) * hop;
     afs::LaneArgs a{c->dev_tab, frames, fstride, frame_row, k, ke, hop, o, ostride, (double *)ws, rng, bp, B,
                     c->cfg.solver == AFS_SOLVER_SOR ? 1 : 0};
+    hipEvent_t e0 = prof_event(c);
     HIP_TRY(c, afs::launch_lane_synth(a, c->stream));
+    prof_pair(c, e0, prof_event(c), 0);
   }
   return AFS_OK;
 }
@@ -286,6 +272,9 @@ void afs_destroy(afs_ctx *c) {
   if (c->hcount) (void)hipHostFree(c->hcount);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
+  for (void *p : {c->m_out, c->m_pcm, c->m_nf, c->m_root})
+    if (p) (void)hipFree(p);
   delete c;
 }
 
@@ -303,9 +292,11 @@ afs_status afs_synchronize(afs_ctx *c) {
   return AFS_OK;
 }
 
-afs_status afs_synthesize(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B,
-                          int32_t F, int32_t hop, double *out, uint8_t *nonfinite, afs_report *rep) {
-  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+}  // extern "C"
+
+// afs_synthesize; force_async: leave the stream running unless a host buffer needs a wait
+static afs_status synth_core(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B, int32_t F,
+                             int32_t hop, double *out, uint8_t *nonfinite, afs_report *rep, bool force_async) {
   if (!frames || !out || B <= 0 || F < 2 || hop < 1)
     return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_synthesize: need frames, out, batch>0, num_frames>=2, hop>=1");
   HIP_TRY(c, hipSetDevice(c->cfg.device));
@@ -345,7 +336,7 @@ afs_status afs_synthesize(afs_ctx *c, const afs_frame *frames, const uint32_t *s
   bool nf_sync = false;
   if ((s = nonfinite_report(c, c->ws, bp, B, nonfinite, rep != nullptr, &nf_sync)) != AFS_OK) return s;
   if (host_out) HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)B * T * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  const bool sync = !(c->cfg.flags & AFS_ASYNC) || host_out || rep || nf_sync;
+  const bool sync = !(force_async || (c->cfg.flags & AFS_ASYNC)) || host_out || rep || nf_sync;
   if (sync) HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (rep) {
     float ms = 0.f;
@@ -355,6 +346,47 @@ afs_status afs_synthesize(afs_ctx *c, const afs_frame *frames, const uint32_t *s
     rep->nonfinite_utterances = *c->hcount;
     rep->kernel = c->cfg.solver;
   }
+  return AFS_OK;
+}
+
+afs_status afs::synthesize_async(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B, int32_t F,
+                                 int32_t hop, double *out, uint8_t *nonfinite) {
+  return synth_core(c, frames, seeds, B, F, hop, out, nonfinite, nullptr, true);
+}
+
+extern "C" {
+
+afs_status afs_synthesize(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B,
+                          int32_t F, int32_t hop, double *out, uint8_t *nonfinite, afs_report *rep) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (!frames || !out || B <= 0 || F < 2 || hop < 1)
+    return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_synthesize: need frames, out, batch>0, num_frames>=2, hop>=1");
+  return synth_core(c, frames, seeds, B, F, hop, out, nonfinite, rep, false);
+}
+
+afs_status afs_kernel_times(afs_ctx *c, double *synth_ms, int32_t *synth_launches, double *plan_ms,
+                            int32_t *plan_launches) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (!(c->cfg.flags & AFS_PROFILE)) return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_kernel_times: AFS_PROFILE is off");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  double ms[2] = {0.0, 0.0};
+  int32_t n[2] = {0, 0};
+  for (const auto &t : c->timed) {
+    float x = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&x, t.a, t.b));
+    ms[t.kind] += x;
+    ++n[t.kind];
+  }
+  const bool overflow = c->timed_overflow;
+  c->timed.clear();
+  c->pev_used = 0;
+  c->timed_overflow = false;
+  if (synth_ms) *synth_ms = ms[0];
+  if (synth_launches) *synth_launches = n[0];
+  if (plan_ms) *plan_ms = ms[1];
+  if (plan_launches) *plan_launches = n[1];
+  if (overflow) return fail(c, AFS_ERR_UNSUPPORTED, "afs_kernel_times: more launches than the event pool holds");
   return AFS_OK;
 }
 

@@ -1,0 +1,84 @@
+// afs_ctx.h -- the library's internal context and session objects (afs_capi.cpp,
+// afs_comm.cpp) and the host helpers they share.  Not part of the C ABI.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "afs_model.h"
+
+struct afs_ctx {
+  afs_config cfg{};
+  hipStream_t stream = nullptr;
+  afs::Tables host_tab{};
+  afs::Tables *dev_tab = nullptr;
+  std::string err;
+  // reusable device buffers for whole-trajectory calls
+  void *ws = nullptr;
+  size_t ws_bytes = 0;
+  int32_t *rng = nullptr;
+  size_t rng_bytes = 0;
+  void *tree_lanes = nullptr;
+  size_t tree_lanes_bytes = 0;
+  void *stage_in = nullptr;
+  size_t stage_in_bytes = 0;
+  void *stage_out = nullptr;
+  size_t stage_out_bytes = 0;
+  void *stage_seeds = nullptr;
+  size_t stage_seeds_bytes = 0;
+  void *tgt = nullptr;  // target sequences: shape rows [Q][4][16] then frame_row [B]
+  size_t tgt_bytes = 0;
+  void *plan = nullptr;   // tree solver: noise-source plans of one launch (tree_plan.h)
+  size_t plan_bytes = 0;
+  void *stage_nf = nullptr;  // per-utterance non-finite flags staged for a host array
+  size_t stage_nf_bytes = 0;
+  // afs_multi_synthesize: this device's shard of float audio, its int16 audio, its flags, and
+  // (device 0) the gathered int16 audio of the whole batch
+  void *m_out = nullptr, *m_pcm = nullptr, *m_nf = nullptr, *m_root = nullptr;
+  size_t m_out_bytes = 0, m_pcm_bytes = 0, m_nf_bytes = 0, m_root_bytes = 0;
+  int32_t last_B = 0;        // batch of the last whole-trajectory call (afs_rng_draws)
+  int32_t *dcount = nullptr;
+  int32_t *hcount = nullptr;  // pinned host copy of dcount
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // AFS_PROFILE: an event pair around every kernel launch of the synthesis calls
+  struct Timed { hipEvent_t a, b; int kind; };  // kind 0: synthesis kernel, 1: noise-source plan (K5)
+  std::vector<hipEvent_t> pev;  // pool
+  size_t pev_used = 0;
+  std::vector<Timed> timed;
+  bool timed_overflow = false;
+};
+
+struct afs_session {
+  afs_ctx *ctx = nullptr;
+  int B = 0;
+  int64_t bp = 0;
+  void *ws = nullptr;          // lane solver: SoA workspace; tree solver: per-utterance LDS blocks
+  int32_t *rng = nullptr;      // lane solver: generator state; tree solver: unused
+  void *tree_lanes = nullptr;  // tree solver: per-lane register state
+  afs_frame *pair = nullptr;   // [B][2]: previous frame, new frame
+  uint32_t *seeds = nullptr;   // device copy
+  bool latched = false;
+};
+
+namespace afs {
+
+afs_status fail(afs_ctx *c, afs_status s, const char *fmt, ...);
+bool is_device_ptr(const void *p);
+afs_status ensure(afs_ctx *c, void **buf, size_t *cap, size_t bytes);
+// afs_synthesize with the call's synchronisation left to the caller (no host wait unless a
+// host buffer needs it)
+afs_status synthesize_async(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B, int32_t F,
+                            int32_t hop, double *out, uint8_t *nonfinite);
+
+}  // namespace afs
+
+#define HIP_TRY(ctx, call)                                                                   \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return afs::fail((ctx), e_ == hipErrorOutOfMemory ? AFS_ERR_OUT_OF_MEMORY : AFS_ERR_HIP, \
+                       "%s failed: %s", #call, hipGetErrorString(e_));                       \
+  } while (0)

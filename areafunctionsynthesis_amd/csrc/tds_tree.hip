@@ -14,17 +14,41 @@ __global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_synth_kerne
   tree_synth_body<false>(a, lds, nullptr);
 }
 
-// One thread per (frame row, sample); consecutive threads take consecutive samples of a row,
-// so a wave reads the same two frames (cache hits) and writes 64 contiguous records.
-__global__ void __launch_bounds__(256) plan_kernel(PlanArgs a) {
+// Grid (rows, sample blocks of PLAN_BLOCK): one thread per (frame row, sample), a block of
+// consecutive samples of one row.  When the block's samples span at most PLAN_STAGE frames
+// (hops >= 128), the frames are staged in LDS first: the plan's scans read every section's
+// area / length / articulator several times, and from LDS those reads cost a fraction of the
+// cache-hit latency of global loads.  Shorter hops (target sequences, hop 1) read the frames
+// from global memory.  Each thread writes its 128-B record as 8 16-byte stores.
+constexpr int PLAN_BLOCK = 256, PLAN_STAGE = 4;
+constexpr int FRAME_WORDS = (int)(sizeof(afs_frame) / 8);
+static_assert(sizeof(afs_frame) % 8 == 0, "frames are copied as 8-byte words");
+
+__global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
+  __shared__ uint64_t fr_lds[PLAN_STAGE][FRAME_WORDS];
   const int64_t n = a.s_end - a.s_begin;
-  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= (int64_t)a.rows * n) return;
-  const int64_t row = id / n, t = id - row * n, s = a.s_begin + t;
-  const int k = (int)(s / a.hop) + 1, i = (int)(s % a.hop);
+  const int64_t row = blockIdx.x;
+  const int64_t t_first = (int64_t)blockIdx.y * PLAN_BLOCK;
+  const int64_t t_last = (t_first + PLAN_BLOCK < n ? t_first + PLAN_BLOCK : n) - 1;
+  const int64_t t = t_first + threadIdx.x;
   const afs_frame *f = a.frames + row * a.frame_stride;
+  // sample s plays frames s / hop and s / hop + 1
+  const int64_t k_lo = (a.s_begin + t_first) / a.hop, k_hi = (a.s_begin + t_last) / a.hop + 1;
+  const bool staged = k_hi - k_lo + 1 <= PLAN_STAGE;  // uniform over the block
+  if (staged) {
+    const uint64_t *src = (const uint64_t *)(f + k_lo);
+    const int words = (int)(k_hi - k_lo + 1) * FRAME_WORDS;
+    for (int w = threadIdx.x; w < words; w += PLAN_BLOCK) (&fr_lds[0][0])[w] = src[w];
+    __syncthreads();
+  }
+  if (t >= n) return;  // (after the block's only barrier)
+  const int64_t s = a.s_begin + t;
+  const int64_t k = s / a.hop + 1;
+  const int i = (int)(s - (k - 1) * a.hop);
+  const afs_frame *fl = staged ? (const afs_frame *)fr_lds[k - 1 - k_lo] : f + (k - 1);
+  const afs_frame *fr = staged ? (const afs_frame *)fr_lds[k - k_lo] : f + k;
   uint64_t w[PLAN_WORDS];
-  plan_sample(f + (k - 1), f + k, (double)i / (double)a.hop, a.tab->consts.sec, a.two_mass != 0, w);
+  plan_sample(fl, fr, (double)i / (double)a.hop, a.tab->consts.sec, a.two_mass != 0, w);
   ulonglong2 *o = (ulonglong2 *)(a.plan + (row * a.plan_stride + t) * PLAN_WORDS);
 #pragma unroll
   for (int q = 0; q < PLAN_WORDS / 2; ++q) o[q] = make_ulonglong2(w[2 * q], w[2 * q + 1]);
@@ -75,9 +99,10 @@ hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st) {
 }
 
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
-  const int64_t n = (int64_t)a.rows * (a.s_end - a.s_begin);
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(plan_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+  const int64_t n = a.s_end - a.s_begin;
+  if (n <= 0 || a.rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(plan_kernel, dim3((unsigned)a.rows, (unsigned)((n + PLAN_BLOCK - 1) / PLAN_BLOCK)),
+                     dim3(PLAN_BLOCK), 0, st, a);
   return hipGetLastError();
 }
 

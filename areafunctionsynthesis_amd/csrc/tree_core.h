@@ -105,7 +105,7 @@ static_assert(X_STRIDE % 32 == 16, "utterance blocks offset by half a bank row")
 // Phase ids for Exec::mark (cycle accounting in tools/phase_prof; a no-op otherwise).
 enum : int {
   PH_GEOMETRY, PH_NETWORK, PH_NOISE, PH_N_AMP, PH_N_RNG,
-  PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_COUNT
+  PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_TARGETS, PH_COUNT
 };
 
 // Solver sink / zero slots (see StepRec).
@@ -1372,11 +1372,11 @@ AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts
   GlotOut go{};
   x.par_uniform([&](int gl, Lane<W> &R) { phase_interpolate<W>(gl, R, X, C, ratio); },
                 [&](Lane<W> &R) { (void)R; go = phase_glottis<MODEL>(X, C, ratio); });
+  x.mark(PH_GEOMETRY);  // (phase marks: cycle accounting of tools/phase_prof, no-ops otherwise)
   x.dyn_neighbors();
-  x.par([&](int gl, Lane<W> &R) {
-    phase_network<W, VARLOSS>(gl, R, X, U, C, go);
-    phase_targets<W>(x, gl, R, X, C, go.a1);
-  });
+  x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS>(gl, R, X, U, C, go); });
+  x.mark(PH_NETWORK);
+  x.par([&](int gl, Lane<W> &R) { phase_targets<W>(x, gl, R, X, C, go.a1); });
 }
 
 template <int W, class Xc>
@@ -1396,8 +1396,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
     else geometry_network<W, AFS_GLOTTIS_TRIANGULAR, false>(x, X, U, C, ratio);
   }
   x.sync();
-  x.mark(PH_GEOMETRY);
-  x.mark(PH_NETWORK);
+  x.mark(PH_TARGETS);
   if (U.opt.generate_noise_sources) {
     phase_noise<W>(x, X, U, C);
   } else {

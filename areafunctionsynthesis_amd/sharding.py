@@ -3,8 +3,10 @@
 Utterances are independent, so the batch is split into contiguous per-rank blocks with no
 data-path collective; each rank builds exactly the rows the full batch would give it
 (workloads.* take ``first_utterance``; seeds are u + 1 for the global index u, so audio is
-independent of the GPU count).  The only collective is the gather of the audio to rank 0
-(RCCL ``gather`` on the GPU, gloo in the CPU tests).
+independent of the GPU count).  The only collective is the gather of the audio to rank 0:
+on GPUs the library's own RCCL gather (``afs_gather_pcm`` through :class:`CommTransport`), in
+the CPU tests torch's gloo gather (:class:`TorchTransport`) -- :class:`PcmGather` is the same
+code over either.
 """
 from __future__ import annotations
 
@@ -27,47 +29,79 @@ def gather_to_rank0(t, world: int, rank: int, dist) -> Optional[List]:
     return bufs
 
 
+class CommTransport:
+    """The library's RCCL gather (afs_gather_pcm): runs on the comm's own stream behind the
+    conversion, so the next synthesis overlaps it; ``fence`` orders later writes of the
+    buffers after it on the synthesis stream (no host wait)."""
+
+    def __init__(self, comm):
+        self.comm = comm
+
+    def gather(self, slot, local, root):
+        self.comm.gather_pcm(local.view(-1), root.view(-1) if root is not None else None)
+
+    def fence(self, slot):
+        self.comm.fence()
+
+    def drain(self):
+        self.comm.synchronize()
+
+
+class TorchTransport:
+    """torch.distributed gather into rank 0's root buffer (gloo in the CPU tests; the
+    collective moves raw bytes, gloo has no int16 collectives)."""
+
+    def __init__(self, dist, world: int, rank: int):
+        self.dist, self.world, self.rank = dist, world, rank
+        self.work = {}
+
+    def gather(self, slot, local, root):
+        import torch
+        recv = None
+        if self.rank == 0:
+            recv = [r.view(-1).view(torch.uint8) for r in root.view(self.world, -1)]
+        self.work[slot] = self.dist.gather(local.view(-1).view(torch.uint8), gather_list=recv, dst=0, async_op=True)
+
+    def fence(self, slot):
+        w = self.work.pop(slot, None)
+        if w is not None:
+            w.wait()
+
+    def drain(self):
+        for slot in list(self.work):
+            self.fence(slot)
+
+
 class PcmGather:
     """int16 audio of each step gathered to rank 0 while the next step synthesizes.
 
     ``submit(samples)`` converts the step's float audio to the reference's int16 format
-    (``convert(samples, out)``, i.e. ``Context.to_int16`` on the synthesis stream) into one
-    of ``depth`` rotating buffers and starts an asynchronous gather of it; the collective runs
-    on the process group's own stream, so the next step's kernels are not queued behind it.
-    A buffer is reused only after its previous gather completed.  int16 quarters the bytes
-    that cross xGMI compared with gathering the float64 output.
+    (``convert(samples, out)``, i.e. ``Context.to_int16`` on the synthesis stream) into one of
+    ``depth`` rotating buffers and starts the gather of it into rank 0's root buffer of the
+    same slot ([world][B][T], rank order = utterance order).  A buffer is rewritten only after
+    its previous gather completed (``transport.fence``).  int16 quarters the bytes that cross
+    xGMI compared with gathering the float64 output.
     """
 
-    def __init__(self, convert, shape, world: int, rank: int, dist, device=None, depth: int = 2):
+    def __init__(self, convert, shape, world: int, rank: int, transport, device=None, depth: int = 2):
         import torch
-        self.convert, self.world, self.rank, self.dist = convert, world, rank, dist
+        self.convert, self.world, self.rank, self.transport = convert, world, rank, transport
         self.bufs = [torch.empty(tuple(shape), dtype=torch.int16, device=device) for _ in range(depth)]
-        # the collective moves raw bytes (gloo has no int16 collectives; RCCL does not care)
-        self.recv = [[torch.empty_like(b) for _ in range(world)] if (rank == 0 and world > 1) else None
-                     for b in self.bufs]
-        self.work = [None] * depth
+        self.roots = [torch.empty((world,) + tuple(shape), dtype=torch.int16, device=device)
+                      if (rank == 0 and world > 1) else None for _ in range(depth)]
         self.k = 0
 
     def submit(self, samples):
-        import torch
         slot = self.k % len(self.bufs)
         self.k += 1
-        if self.work[slot] is not None:
-            self.work[slot].wait()
-            self.work[slot] = None
+        self.transport.fence(slot)
         self.convert(samples, self.bufs[slot])
-        if self.world > 1:
-            recv = [r.view(-1).view(torch.uint8) for r in self.recv[slot]] if self.recv[slot] else None
-            self.work[slot] = self.dist.gather(self.bufs[slot].view(-1).view(torch.uint8), gather_list=recv,
-                                               dst=0, async_op=True)
+        self.transport.gather(slot, self.bufs[slot], self.roots[slot])
         return slot
 
     def result(self, slot):
-        """Rank 0: the gathered [world] list of int16 shards of ``slot`` (after :meth:`drain`)."""
-        return self.recv[slot] if self.world > 1 else [self.bufs[slot]]
+        """Rank 0: the gathered [world, B, T] int16 audio of ``slot`` (after :meth:`drain`)."""
+        return self.roots[slot] if self.world > 1 else self.bufs[slot][None]
 
     def drain(self):
-        for i, w in enumerate(self.work):
-            if w is not None:
-                w.wait()
-                self.work[i] = None
+        self.transport.drain()

@@ -50,14 +50,14 @@ class Context:
     """An afs_ctx: device + sampling rate + solver + options (TdsModel::Options)."""
 
     def __init__(self, sampling_rate_hz: float = 22050.0, solver: str = "tree", device: int = 0,
-                 async_calls: bool = False, **options):
+                 async_calls: bool = False, profile: bool = False, **options):
         lib = _native.load()
         cfg = _native.AfsConfig()
         lib.afs_config_default(ctypes.byref(cfg))
         cfg.sampling_rate_hz = float(sampling_rate_hz)
         cfg.solver = SOLVERS[solver]
         cfg.device = int(device)
-        cfg.flags = _native.AFS_ASYNC if async_calls else 0
+        cfg.flags = (_native.AFS_ASYNC if async_calls else 0) | (_native.AFS_PROFILE if profile else 0)
         for k, v in options.items():
             if not hasattr(cfg.options, k):
                 raise TypeError(f"unknown option {k}")
@@ -133,6 +133,15 @@ class Context:
                          "nonfinite_utterances": rep.nonfinite_utterances, "kernel": rep.kernel,
                          "nonfinite": nonfinite}
         return out
+
+    def kernel_times(self) -> dict:
+        """(profile=True contexts) summed device time and count of the synthesis-kernel and
+        noise-source-plan launches since the previous call (waits for the stream)."""
+        sm, pm = ctypes.c_double(), ctypes.c_double()
+        sn, pn = ctypes.c_int32(), ctypes.c_int32()
+        _native.check(self._lib.afs_kernel_times(self._h, ctypes.byref(sm), ctypes.byref(sn), ctypes.byref(pm),
+                                                 ctypes.byref(pn)), self._h, "afs_kernel_times")
+        return {"synth_ms": sm.value, "synth_launches": sn.value, "plan_ms": pm.value, "plan_launches": pn.value}
 
     def rng_draws(self, batch: int) -> np.ndarray:
         """rand() calls per utterance of the last synthesize / play_target_sequences call
@@ -212,6 +221,102 @@ class Context:
         st = self._lib.afs_to_int16(self._h, _vp(_addr(samples)), n, _vp(_addr(out)))
         _native.check(st, self._h, "afs_to_int16")
         return out
+
+
+def shard_range(total: int, world: int, rank: int):
+    """afs_shard_range: (first, count) of ``rank``'s contiguous block of ``total`` utterances."""
+    f, n = ctypes.c_int64(), ctypes.c_int64()
+    _native.load().afs_shard_range(int(total), int(world), int(rank), ctypes.byref(f), ctypes.byref(n))
+    return f.value, n.value
+
+
+def comm_unique_id() -> bytes:
+    """afs_comm_unique_id (rank 0): the RCCL id every rank passes to :class:`Comm`."""
+    buf = (ctypes.c_uint8 * _native.AFS_COMM_ID_BYTES)()
+    _native.check(_native.load().afs_comm_unique_id(buf), None, "afs_comm_unique_id")
+    return bytes(buf)
+
+
+class Comm:
+    """afs_comm: this process's rank of the audio gather (one process per GPU, RCCL)."""
+
+    def __init__(self, ctx: Context, uid: bytes, rank: int, world: int):
+        if len(uid) != _native.AFS_COMM_ID_BYTES:
+            raise ValueError("the unique id holds AFS_COMM_ID_BYTES bytes")
+        self.ctx, self.rank, self.world = ctx, int(rank), int(world)
+        buf = (ctypes.c_uint8 * _native.AFS_COMM_ID_BYTES).from_buffer_copy(uid)
+        h = _vp()
+        _native.check(ctx._lib.afs_comm_create(ctx.handle, buf, self.rank, self.world, ctypes.byref(h)), ctx.handle,
+                      "afs_comm_create")
+        self._h, self._lib = h, ctx._lib
+
+    def gather_pcm(self, local, root_out=None, root_counts=None) -> None:
+        """afs_gather_pcm: int16 device tensor ``local`` to rank 0's ``root_out`` (device)."""
+        counts = None
+        if root_counts is not None:
+            counts = np.ascontiguousarray(root_counts, dtype=np.int64)
+        n = int(local.numel()) if hasattr(local, "numel") else int(local.size)
+        _native.check(self._lib.afs_gather_pcm(self._h, _vp(_addr(local)), n, _vp(_addr(root_out)),
+                                               _vp(_addr(counts))), self.ctx.handle, "afs_gather_pcm")
+
+    def fence(self) -> None:
+        _native.check(self._lib.afs_comm_fence(self._h), self.ctx.handle, "afs_comm_fence")
+
+    def synchronize(self) -> None:
+        _native.check(self._lib.afs_comm_synchronize(self._h), self.ctx.handle, "afs_comm_synchronize")
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.afs_comm_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Node:
+    """Several GPUs driven from this one process (afs_comm_create_all + afs_multi_synthesize):
+    ``synthesize`` shards the batch over the devices and returns the int16 audio of the whole
+    batch, gathered to the first device over RCCL."""
+
+    def __init__(self, sampling_rate_hz: float, devices: Sequence[int], solver: str = "tree", **options):
+        self.ctxs = [Context(sampling_rate_hz, solver=solver, device=d, **options) for d in devices]
+        n = len(self.ctxs)
+        hs = (_vp * n)(*[c.handle for c in self.ctxs])
+        self._comms = (_vp * n)()
+        lib = self.ctxs[0]._lib
+        _native.check(lib.afs_comm_create_all(hs, n, self._comms), self.ctxs[0].handle, "afs_comm_create_all")
+        self._hs, self._lib = hs, lib
+
+    def synthesize(self, frames: np.ndarray, hop: int, seeds=None, pcm_out=None, report: bool = False):
+        frames = np.ascontiguousarray(frames, dtype=FRAME_DTYPE)
+        B, F = frames.shape
+        T = (F - 1) * hop
+        if seeds is not None:
+            seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        if pcm_out is None:
+            pcm_out = np.zeros((B, T), dtype=np.int16)
+        nonfinite = np.zeros(B, dtype=np.uint8)
+        rep = _native.AfsReport()
+        st = self._lib.afs_multi_synthesize(self._hs, self._comms, len(self.ctxs), _vp(_addr(frames)),
+                                            _vp(_addr(seeds)), B, F, hop, _vp(_addr(pcm_out)), _vp(_addr(nonfinite)),
+                                            ctypes.byref(rep))
+        _native.check(st, self.ctxs[0].handle, "afs_multi_synthesize")
+        if report:
+            return pcm_out, {"device_ms": rep.device_ms, "samples": rep.samples,
+                             "nonfinite_utterances": rep.nonfinite_utterances, "nonfinite": nonfinite}
+        return pcm_out
+
+    def close(self) -> None:
+        for i in range(len(self.ctxs)):
+            if self._comms[i]:
+                self._lib.afs_comm_destroy(self._comms[i])
+                self._comms[i] = None
+        for c in self.ctxs:
+            c.close()
 
 
 def target_sequence(overrides: Optional[dict] = None) -> "_native.AfsTargetSequence":

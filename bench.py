@@ -1,17 +1,23 @@
 """Benchmark: batched time-domain tube synthesis on MI355X.
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--seconds S] [--fs HZ]
-For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).
+                [--workload static|fricatives|vcv]
+For N > 1 launch with torch.distributed.run (one rank per GPU).
 
-One *step* = one pass of the hot path over this rank's shard of the BASELINE config-4
-batch: B static-vowel utterances (default 8192 per GPU; 65536 at 8 GPUs) of S seconds at
-fs Hz, from frames already resident in HBM to fp64 audio in HBM, converted on the GPU to
-the reference's int16 output format and (N > 1) gathered to rank 0 over RCCL while the next
-step synthesizes.  Scaling is weak: per-GPU work is fixed.
+One *step* = one pass of the hot path over this rank's shard of the BASELINE config-4 batch:
+B static-vowel utterances (default 8192 per GPU; 65536 at 8 GPUs) of S seconds at fs Hz, from
+frames already resident in HBM to fp64 audio in HBM, converted on the GPU to the reference's
+int16 output format and (N > 1) gathered to rank 0 by the library's RCCL gather
+(afs_gather_pcm, xGMI) while the next step synthesizes.  Scaling is weak: per-GPU work is
+fixed.  torch.distributed (gloo) only carries the control plane: the RCCL id, barriers and the
+max-over-ranks time.
 
-Printed (rank 0): one JSON line with the BASELINE metric (whole-node samples/s), the
-roofline object of the dominant kernel and the CPU baseline (the reference's own
-sources, oracle/_ref, timed on this host's cores over a bounded sample).
+Printed (rank 0): one JSON line with the BASELINE metric (whole-node samples/s), the roofline
+object of the dominant kernel (HBM, as the north star asks, with the kernel's own launch times
+from HIP events around every launch: afs_kernel_times), the fp64 object (the path's binding
+resource: algorithmic flops counted from the restatement, profiles/flops_per_sample.json) and
+the CPU baseline (the reference's own sources, oracle/_ref, timed on this host's cores over a
+bounded sample, plus the single-core config-1 figure).
 """
 from __future__ import annotations
 
@@ -28,22 +34,29 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters (spec)
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector peak (spec)
-# fp64 lane-flops per utterance-sample executed by the tree kernel, counted on the GPU:
-# SQ_INSTS_VALU_FLOPS_FP64 counts flops per wave-instruction (2050.3 per wave-sample), x 64 lanes
-# / 4 utterances per wave (profiles/r01_pmc_sq_v2p.txt).  Lane-uniform work (glottis, output
-# stage) is counted on every lane.  (SURVEY.md 8(a)'s 1.8e4 is the reference algorithm's count.)
-FLOPS_PER_SAMPLE = 32805.0
+CPU_PROC_CAP = 16              # the box's CPU share per GPU (gpurun: 16 for one GPU)
 
 
-def pmc_traffic(kernel: str, workload: str, batch: int, samples: int, hop: int):
-    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/pmc_traffic.json,
-    written by tools/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE runs of this same
-    command), or None when no pass covers this configuration."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def flops_per_sample(workload: str):
+    """Reference-algorithm fp64 flops per sample (tools/flopcount: the restatement in the
+    reference's operation order, instrumented), for the workload's family."""
+    path = os.path.join(ROOT, "profiles", "flops_per_sample.json")
     if not os.path.exists(path):
         return None, None
-    e = json.load(open(path)).get(f"{kernel}|{workload}|B={batch}|T={samples}|hop={hop}")
-    return (e["traffic_bytes_per_launch"], e["tag"]) if e else (None, None)
+    db = json.load(open(path))["workloads"]
+    fam = {"static": "config2", "fricatives": "config5", "vcv": "config2"}[workload]
+    for name, e in db.items():
+        if name.startswith(fam):
+            return e["per_sample"], name
+    return None, None
+
+
+def pmc_entry(name: str, key: str):
+    """An entry of a committed PMC summary under profiles/ (None when absent)."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    return json.load(open(path)).get(key)
 
 
 def frame_bytes_per_sample(hop: int) -> float:
@@ -51,43 +64,81 @@ def frame_bytes_per_sample(hop: int) -> float:
     return 1072.0 / hop + 8.0
 
 
-def cpu_baseline(jobs, fs: float, n_utt: int, gpu_out: np.ndarray, what: str):
-    """Time the reference build (oracle/_ref) on a bounded sample, one process per core.
-    jobs[u] = ("frames", frames, seed, hop) or ("target", shapes4, seed, None)."""
-    import multiprocessing as mp
-
+def _cpu_init():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle_lib import REF_SO, ORACLE_SO  # noqa: F401
-
-    kind = "reference" if os.path.exists(REF_SO) else "port"
-    cores = max(1, min(16, os.cpu_count() or 1, n_utt))
-    jobs = [(kind,) + tuple(j) + (fs,) for j in jobs]
-    ctx = mp.get_context("spawn")
-    t0 = time.perf_counter()
-    with ctx.Pool(cores) as pool:
-        outs = pool.map(_cpu_job, jobs)
-    wall = time.perf_counter() - t0
-    samples = sum(o.size for o in outs)
-    errs = [float(np.abs(gpu_out[u] - outs[u]).max()) for u in range(n_utt)]
-    rmss = [float(np.sqrt(np.mean((gpu_out[u] - outs[u]) ** 2))) for u in range(n_utt)]
-    return {
-        "value": samples / wall,
-        "unit": "samples/s",
-        "cores": cores,
-        "kind": kind,
-        "sample": f"{n_utt} utterances ({what}) @ {fs:g} Hz (first utterances of this shard), {cores} processes",
-        "wall_s": wall,
-    }, max(errs), max(rmss)
+    import oracle_lib  # noqa: F401  (load the libraries before the clock starts)
 
 
 def _cpu_job(job):
+    """One utterance on one core; returns (samples, seconds of compute, audio)."""
     kind, what, data, seed, hop, fs = job
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import Oracle, RefLib
     lib = RefLib() if kind == "reference" else Oracle()
     if what == "target":  # playTargetSequence: per-sample area function -> tube, then n = 1 calls
-        return lib.utterance(Oracle().target_frames(data, fs), 1, seed, fs)
-    return lib.utterance(data, hop, seed, fs)
+        t0 = time.perf_counter()
+        x = lib.utterance(Oracle().target_frames(data, fs), 1, seed, fs)
+    else:
+        t0 = time.perf_counter()
+        x = lib.utterance(data, hop, seed, fs)
+    return x.size, time.perf_counter() - t0, x
+
+
+def cpu_baseline(jobs, fs: float, n_utt: int, gpu_out: np.ndarray, what: str, config1_frames):
+    """The reference build (oracle/_ref; the restatement if it is absent) on a bounded sample of
+    the same workload, one process per core, plus config 1 (the `a:` utterance, 1 s, one core).
+    The pool is started and warmed before the clock; each job also times its own compute."""
+    import multiprocessing as mp
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import REF_SO
+
+    kind = "reference" if os.path.exists(REF_SO) else "port"
+    host_cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cores = max(1, min(CPU_PROC_CAP, host_cpus, n_utt))
+    jobs = [(kind,) + tuple(j) + (fs,) for j in jobs]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(cores, initializer=_cpu_init) as pool:
+        pool.map(_cpu_init_probe, range(cores))  # every worker up and its libraries loaded
+        t0 = time.perf_counter()
+        outs = pool.map(_cpu_job, jobs, chunksize=1)
+        wall = time.perf_counter() - t0
+        c1 = pool.apply(_cpu_job, ((kind, "frames", config1_frames, 1, 441, fs),))
+    samples = sum(o[0] for o in outs)
+    busy = sum(o[1] for o in outs)
+    errs = [float(np.abs(gpu_out[u] - outs[u][2]).max()) for u in range(n_utt)]
+    rmss = [float(np.sqrt(np.mean((gpu_out[u] - outs[u][2]) ** 2))) for u in range(n_utt)]
+    per_core = samples / busy
+    return {
+        "value": samples / wall,
+        "unit": "samples/s",
+        "cores": cores,
+        "kind": kind,
+        "sample": f"{n_utt} utterances ({what}) @ {fs:g} Hz (the first utterances of this shard), "
+                  f"{cores} worker processes (pool warmed before the clock)",
+        "per_core_samples_per_s": per_core,
+        "host_cpus": host_cpus,
+        "process_cap": CPU_PROC_CAP,
+        "whole_host_estimate_samples_per_s": per_core * host_cpus,
+        "config1_single_core_samples_per_s": c1[0] / c1[1],
+        "config1": f"a: (Default.params), f0 120 Hz, 8000 dPa, 1 s @ {fs:g} Hz, one core, "
+                   "Synthesizer.cpp:515-639 driver restated in oracle/ref_harness.cpp",
+    }, max(errs), max(rmss)
+
+
+def _cpu_init_probe(_):
+    return os.getpid()
+
+
+def config1_frames(fs: float):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle
+    from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS
+    from areafunctionsynthesis_amd.params import default_shapes
+    f = Oracle().af_to_frame(default_shapes()["a:"])
+    f["glottis"] = DEFAULT_GLOTTIS
+    f["glottis"][1] = 8000.0  # sensorDataToGlottisParams (Synthesizer.cpp:905)
+    return np.repeat(f[None], int(round(fs / 441)) + 1)
 
 
 def main() -> None:
@@ -101,9 +152,10 @@ def main() -> None:
     ap.add_argument("--solver", default=os.environ.get("AFS_SOLVER", "tree"))
     ap.add_argument("--cpu-utterances", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=("static", "vcv"), default="static",
-                    help="static: config-4 shard of static vowels (default); vcv: config-3 VCV "
-                         "utterances through playTargetSequence (per-sample tubes, hop 1)")
+    ap.add_argument("--workload", choices=("static", "fricatives", "vcv"), default="static",
+                    help="static: config-4 shard of static vowels (default); fricatives: config 5 "
+                         "(fricatives + velum 1.0 cm^2); vcv: config-3 VCV utterances through "
+                         "playTargetSequence (per-sample tubes, hop 1)")
     args = ap.parse_args()
 
     import torch
@@ -114,45 +166,51 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     from areafunctionsynthesis_amd import sharding
     from areafunctionsynthesis_amd.frames import FRAME_DTYPE
-    from areafunctionsynthesis_amd.synthesizer import Context
-    from areafunctionsynthesis_amd.workloads import build_frames, static_vowels, vcv_targets
+    from areafunctionsynthesis_amd.synthesizer import Comm, Context, comm_unique_id
+    from areafunctionsynthesis_amd.workloads import build_frames, fricatives, static_vowels, vcv_targets
 
     B = args.batch
-    ctx = Context(args.fs, solver=args.solver, device=local, async_calls=True)
+    ctx = Context(args.fs, solver=args.solver, device=local, async_calls=True, profile=True)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
 
     first, _ = sharding.shard_range(rank, world, B)
-    max_launch_samples = 65536 if args.solver == "tree" else 8192
-    if args.workload == "static":
-        w = static_vowels(B, seconds=args.seconds, fs=args.fs, first_utterance=first)
+    if args.workload in ("static", "fricatives"):
+        gen = static_vowels if args.workload == "static" else fricatives
+        w = gen(B, seconds=args.seconds, fs=args.fs, first_utterance=first)
         frames = build_frames(w, ctx.af_to_frames)
         F, hop, T = w.num_frames, w.hop, w.samples_per_utterance
         seeds = w.seeds
         frames_dev = torch.from_numpy(frames.view(np.uint8).reshape(B, F, FRAME_DTYPE.itemsize)).to(dev)
-        launches_per_step = -(-(F - 1) // max(1, max_launch_samples // hop))
 
         def synth():
             ctx.synthesize(frames_dev, hop, seeds=seeds_dev, out=out_dev)
     else:
         shapes, targets, seeds = vcv_targets(B, first_utterance=first)
         hop, T = 1, ctx.target_sequence_samples()
-        launches_per_step = -(-T // max_launch_samples)
 
         def synth():
             ctx.play_target_sequences(shapes, targets, seeds=seeds_dev, out=out_dev)
     seeds_dev = torch.from_numpy(seeds.astype(np.int32)).to(dev)
     out_dev = torch.empty((B, T), dtype=torch.float64, device=dev)
 
-    # the reference's output format (int16, Synthesizer.cpp:955-973) is produced on the GPU
-    # and gathered to rank 0 while the next step synthesizes
-    pcm = sharding.PcmGather(lambda x, o: ctx.to_int16(x, out=o), (B, T), world, rank, dist, device=dev)
+    # the reference's output format (int16, Synthesizer.cpp:955-973) is produced on the GPU and
+    # gathered to rank 0 by the library's RCCL gather while the next step synthesizes
+    comm = None
+    if world > 1:
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = Comm(ctx, uid[0], rank, world)
+        transport = sharding.CommTransport(comm)
+    else:
+        transport = _NoGather()
+    pcm = sharding.PcmGather(lambda x, o: ctx.to_int16(x, out=o), (B, T), world, rank, transport, device=dev)
 
     def step():
         synth()
@@ -162,6 +220,7 @@ def main() -> None:
         step()
     pcm.drain()
     torch.cuda.synchronize(dev)
+    ctx.kernel_times()  # drop the warm-up launches
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
@@ -179,7 +238,8 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     synth_ms = [a.elapsed_time(b) for a, b in ev]
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    kt = ctx.kernel_times()
+    t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -188,15 +248,32 @@ def main() -> None:
         total_samples = float(world) * B * T * args.steps
         value = total_samples / elapsed
         ms_step = elapsed / args.steps * 1e3
-        avg_launch_s = (np.mean(synth_ms) / 1e3) / launches_per_step
-        samples_per_launch = B * T / launches_per_step
-        alg_bytes = samples_per_launch * frame_bytes_per_sample(hop)
+        kname = "lane_synth_kernel" if args.solver in ("cholesky", "sor") else "tree_synth_kernel"
+        launches = max(1, kt["synth_launches"])
+        avg_launch_s = kt["synth_ms"] / launches / 1e3
+        samples_per_launch = B * T * args.steps / launches
+        bps = frame_bytes_per_sample(hop)
+        alg_bytes = samples_per_launch * bps
         achieved_gbs = alg_bytes / avg_launch_s / 1e9
-        flops = samples_per_launch * FLOPS_PER_SAMPLE
-        kname = "lane_synth_kernel" if args.solver == "cholesky" else "tree_synth_kernel"
-        traffic, traffic_tag = (None, None)
-        if launches_per_step == 1:
-            traffic, traffic_tag = pmc_traffic(kname, args.workload, B, T, hop)
+        tkey = f"{kname}|{args.workload}|B={B}|T={T}|hop={hop}"
+        tr = pmc_entry("pmc_traffic.json", tkey)
+        per, per_src = flops_per_sample(args.workload)
+        sq = pmc_entry("pmc_sq_fp64.json", tkey)
+        fp64 = None
+        if per is not None:
+            alg_tf = per["flops"] * samples_per_launch / avg_launch_s / 1e12
+            fp64 = {
+                "algorithmic_flops_per_sample": per["flops"],
+                "algorithmic_transcendentals_per_sample": per["transc"],
+                "algorithmic_source": f"profiles/flops_per_sample.json [{per_src}]: the restatement in the "
+                                      "reference's operation order (envelope Cholesky), instrumented per IR block",
+                "achieved_tflops": alg_tf,
+                "peak_tflops": FP64_PEAK_TFLOPS,
+                "frac": alg_tf / FP64_PEAK_TFLOPS,
+                "executed_lane_flops_per_sample": sq["lane_flops_per_sample"] if sq else None,
+                "executed_source": f"profiles/pmc_sq_fp64.json [{sq['tag']}] (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes / "
+                                   "4 utterances per wave)" if sq else None,
+            }
         result = {
             "metric": "audio samples/s (whole node) on 64k-utterance batch; max-abs err vs CPU ref",
             "value": value,
@@ -211,56 +288,78 @@ def main() -> None:
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": (f"BASELINE config 4 shard: {B} static-vowel utterances/GPU x {args.seconds:g} s "
-                             f"@ {args.fs:g} Hz ({B * 8} at 8 GPUs), frames resident in HBM")
-                if args.workload == "static" else
-                (f"BASELINE config 3 (fp64 state): {B} VCV utterances/GPU through playTargetSequence "
-                 f"({T} samples @ {args.fs:g} Hz, per-sample area-function tubes built on the GPU)"),
+                "workload": {
+                    "static": f"BASELINE config 4 shard: {B} static-vowel utterances/GPU x {args.seconds:g} s "
+                              f"@ {args.fs:g} Hz ({B * 8} at 8 GPUs), frames resident in HBM",
+                    "fricatives": f"BASELINE config 5: {B} fricative utterances (s f z S Z x C R v) + velum "
+                                  f"1.0 cm^2/GPU x {args.seconds:g} s @ {args.fs:g} Hz, frames resident in HBM",
+                    "vcv": f"BASELINE config 3 (fp64 state): {B} VCV utterances/GPU through playTargetSequence "
+                           f"({T} samples @ {args.fs:g} Hz, per-sample area-function tubes built on the GPU)",
+                }[args.workload],
                 "batch_per_gpu": B,
                 "global_batch": B * world,
                 "samples_per_utterance": T,
                 "fs_hz": args.fs,
                 "hop": hop,
                 "solver": args.solver,
-                "parallelism": f"dp{world} (utterance shards, int16 audio gathered to rank 0 over RCCL, overlapped)" if world > 1
-                               else "dp1",
+                "parallelism": f"dp{world} (utterance shards; int16 audio gathered to rank 0 by afs_gather_pcm over "
+                               "RCCL, overlapped with the next step)" if world > 1 else "dp1",
             },
             "x_realtime": value / args.fs,
+            "step_device_ms": float(np.mean(synth_ms)),
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_unit": "bytes per launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
-                "traffic_source": f"profiles/pmc_traffic.json [{traffic_tag}]" if traffic else None,
+                "traffic": tr["traffic_bytes_per_launch"] if tr else None,
+                "traffic_unit": "bytes per launch (rocprofv3 PMC)",
+                "traffic_correction": tr["correction"] if tr else None,
+                "traffic_source": f"profiles/pmc_traffic.json [{tr['tag']}]" if tr else None,
                 "algorithmic_bytes_per_launch": alg_bytes,
+                "bytes_per_sample": bps,
                 "kernel": kname,
                 "avg_launch_ms": avg_launch_s * 1e3,
-                "launches_per_step": launches_per_step,
-                "bytes_per_sample": frame_bytes_per_sample(hop),
-                "fp64_achieved_tflops": flops / avg_launch_s / 1e12,
-                "fp64_peak_tflops": FP64_PEAK_TFLOPS,
+                "launches_per_step": kt["synth_launches"] / args.steps,
+                "launch_timing": "HIP events around every launch on the library's stream (afs_kernel_times)",
+                "plan_kernel_ms_per_step": kt["plan_ms"] / args.steps,
+                "binding_resource": "neither HBM nor MFMA: the latency of the per-sample fp64 recurrence "
+                                    "(SURVEY.md 8(d)); see fp64",
             },
+            "fp64": fp64,
         }
         if world == 1 and not args.no_cpu_baseline:
             n = min(args.cpu_utterances, B)
             gpu_out = out_dev[:n].cpu().numpy()
-            if args.workload == "static":
+            if args.workload != "vcv":
                 jobs = [("frames", frames[u], int(seeds[u]), hop) for u in range(n)]
                 what = f"{F - 1} frames x {hop} samples"
             else:
                 jobs = [("target", shapes[targets[u]], int(seeds[u]), None) for u in range(n)]
                 what = f"playTargetSequence, {T} samples, trajectory built per sample on the CPU"
-            cb, max_abs, max_rms = cpu_baseline(jobs, args.fs, n, gpu_out, what)
-            cb.pop("wall_s")
+            cb, max_abs, max_rms = cpu_baseline(jobs, args.fs, n, gpu_out, what, config1_frames(args.fs))
             result["cpu_baseline"] = cb
             result["max_abs_err_vs_cpu_ref"] = max_abs
             result["max_rms_err_vs_cpu_ref"] = max_rms
         print(json.dumps(result), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+class _NoGather:
+    """One GPU: the int16 audio is already whole on rank 0."""
+
+    def gather(self, slot, local, root):
+        pass
+
+    def fence(self, slot):
+        pass
+
+    def drain(self):
+        pass
 
 
 if __name__ == "__main__":

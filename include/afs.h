@@ -23,6 +23,10 @@
  *                              (Synthesizer.cpp:955-973, Signal16 = short, Signal.h:19)
  *   afs_play_target_sequences <- Synthesizer::playTargetSequence (Synthesizer.cpp:1299-1422)
  *                              with interpolateParameters (:1286-1294), for B utterances
+ *   afs_multi_synthesize    <- the same whole-trajectory driver over several GPUs of one node,
+ *   afs_comm_*, afs_gather_pcm  the int16 audio (Synthesizer.cpp:955-973) gathered to the first
+ *                              GPU over RCCL (the reference has one Synthesizer per process and
+ *                              no collectives; this is the only exchange the batch needs)
  *
  * Errors: the reference prints and continues (TdsModel.cpp:1832,1849,1898,2267); here every
  * call returns an afs_status and afs_last_error() holds a message.  Inputs are clamped exactly
@@ -48,7 +52,7 @@
 extern "C" {
 #endif
 
-#define AFS_ABI_VERSION 3
+#define AFS_ABI_VERSION 4
 #define AFS_NUM_TUBE_SECTIONS 40   /* Tube::NUM_PHARYNX_MOUTH_SECTIONS (Tube.h:56-58) */
 #define AFS_NUM_GLOTTIS_PARAMS 6   /* TriangularGlottis::NUM_CONTROL_PARAMS (TriangularGlottis.h:26-35) */
 #define AFS_NUM_AF_PARAMS 16       /* OneDimAreaFunction::NUM_AF_PARAMS (OneDimAreaFunction.h:34-43) */
@@ -103,13 +107,16 @@ typedef struct afs_options {
 } afs_options;
 
 #define AFS_ASYNC 0x1u
+/* Record an event pair around every kernel launch of the synthesis calls; afs_kernel_times
+ * returns their summed durations (measurement only: a few microseconds per launch). */
+#define AFS_PROFILE 0x2u
 
 typedef struct afs_config {
   double sampling_rate_hz; /* reference: 22050 (Constants.h:22-26); any rate is accepted */
   int32_t precision;       /* afs_precision */
   int32_t solver;          /* afs_solver */
   int32_t device;          /* HIP device ordinal */
-  uint32_t flags;          /* AFS_ASYNC */
+  uint32_t flags;          /* AFS_ASYNC | AFS_PROFILE */
   afs_options options;
 } afs_config;
 
@@ -210,6 +217,50 @@ afs_status afs_play_target_sequences(afs_ctx *ctx, const double *shapes, int32_t
                                      const int32_t *targets, const afs_target_sequence *ts,
                                      const uint32_t *seeds, int32_t B, double *out, uint8_t *nonfinite,
                                      afs_report *report);
+
+/* AFS_PROFILE contexts: summed device time and count of the synthesis-kernel launches and of
+ * the noise-source plan launches (tree solver, K5) since the previous call (waits for the
+ * stream).  Any pointer may be NULL. */
+afs_status afs_kernel_times(afs_ctx *ctx, double *synth_ms, int32_t *synth_launches, double *plan_ms,
+                            int32_t *plan_launches);
+
+/* ---- Several GPUs: utterance shards, the int16 audio gathered over RCCL (xGMI) ----------
+ * Utterances are independent: shard r of `world` synthesizes a contiguous block with no
+ * exchange; the only collective is the gather of the finished audio to rank 0.  RCCL
+ * (librccl.so.1 of the ROCm installation) is loaded on first use. */
+#define AFS_COMM_ID_BYTES 128 /* NCCL_UNIQUE_ID_BYTES */
+typedef struct afs_comm afs_comm;
+
+/* Block of `rank`: utterances [*first, *first + *count) of `total` over `world` ranks (the first
+ * total % world ranks take one more). */
+void afs_shard_range(int64_t total, int32_t world, int32_t rank, int64_t *first, int64_t *count);
+/* One process per GPU: rank 0 creates the id (ncclGetUniqueId) and hands it to the other
+ * ranks over any channel; every rank then joins with its context (device, stream). */
+afs_status afs_comm_unique_id(uint8_t id[AFS_COMM_ID_BYTES]);
+afs_status afs_comm_create(afs_ctx *ctx, const uint8_t id[AFS_COMM_ID_BYTES], int32_t rank, int32_t world,
+                           afs_comm **comm);
+/* One process, n GPUs: comms[i] = rank i on ctxs[i]'s device (ncclCommInitAll). */
+afs_status afs_comm_create_all(afs_ctx *const *ctxs, int32_t n, afs_comm **comms);
+void afs_comm_destroy(afs_comm *comm);
+/* Gather `count` int16 samples (device memory of this rank's context) to rank 0's root_out
+ * (device memory): rank r's block lands at the sum of the counts of ranks < r.  root_counts
+ * (rank 0, world entries; NULL = every rank sends `count`).  The transfer runs on the comm's own
+ * stream after the work queued so far on the context's stream, so the next synthesis overlaps
+ * it; afs_comm_fence makes the context's stream wait for it (before local or root_out is
+ * written again), afs_comm_synchronize waits on the host. */
+afs_status afs_gather_pcm(afs_comm *comm, const int16_t *local, int64_t count, int16_t *root_out,
+                          const int64_t *root_counts);
+afs_status afs_comm_fence(afs_comm *comm);
+afs_status afs_comm_synchronize(afs_comm *comm);
+/* The whole node from one host thread: `batch` utterances sharded over the n contexts of comms
+ * (afs_comm_create_all) with afs_shard_range; each shard runs afs_synthesize on its GPU (seeds
+ * keep the global index: NULL = u + 1), is converted to int16 on its GPU (afs_to_int16) and
+ * gathered to ctxs[0]'s GPU.  frames[batch][num_frames] and seeds are host arrays; pcm_out
+ * [batch][(num_frames-1)*hop] is host memory or device memory of ctxs[0]; nonfinite (host,
+ * batch bytes) and report may be NULL.  Returns when pcm_out is complete. */
+afs_status afs_multi_synthesize(afs_ctx *const *ctxs, afs_comm *const *comms, int32_t n, const afs_frame *frames,
+                                const uint32_t *seeds, int32_t batch, int32_t num_frames, int32_t hop,
+                                int16_t *pcm_out, uint8_t *nonfinite, afs_report *report);
 
 #ifdef __cplusplus
 }

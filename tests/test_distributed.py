@@ -44,13 +44,13 @@ def _worker(rank, world, port, q):
     out = _standin(w)
     got = sharding.gather_to_rank0(out, world, rank, dist)
     pcm = []
-    pg = sharding.PcmGather(_to_int16, out.shape, world, rank, dist, depth=2)
+    pg = sharding.PcmGather(_to_int16, out.shape, world, rank, sharding.TorchTransport(dist, world, rank), depth=2)
     for scale in (0.5, -3.0, 1.0):  # three steps through two rotating buffers
         slot = pg.submit(torch.sin(out * 1e3) * scale)
         if slot == 1 or scale == 1.0:
             pg.drain()
             if rank == 0:
-                pcm.append(torch.cat(pg.result(slot)).numpy().copy())
+                pcm.append(pg.result(slot).reshape(-1, out.shape[1]).numpy().copy())
     t = torch.tensor([float(out.numel())], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks timing reduction
     if rank == 0:
@@ -92,3 +92,30 @@ def test_gloo_world2_gather_matches_single_process():
     assert len(pcm) == 2
     assert np.array_equal(pcm[0], Oracle().to_int16(x * -3.0).reshape(x.shape))  # step 2 (slot 1)
     assert np.array_equal(pcm[1], Oracle().to_int16(x).reshape(x.shape))  # step 3 reused slot 0
+
+
+def test_shard_gather_loopback(tmp_path):
+    """afs_gather.h -- the shard and gather logic libafs.so drives over RCCL -- over an
+    in-process loopback transport (one thread per rank): uneven shards, world 1..8."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "gather_main")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-pthread",
+                           "-I", os.path.join(root, "areafunctionsynthesis_amd", "csrc"),
+                           os.path.join(root, "tests", "cpp", "gather_main.cpp"), "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+    assert out.strip() == "gather-ok"
+
+
+def test_library_shard_range_matches():
+    """afs_shard_range (the C ABI export) partitions exactly like afs_gather.h."""
+    from areafunctionsynthesis_amd.synthesizer import shard_range
+    for total, world in ((65536, 8), (10, 3), (7, 8), (0, 2)):
+        nxt = 0
+        for r in range(world):
+            f, n = shard_range(total, world, r)
+            assert f == nxt
+            nxt += n
+            assert n in (total // world, total // world + 1)
+        assert nxt == total
+    assert shard_range(65536, 8, 3) == (3 * 8192, 8192)

@@ -1,0 +1,78 @@
+"""Several GPUs through the C ABI (afs_comm_*, afs_gather_pcm, afs_multi_synthesize) and the
+launch timing bench.py reads (afs_kernel_times).
+
+The GPU box has one device, so the RCCL communicators here have one rank: the gather is the
+local copy and afs_multi_synthesize runs one shard.  That still drives every library call of
+the multi-GPU path on the hardware (RCCL loaded and initialised, the gather's stream and
+events, the shard offsets); the N > 1 exchange itself is covered by the loopback test of the
+same gather logic (tests/test_distributed.py) and is unmeasured on hardware.
+"""
+import numpy as np
+import pytest
+
+from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS
+from areafunctionsynthesis_amd.params import default_shapes
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(oracle, B, F):
+    sh = default_shapes()
+    names = ("a:", "s", "i:", "f", "u:")
+    frames = np.stack([np.repeat(oracle.af_to_frame(sh[names[u % len(names)]])[None], F) for u in range(B)])
+    frames["glottis"] = DEFAULT_GLOTTIS
+    frames["glottis"][:, :, 0] += np.arange(B)[:, None]
+    frames["velum_opening_cm2"][1::2] = 0.5
+    return frames
+
+
+def test_kernel_times_count_every_launch(oracle):
+    from areafunctionsynthesis_amd.synthesizer import Context
+    ctx = Context(44100.0, profile=True)
+    frames = _frames(oracle, 6, 5)
+    ctx.synthesize(frames, 441)
+    kt = ctx.kernel_times()
+    assert kt["synth_launches"] >= 1 and kt["synth_ms"] > 0.0
+    assert kt["plan_launches"] == kt["synth_launches"]  # one noise-source plan per tree launch
+    assert ctx.kernel_times() == {"synth_ms": 0.0, "synth_launches": 0, "plan_ms": 0.0, "plan_launches": 0}
+    ctx.close()
+    plain = Context(44100.0)
+    with pytest.raises(Exception):
+        plain.kernel_times()  # AFS_PROFILE off
+    plain.close()
+
+
+def test_comm_gather_one_rank():
+    import torch
+    from areafunctionsynthesis_amd.synthesizer import Comm, Context, comm_unique_id
+    ctx = Context(44100.0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    comm = Comm(ctx, comm_unique_id(), 0, 1)
+    x = torch.arange(-5000, 5000, dtype=torch.int16, device="cuda")
+    root = torch.zeros_like(x)
+    comm.gather_pcm(x, root)
+    comm.fence()
+    comm.synchronize()
+    assert torch.equal(root, x)
+    comm.close()
+    ctx.close()
+
+
+def test_multi_synthesize_equals_single_device(oracle):
+    """afs_multi_synthesize (shard, synthesize, int16, RCCL gather) over the box's device gives
+    the int16 audio of afs_synthesize + afs_to_int16, with global seeds u + 1."""
+    from areafunctionsynthesis_amd.synthesizer import Context, Node
+    B, F, hop = 7, 4, 300
+    frames = _frames(oracle, B, F)
+    node = Node(44100.0, [0])
+    pcm, rep = node.synthesize(frames, hop, report=True)
+    ctx = Context(44100.0)
+    y = ctx.synthesize(frames, hop)
+    ref = ctx.to_int16(y)
+    assert pcm.shape == (B, (F - 1) * hop)
+    assert np.array_equal(pcm, ref)
+    assert rep["samples"] == B * (F - 1) * hop and rep["nonfinite_utterances"] == 0
+    seeds = np.arange(11, 11 + B, dtype=np.uint32)
+    assert np.array_equal(node.synthesize(frames, hop, seeds=seeds), ctx.to_int16(ctx.synthesize(frames, hop, seeds=seeds)))
+    node.close()
+    ctx.close()

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = _native.load()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.afs_abi_version() == 3
+    assert lib.afs_abi_version() == 4
 
 
 def test_config_defaults_mirror_tdsmodel_options():

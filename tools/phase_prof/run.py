@@ -12,8 +12,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", ".."))
 
-PHASES = ["geometry+targets", "network", "n:filter", "n:act", "n:rng", "rows", "forward", "backward", "update",
-          "output"]
+PHASES = ["geometry", "network", "n:filter", "n:act", "n:rng", "rows", "forward", "backward", "update",
+          "output", "targets"]
 
 
 def main():

@@ -44,13 +44,21 @@ def main() -> None:
     kib = 1024.0
     fetch_b = 2.0 * kib * sum(fetch) / len(fetch)   # gfx950: FETCH_SIZE = half the read bytes
     write_b = kib * sum(write) / len(write)
+    plan_f = per_launch(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"), "plan_kernel")
+    plan_w = per_launch(os.path.join(a.dir, "pmc_write", "run_counter_collection.csv"), "plan_kernel")
     entry = {
         "tag": a.tag,
+        "launches": len(fetch),
         "fetch_size_kib": fetch, "write_size_kib": write,
         "read_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
         "traffic_bytes_per_launch": fetch_b + write_b,
-        "correction": "read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE; KiB -> bytes",
+        "correction": "read = 2 x FETCH_SIZE (gfx950; calibrated for this kernel's read patterns -- 8-B loads of "
+                      "16-lane rows, 16-B loads, lane-0 8-B loads -- by tools/microbench/fetch_calib: each reports "
+                      "half the bytes of the 128-B lines it reads, profiles/r02_fetch_calib.txt), write = WRITE_SIZE; "
+                      "KiB -> bytes",
     }
+    if plan_f and plan_w:  # K5, the noise-source plan producer of the same launches
+        entry["plan_kernel_traffic_bytes_per_launch"] = 2.0 * kib * sum(plan_f) / len(plan_f) + kib * sum(plan_w) / len(plan_w)
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     db = json.load(open(path)) if os.path.exists(path) else {}
     db[key(a.kernel, a.workload, a.batch, a.samples, a.hop)] = entry
