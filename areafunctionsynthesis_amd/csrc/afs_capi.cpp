@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -71,9 +72,10 @@ bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_T
 
 bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE; }
 
-// Bytes of noise-source plans one tree launch may use; a launch covers at most
-// PLAN_BUDGET / (rows * 128 B) samples (4096 samples at 8192 rows).
-constexpr int64_t PLAN_BUDGET = (int64_t)4 << 30;
+// Bytes of noise-source plans one tree launch may use (afs_ctx::plan_budget, set at create: a
+// quarter of the free device memory, at least 4 GiB; AFS_PLAN_BUDGET_MB overrides it); a
+// launch covers at most plan_budget / (rows * 128 B) samples and at most 65536.
+constexpr int64_t PLAN_BUDGET_MIN = (int64_t)4 << 30;
 
 // Launch the synthesis of frame transitions 1 .. ntrans (frames[row * fstride + k], k = 0 the
 // latched frame) in chunks that keep each kernel well below a second; state is carried
@@ -104,7 +106,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
                       const int32_t *frame_row = nullptr) {
   if (tree(c)) {
     const int64_t S = (int64_t)ntrans * hop;
-    const int64_t per = std::max<int64_t>(1, std::min<int64_t>({S, 65536, PLAN_BUDGET / ((int64_t)rows * afs::PLAN_RECORD_BYTES)}));
+    const int64_t per = std::max<int64_t>(1, std::min<int64_t>({S, 65536, c->plan_budget / ((int64_t)rows * afs::PLAN_RECORD_BYTES)}));
     afs_status st = ensure(c, &c->plan, &c->plan_bytes, (size_t)rows * (size_t)per * afs::PLAN_RECORD_BYTES);
     if (st != AFS_OK) return st;
     for (int64_t s0 = 0; s0 < S; s0 += per) {
@@ -250,6 +252,16 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
     return bail(AFS_ERR_OUT_OF_MEMORY);
   *ctx->hcount = 0;
   if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return bail(AFS_ERR_HIP);
+  {
+    size_t free_b = 0, total_b = 0;
+    ctx->plan_budget = PLAN_BUDGET_MIN;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+      ctx->plan_budget = std::max<int64_t>(PLAN_BUDGET_MIN, (int64_t)(free_b / 4));
+    if (const char *e = std::getenv("AFS_PLAN_BUDGET_MB")) {
+      const long long mb = std::atoll(e);
+      if (mb > 0) ctx->plan_budget = (int64_t)mb << 20;
+    }
+  }
   (void)st;
   *out = ctx;
   return AFS_OK;

@@ -33,6 +33,7 @@ struct afs_ctx {
   size_t tgt_bytes = 0;
   void *plan = nullptr;   // tree solver: noise-source plans of one launch (tree_plan.h)
   size_t plan_bytes = 0;
+  int64_t plan_budget = 0;  // bytes of plans one launch may use (afs_capi.cpp)
   void *stage_nf = nullptr;  // per-utterance non-finite flags staged for a host array
   size_t stage_nf_bytes = 0;
   // afs_multi_synthesize: this device's shard of float audio, its int16 audio, its flags, and

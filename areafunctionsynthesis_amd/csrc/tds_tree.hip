@@ -19,13 +19,16 @@ __global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_synth_kerne
 // (hops >= 128), the frames are staged in LDS first: the plan's scans read every section's
 // area / length / articulator several times, and from LDS those reads cost a fraction of the
 // cache-hit latency of global loads.  Shorter hops (target sequences, hop 1) read the frames
-// from global memory.  Each thread writes its 128-B record as 8 16-byte stores.
-constexpr int PLAN_BLOCK = 256, PLAN_STAGE = 4;
+// from global memory.  The block's records are contiguous in memory: they are assembled in LDS
+// and written with one 16-byte store per lane and step over the whole range (a thread's own
+// 128-B record written directly would spread each store instruction over 64 lines).
+constexpr int PLAN_BLOCK = 256, PLAN_STAGE = 4, PLAN_PITCH = PLAN_WORDS + 1;  // (odd pitch: fewer bank conflicts)
 constexpr int FRAME_WORDS = (int)(sizeof(afs_frame) / 8);
 static_assert(sizeof(afs_frame) % 8 == 0, "frames are copied as 8-byte words");
 
 __global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
   __shared__ uint64_t fr_lds[PLAN_STAGE][FRAME_WORDS];
+  __shared__ uint64_t rec_lds[PLAN_BLOCK * PLAN_PITCH];
   const int64_t n = a.s_end - a.s_begin;
   const int64_t row = blockIdx.x;
   const int64_t t_first = (int64_t)blockIdx.y * PLAN_BLOCK;
@@ -41,17 +44,25 @@ __global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
     for (int w = threadIdx.x; w < words; w += PLAN_BLOCK) (&fr_lds[0][0])[w] = src[w];
     __syncthreads();
   }
-  if (t >= n) return;  // (after the block's only barrier)
-  const int64_t s = a.s_begin + t;
-  const int64_t k = s / a.hop + 1;
-  const int i = (int)(s - (k - 1) * a.hop);
-  const afs_frame *fl = staged ? (const afs_frame *)fr_lds[k - 1 - k_lo] : f + (k - 1);
-  const afs_frame *fr = staged ? (const afs_frame *)fr_lds[k - k_lo] : f + k;
-  uint64_t w[PLAN_WORDS];
-  plan_sample(fl, fr, (double)i / (double)a.hop, a.tab->consts.sec, a.two_mass != 0, w);
-  ulonglong2 *o = (ulonglong2 *)(a.plan + (row * a.plan_stride + t) * PLAN_WORDS);
+  if (t < n) {
+    const int64_t s = a.s_begin + t;
+    const int64_t k = s / a.hop + 1;
+    const int i = (int)(s - (k - 1) * a.hop);
+    const afs_frame *fl = staged ? (const afs_frame *)fr_lds[k - 1 - k_lo] : f + (k - 1);
+    const afs_frame *fr = staged ? (const afs_frame *)fr_lds[k - k_lo] : f + k;
+    uint64_t w[PLAN_WORDS];
+    plan_sample(fl, fr, (double)i / (double)a.hop, a.tab->consts.sec, a.two_mass != 0, w);
 #pragma unroll
-  for (int q = 0; q < PLAN_WORDS / 2; ++q) o[q] = make_ulonglong2(w[2 * q], w[2 * q + 1]);
+    for (int q = 0; q < PLAN_WORDS; ++q) rec_lds[threadIdx.x * PLAN_PITCH + q] = w[q];
+  }
+  __syncthreads();
+  // the block's (t_last - t_first + 1) records, 16 bytes per lane and step
+  const int chunks = (int)(t_last - t_first + 1) * (PLAN_WORDS / 2);
+  ulonglong2 *o = (ulonglong2 *)(a.plan + (row * a.plan_stride + t_first) * PLAN_WORDS);
+  for (int c = threadIdx.x; c < chunks; c += PLAN_BLOCK) {
+    const int r = c / (PLAN_WORDS / 2), q = 2 * (c % (PLAN_WORDS / 2));
+    o[c] = make_ulonglong2(rec_lds[r * PLAN_PITCH + q], rec_lds[r * PLAN_PITCH + q + 1]);
+  }
 }
 
 // seeds == nullptr: utterance u is seeded u + 1 (afs.h)

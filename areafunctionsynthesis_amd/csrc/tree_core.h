@@ -542,6 +542,10 @@ AFS_HD inline GlotOut phase_glottis(double *X, const Consts &C, double ratio) {
     X[X_GP + 5] = GLOTTIS_DEFAULT_ASPIRATION_DB;  // X_GP + 5 is read as the aspiration strength
     return two_mass_glottis(X, C, gp);
   } else {
+#if defined(AFS_EXP_NO_GLOTTIS)  // timing experiment only (tools/phase_prof): no glottis work
+    (void)r1;
+    return GlotOut{0.1 + 1e-3 * ratio, 0.1, 0.3, 0.3};
+#endif
     double gp[6];
     for (int k = 0; k < 6; ++k) {
       gp[k] = r1 * X[X_FRAME + 4 + k] + ratio * X[X_FRAME + 10 + k];
@@ -662,6 +666,12 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     const double len = glot ? (s == S_GLOT_LO ? go.l0 : go.l1) : R.lcur[j];
     // prepareTimeStep's section quantities (TdsModel.cpp:732-834), with the repeated
     // divisions folded into one reciprocal of the area and one of the wall surface.
+#if defined(AFS_EXP_NO_NETGEO)  // timing experiment only (tools/phase_prof): no geometric chains
+    const double inv_area = area, r0 = area * 0.5641895835, Rr = len * 1e-3, L = len * area, alw = 1e-3 * area,
+                 E = 1e-3 * len, c1 = 1e-3, c2 = 2e-3, c3 = 3e-3;
+    const double bew = alw * (R.w[j] * c1 + R.wr[j] * c2 + R.wr2[j] * c3);
+    (void)idt; (void)idt2;
+#else
     const double vol = area * len;
     const double inv_area = fast_rcp(area);
     const double r0 = fast_sqrt(area * (1.0 / PI));
@@ -685,6 +695,12 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     const bool walls = opt.soft_walls && !glot;
     const double alpha = walls ? alw : 0.0, beta = walls ? bew : 0.0;
     const double E = fast_div(dt * TH, Cc + alpha);
+#endif
+#if defined(AFS_EXP_NO_NETGEO)
+    const bool walls = opt.soft_walls && !glot;
+    const double alpha = walls ? alw : 0.0, beta = walls ? bew : 0.0;
+    (void)dt;
+#endif
     double R0 = Rr, R1 = Rr;
     // Bernoulli losses between pharynx/mouth sections (TdsModel.cpp:850-877)
     const bool turb = opt.turbulence_losses && pm;

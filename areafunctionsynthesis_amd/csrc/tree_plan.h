@@ -80,12 +80,6 @@ struct PlanGeom {
   AFS_HD double len(int m) const { return r1 * fl->length_cm[m] + ratio * fr->length_cm[m]; }
   AFS_HD double lat(int m) const { return r1 * fl->laterality[m] + ratio * fr->laterality[m]; }
   AFS_HD int art(int m) const { return fl->articulator[m]; }  // the left tube's (Tube.cpp:452)
-  // position of section m: the sequential sum of Tube::calcPositions (:611-622)
-  AFS_HD double pos(int m) const {
-    double p = 0.0;
-    for (int i = 0; i < m; ++i) p += len(i);
-    return p;
-  }
   // first section with the articulator and the smallest area (strict "<", from 1e6), -1: none
   AFS_HD int argmin(int a, double &amin, int skip_lo = 1, int skip_hi = 0) const {
     int n = -1;
@@ -113,29 +107,80 @@ struct PlanGeom {
       if (lat(m) > l) l = lat(m);
     return l;
   }
-  // first section whose extent contains the obstacle (:1462-1471), -1: none; *p its position
-  AFS_HD int obstacle(double obst, double *p_out) const {
-    double p = 0.0;
-    for (int m = 0; m < NPM; ++m) {
-      const double l = len(m);
-      if (p <= obst && p + l >= obst) { *p_out = p; return m; }
-      p += l;
-    }
-    return -1;
-  }
 };
 
 // The plan of the sample at `ratio` between frames fl and fr.  sec: the kernel tables' section
 // records (X_UN offsets of the section outputs).  two_mass: the glottis is the TwoMassModel,
 // whose aspiration strength is Glottis::DEFAULT_ASPIRATION_STRENGTH_DB.
+// The reference's scans (argmin, extent, position, obstacle) are merged into four passes over
+// the 40 sections: the narrowest tongue and lip sections together, the second tongue
+// constriction, one running position sum for every position the obstacles need, and one
+// obstacle search for all four constrictions.  Every value is the one the separate scans give
+// (the same comparisons and the same sequential sums).
 AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double ratio, const SecRec *sec,
                                bool two_mass, uint64_t *w) {
   const PlanGeom g{fl, fr, 1.0 - ratio, ratio};
   const double teeth = g.r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm;
   const double asp_db = two_mass ? GLOTTIS_DEFAULT_ASPIRATION_DB : g.r1 * fl->glottis[5] + ratio * fr->glottis[5];
-  // position of the obstacle of a tongue constriction ending at `last` (:1283-1299)
-  auto tongue_obstacle = [&](int last, int narrow, double &min_teeth) {
-    const double pl = g.pos(last);
+
+  // narrowest tongue section (:1228-1240) and narrowest lower-lip section (:1399-1410): the
+  // first strict minimum from 1e6
+  int n1 = -1, nl = -1;
+  double amin1 = 1000000.0, aminl = 1000000.0;
+  for (int m = 0; m < NPM; ++m) {
+    const double A = g.area(m);
+    const int a = g.art(m);
+    if (a == TONGUE && A < amin1) { amin1 = A; n1 = m; }
+    if (a == LOWER_LIP && A < aminl) { aminl = A; nl = m; }
+  }
+  // tongue constriction 1 (:1228-1302)
+  const bool has_t1 = amin1 < 1.0;
+  int f1 = 0, l1 = -1;
+  double lat1 = 0.0, obst1 = 0.0;
+  if (has_t1) {
+    g.grow(n1, amin1, TONGUE, f1, l1);
+    lat1 = g.max_lat(f1, l1);
+  }
+  // tongue constriction 2 (:1309-1392), kept when it does not touch the first
+  bool has_t2 = false;
+  int n2 = -1, l2 = -1;
+  double lat2 = 0.0, obst2 = 0.0;
+  if (has_t1) {
+    double amin2;
+    n2 = g.argmin(TONGUE, amin2, f1, l1);
+    if (amin2 < 1.0) {
+      int f2;
+      g.grow(n2, amin2, TONGUE, f2, l2);
+      if (f2 > l1 + 1 || l2 < f1 - 1) {
+        has_t2 = true;
+        lat2 = g.max_lat(f2, l2);
+      }
+    }
+  }
+  // extent of the lip constriction (:1399-1444)
+  const bool lip_c = aminl < 1.0;
+  int ll = -1;
+  if (lip_c) {
+    int fl_;
+    g.grow(nl, aminl, LOWER_LIP, fl_, ll);
+  }
+  // positions of sections l1, l2 and ll + 1: Tube::calcPositions' sequential sum (:611-622)
+  const int i1 = has_t1 ? l1 : -1, i2 = has_t2 ? l2 : -1, i3 = lip_c ? ll + 1 : -1;
+  const int imax = i1 > i2 ? (i1 > i3 ? i1 : i3) : (i2 > i3 ? i2 : i3);
+  double P1 = 0.0, P2 = 0.0, P3 = 0.0;
+  {
+    double p = 0.0;
+    for (int m = 0; m <= imax; ++m) {
+      if (m == i1) P1 = p;
+      if (m == i2) P2 = p;
+      if (m == i3) P3 = p;
+      p += g.len(m);
+    }
+  }
+  // obstacles of the tongue constrictions (:1283-1299): the teeth when the jet ends within
+  // 2 cm of them, else the middle of the section after the constriction
+  double min_teeth = 1000000.0;
+  auto tongue_obstacle = [&](double pl, int last, int narrow) {
     const double jet = pl + g.len(last);
     if (teeth - jet < 2.0) {
       min_teeth = g.area(narrow);
@@ -143,59 +188,38 @@ AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double 
     }
     return (pl + g.len(last)) + 0.5 * g.len(last + 1);  // pos[last + 1] + 0.5 len[last + 1]
   };
-
-  // tongue constriction 1 (:1228-1302)
-  double min_teeth = 1000000.0, amin1;
-  const int n1 = g.argmin(TONGUE, amin1);
-  const bool has_t1 = amin1 < 1.0;
-  int f1 = 0, l1 = -1;
-  double lat1 = 0.0, obst1 = 0.0;
-  if (has_t1) {
-    g.grow(n1, amin1, TONGUE, f1, l1);
-    lat1 = g.max_lat(f1, l1);
-    obst1 = tongue_obstacle(l1, n1, min_teeth);
-  }
-  // tongue constriction 2 (:1309-1392), kept when it does not touch the first
-  bool has_t2 = false;
-  int n2 = -1;
-  double lat2 = 0.0, obst2 = 0.0;
-  if (has_t1) {
-    double amin2;
-    n2 = g.argmin(TONGUE, amin2, f1, l1);
-    if (amin2 < 1.0) {
-      int f2, l2;
-      g.grow(n2, amin2, TONGUE, f2, l2);
-      if (f2 > l1 + 1 || l2 < f1 - 1) {
-        has_t2 = true;
-        lat2 = g.max_lat(f2, l2);
-        obst2 = tongue_obstacle(l2, n2, min_teeth);
-      }
-    }
-  }
-  // lower lip (:1399-1444): narrower than a tongue constriction at the teeth
-  double aminl;
-  const int nl = g.argmin(LOWER_LIP, aminl);
-  const bool has_l = aminl < 1.0 && aminl < min_teeth;
-  double obstl = 0.0;
-  if (has_l) {
-    int fl_, ll;
-    g.grow(nl, aminl, LOWER_LIP, fl_, ll);
-    obstl = g.pos(ll + 1);
-  }
+  if (has_t1) obst1 = tongue_obstacle(P1, l1, n1);
+  if (has_t2) obst2 = tongue_obstacle(P2, l2, n2);
+  // the lower lip counts when narrower than a tongue constriction at the teeth
+  const bool has_l = lip_c && aminl < min_teeth;
+  const double obstl = has_l ? P3 : 0.0;
 
   // obstacle sections and source weights (:1456-1499)
   const double obst[4] = {1.5, obst1, obst2, obstl};
   const bool has[4] = {true, has_t1, has_t2, has_l};
   uint32_t flags = 0, up[4] = {0, 0, 0, 0};
   double fdn[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int c = 0; c < 4; ++c) {
-    if (!has[c]) continue;
+  {  // the first section whose extent contains each obstacle (:1462-1471), one pass for all four
+    int mo[4] = {-1, -1, -1, -1};
+    double po[4] = {0.0, 0.0, 0.0, 0.0};
     double p = 0.0;
-    const int m = g.obstacle(obst[c], &p);
-    if (m < 0) continue;
-    flags |= 1u << c;
-    up[c] = (uint32_t)m;
-    fdn[c] = (obst[c] - p) / g.len(m);
+    for (int m = 0; m < NPM; ++m) {
+      const double l = g.len(m);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (has[c] && mo[c] < 0 && p <= obst[c] && p + l >= obst[c]) {
+          mo[c] = m;
+          po[c] = p;
+        }
+      p += l;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (mo[c] < 0) continue;
+      flags |= 1u << c;
+      up[c] = (uint32_t)mo[c];
+      fdn[c] = (obst[c] - po[c]) / g.len(mo[c]);
+    }
   }
   if (lat1 > 0.1) flags |= PF_T1_LAT;
   if (lat2 > 0.1) flags |= PF_T2_LAT;

@@ -58,3 +58,49 @@ def test_adapter_single_voice_vs_oracle(adapter_bin, oracle, tmp_path):
     x = oracle.utterance(frames, hop, seed, fs)
     assert y.shape == x.shape == ((len(frames) - 1) * hop,)
     assert np.abs(y - x).max() <= 1e-9
+
+
+REF_BACKEND = "/root/reference/src/Backend"
+REF_TUBE_O = os.path.join(ROOT, "oracle", "_ref", "obj", "Tube.o")
+
+
+@pytest.fixture(scope="module")
+def tube_bin(tmp_path_factory):
+    if not (os.path.isdir(REF_BACKEND) and os.path.exists(REF_TUBE_O)):
+        pytest.skip("the reference's Tube (/root/reference + oracle/_ref) is not available here")
+    exe = str(tmp_path_factory.mktemp("tube") / "tube_main")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-w", "-I", REF_BACKEND, "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "tube_main.cpp"), REF_TUBE_O, "-o", exe])
+    return exe
+
+
+def test_frame_from_reference_tube(tube_bin, oracle, tmp_path):
+    """afs::frame_from_tube<Tube> on the reference's own Tube class, filled through
+    Tube::setPharynxMouthGeometry / setVelumOpening (Tube.cpp:323-349, 402-416): the frame holds
+    exactly what those setters store (areas and velum clamped at MIN_AREA_CM2 = 0.001, Tube.cpp:337,
+    413), and that frame synthesizes bit for bit like the caller's original input."""
+    sh = default_shapes()
+    rng = np.random.default_rng(5)
+    names = ["a:", "s", "i:", "(a)b(a):", "S", "u:", "f", "x"]
+    frames = np.stack([oracle.af_to_frame(sh[n]) for n in names])
+    frames["glottis"] = DEFAULT_GLOTTIS
+    frames["velum_opening_cm2"] = [0.0, 1.0, 0.5, 1e-5, 0.25, 0.0, 2.0, 0.0005]
+    frames["laterality"][:, 20:30] = rng.random((len(names), 10)) * 0.3
+    frames["area_cm2"][2, 5] = 1e-6          # below MIN_AREA: the setter clamps
+    frames["area_cm2"][4, 39] = 0.0
+    src, dst = tmp_path / "in.bin", tmp_path / "out.bin"
+    with open(src, "wb") as fh:
+        fh.write(np.array([len(frames)], np.int32).tobytes())
+        fh.write(np.ascontiguousarray(frames, FRAME_DTYPE).tobytes())
+    out = subprocess.run([tube_bin, str(src), str(dst)], capture_output=True, text=True, check=True).stdout
+    assert out.strip() == f"ok {len(frames)}"
+    got = np.fromfile(dst, FRAME_DTYPE)
+    want = frames.copy()
+    want["area_cm2"] = np.maximum(want["area_cm2"], 0.001)
+    want["velum_opening_cm2"] = np.maximum(want["velum_opening_cm2"], 0.001)
+    assert got.tobytes() == np.ascontiguousarray(want, FRAME_DTYPE).tobytes()
+    # the synthesis clamps exactly as the Tube does, so the caller's frame and the Tube's agree
+    seq = np.stack([got[[0, 1, 3, 1]], frames[[0, 1, 3, 1]]])
+    x = oracle.utterance(seq[0], 97, 3, 44100.0)
+    y = oracle.utterance(seq[1], 97, 3, 44100.0)
+    assert np.array_equal(x, y)
