@@ -9,9 +9,11 @@ using namespace tree;
 
 namespace {
 
+// one kernel per glottis model (TriangularGlottis, the reference's; TwoMassModel)
+template <int MODEL>
 __global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_synth_kernel(TreeArgs a) {
   __shared__ WaveLds lds;
-  tree_synth_body<false>(a, lds, nullptr);
+  tree_synth_body<false, MODEL>(a, lds, nullptr);
 }
 
 // Grid (rows, sample blocks of PLAN_BLOCK): one thread per (frame row, sample), a block of
@@ -105,7 +107,10 @@ hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const u
 
 hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st) {
   if (a.B <= 0 || a.s_end <= a.s_begin) return hipSuccess;
-  hipLaunchKernelGGL(tree_synth_kernel, dim3((a.B + UPB - 1) / UPB), dim3(64 * WPB), 0, st, a);
+  if (a.uni.opt.glottis_model == AFS_GLOTTIS_TWO_MASS)
+    hipLaunchKernelGGL(tree_synth_kernel<AFS_GLOTTIS_TWO_MASS>, dim3((a.B + UPB - 1) / UPB), dim3(64 * WPB), 0, st, a);
+  else
+    hipLaunchKernelGGL(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR>, dim3((a.B + UPB - 1) / UPB), dim3(64 * WPB), 0, st, a);
   return hipGetLastError();
 }
 

@@ -280,14 +280,16 @@ AFS_HD inline double glottis_dipole_gain(double aspiration_db) {
 struct GlotOut { double a0, a1, l0, l1; };
 
 // TwoMassModel::calcGeometry / getTubeData (TwoMassModel.cpp:359-440) and incTime (:157-349)
-// on lane 0, with the previous sample's pressures X_P4; relative displacements in X_RELX
-// (current 0/1, previous 2/3) as for the triangular glottis.
-AFS_HD inline GlotOut two_mass_glottis(double *X, const Consts &C, const double *gp) {
+// from the interpolated controls gp, the pressures p4 = p[22..25] of the previous sample and the
+// relative displacements rel (current 0/1, previous 2/3, as for the triangular glottis); the new
+// displacements go to rel_out.
+AFS_HD inline GlotOut two_mass_glottis(const Consts &C, const double *gp, const double *p4, const double *rel,
+                                       double *rel_out) {
   double Q = 1.0 + (gp[0] - TM_NAT_F0) * (1.0 / TM_F0_DIV_Q);  // getTensionParameter (:467-485)
   if (Q < 0.05) Q = 0.05;
   const double f = fast_sqrt(Q), inv_f = fast_rcp(f), inv_q = fast_rcp(Q);
   const double len = TM_REST_LEN * f, th0 = TM_REST_THICK0 * inv_f, th1 = TM_REST_THICK1 * inv_f;
-  const double rel0 = X[X_RELX + 0], rel1 = X[X_RELX + 1];
+  const double rel0 = rel[0], rel1 = rel[1];
   const double rest0 = gp[2], rest1 = gp[3];
   // geometry
   double a0 = rest0 + rel0, a1 = rest1 + rel1;
@@ -311,7 +313,7 @@ AFS_HD inline GlotOut two_mass_glottis(double *X, const Consts &C, const double 
   if (ab0 <= crit) dr0 += 1.0;
   if (ab1 <= crit) dr1 += 1.0;
   const double r0 = 2.0 * dr0 * fast_sqrt(m0 * k0) * df * df, r1 = 2.0 * dr1 * fast_sqrt(m1 * k1) * df * df;
-  const double p0 = X[X_P4 + 0], p1 = X[X_P4 + 1], p2 = X[X_P4 + 2], p3 = X[X_P4 + 3];
+  const double p0 = p4[0], p1 = p4[1], p2 = p4[2], p3 = p4[3];
   const bool open0 = ab0 > TM_CRIT_WIDTH, open1 = ab1 > TM_CRIT_WIDTH;
   const double fp0 = open0 ? p1 : p0;
   const double fp1 = open1 ? p2 : (open0 ? p1 : p3);
@@ -326,15 +328,15 @@ AFS_HD inline GlotOut two_mass_glottis(double *X, const Consts &C, const double 
   const double B = -kc * T * T;
   const double Cq = -kc * T * T;
   const double D = m1 + r1 * T + T * T * (k1 + ck1) + kc * T * T;
-  const double E = fo0 * T * T + 2.0 * m0 * rel0 - m0 * X[X_RELX + 2] + r0 * T * rel0 + T * T * ck0 * min0 - nl0 * T * T;
-  const double F = fo1 * T * T + 2.0 * m1 * rel1 - m1 * X[X_RELX + 3] + r1 * T * rel1 + T * T * ck1 * min1 - nl1 * T * T;
+  const double E = fo0 * T * T + 2.0 * m0 * rel0 - m0 * rel[2] + r0 * T * rel0 + T * T * ck0 * min0 - nl0 * T * T;
+  const double F = fo1 * T * T + 2.0 * m1 * rel1 - m1 * rel[3] + r1 * T * rel1 + T * T * ck1 * min1 - nl1 * T * T;
   double det = A * D - B * Cq;
   if (fabs(det) < 0.000000001) det = 0.000000001;
   const double inv_det = fast_rcp(det);
-  X[X_RELX + 2] = rel0;
-  X[X_RELX + 3] = rel1;
-  X[X_RELX + 0] = (E * D - B * F) * inv_det;
-  X[X_RELX + 1] = (A * F - E * Cq) * inv_det;
+  rel_out[2] = rel0;
+  rel_out[3] = rel1;
+  rel_out[0] = (E * D - B * F) * inv_det;
+  rel_out[1] = (A * F - E * Cq) * inv_det;
   return go;
 }
 
@@ -528,30 +530,44 @@ AFS_HD inline void phase_interpolate(int gl, Lane<W> &R, double *X, const Consts
   }
 }
 
-// The glottis (lane-uniform inputs: every lane of the utterance computes the same values, see
-// Exec::par_uniform).
+// The glottis of one sample (lane-uniform inputs: every lane of the utterance computes the same
+// values, see Exec::par_uniform): calcGeometry at the interpolated controls with the current
+// displacements, then incTime with the pressures p4 = p[22..25] of the previous sample.  In
+// three steps -- the loads (glottis_inputs), the arithmetic (glottis_eval), the stores
+// (glottis_commit) -- so that the block can issue every load before its first store and the
+// glottis chain interleaves with the network (an LDS load after a store to the same block
+// cannot be moved above it).
+struct GlotIn { double fl[6], fr[6], rel[4]; };
+struct GlotRes { GlotOut go; double gp[6], rel[4]; };
+
+AFS_HD inline GlotIn glottis_inputs(const double *X) {
+  GlotIn in;
+  for (int k = 0; k < 6; ++k) {
+    in.fl[k] = X[X_FRAME + 4 + k];
+    in.fr[k] = X[X_FRAME + 10 + k];
+  }
+  for (int k = 0; k < 4; ++k) in.rel[k] = X[X_RELX + k];
+  return in;
+}
+
 template <int MODEL>
-AFS_HD inline GlotOut phase_glottis(double *X, const Consts &C, double ratio) {
+AFS_HD inline GlotRes glottis_eval(const GlotIn &in, const Consts &C, double ratio, const double *p4) {
   const double r1 = 1.0 - ratio;
+  GlotRes res;
+  double *gp = res.gp;
+  for (int k = 0; k < 6; ++k) gp[k] = r1 * in.fl[k] + ratio * in.fr[k];
   if constexpr (MODEL == AFS_GLOTTIS_TWO_MASS) {
-    double gp[6];
-    for (int k = 0; k < 6; ++k) {
-      gp[k] = r1 * X[X_FRAME + 4 + k] + ratio * X[X_FRAME + 10 + k];
-      X[X_GP + k] = gp[k];
-    }
-    X[X_GP + 5] = GLOTTIS_DEFAULT_ASPIRATION_DB;  // X_GP + 5 is read as the aspiration strength
-    return two_mass_glottis(X, C, gp);
+    res.go = two_mass_glottis(C, gp, p4, in.rel, res.rel);
+    gp[5] = GLOTTIS_DEFAULT_ASPIRATION_DB;  // X_GP + 5 is read as the aspiration strength
+    return res;
   } else {
 #if defined(AFS_EXP_NO_GLOTTIS)  // timing experiment only (tools/phase_prof): no glottis work
     (void)r1;
-    return GlotOut{0.1 + 1e-3 * ratio, 0.1, 0.3, 0.3};
+    res.go = GlotOut{0.1 + 1e-3 * ratio, 0.1, 0.3, 0.3};
+    for (int k = 0; k < 4; ++k) res.rel[k] = in.rel[k];
+    return res;
 #endif
-    double gp[6];
-    for (int k = 0; k < 6; ++k) {
-      gp[k] = r1 * X[X_FRAME + 4 + k] + ratio * X[X_FRAME + 10 + k];
-      X[X_GP + k] = gp[k];
-    }
-    double rel0 = X[X_RELX + 0], rel1 = X[X_RELX + 1];
+    const double rel0 = in.rel[0], rel1 = in.rel[1];
     // calcGeometry + getTubeData + Tube::setGlottisGeometry (TriangularGlottis.cpp:338-411)
     // (divisions sharing a denominator use one reciprocal; sqrt(m k) is a constant since
     // m ~ 1/q and k ~ q)
@@ -564,10 +580,10 @@ AFS_HD inline GlotOut phase_glottis(double *X, const Consts &C, double ratio) {
     double th0 = G_REST_THICK0 * inv_f, th1 = G_REST_THICK1 * inv_f;
     double olen[2], clen[2], ow[2], cz[2];
     glottis_open_close(gp, cord, rel0, rel1, olen, clen, ow, cz);
-    const GlotOut go{clampA(olen[0] * ow[0] + chink), clampA(olen[1] * ow[1] + chink), th0, th1};
+    res.go = GlotOut{clampA(olen[0] * ow[0] + chink), clampA(olen[1] * ow[1] + chink), th0, th1};
     // incTime (TriangularGlottis.cpp:154-330) with the previous sample's pressures
     const double Tt = C.h.Tt;
-    const double p0 = X[X_P4 + 0], p1 = X[X_P4 + 1], p2 = X[X_P4 + 2], p3 = X[X_P4 + 3];
+    const double p0 = p4[0], p1 = p4[1], p2 = p4[2], p3 = p4[3];
     double m0 = G_MASS0 * inv_q, m1 = G_MASS1 * inv_q;
     double al0 = clen[0] * inv_cord, al1 = clen[1] * inv_cord;
     double k0 = G_K0 * q, k1 = G_K1 * q, kc0 = G_KC0 * q, kc1 = G_KC1 * q;
@@ -584,17 +600,24 @@ AFS_HD inline GlotOut phase_glottis(double *X, const Consts &C, double ratio) {
     double B = -kcp * Tt * Tt;
     double Cq = -kcp * Tt * Tt;
     double Dq = m1 + rr1 * Tt + Tt * Tt * (k1 + kc1 * al1) + kcp * Tt * Tt;
-    double Ee = fo0 * Tt * Tt + 2.0 * m0 * rel0 - m0 * X[X_RELX + 2] + rr0 * Tt * rel0 - Tt * Tt * kc0 * al0 * rs0;
-    double Ff = fo1 * Tt * Tt + 2.0 * m1 * rel1 - m1 * X[X_RELX + 3] + rr1 * Tt * rel1 - Tt * Tt * kc1 * al1 * rs1;
+    double Ee = fo0 * Tt * Tt + 2.0 * m0 * rel0 - m0 * in.rel[2] + rr0 * Tt * rel0 - Tt * Tt * kc0 * al0 * rs0;
+    double Ff = fo1 * Tt * Tt + 2.0 * m1 * rel1 - m1 * in.rel[3] + rr1 * Tt * rel1 - Tt * Tt * kc1 * al1 * rs1;
     double det = A * Dq - B * Cq;
     if (fabs(det) < 0.000000001) det = 0.000000001;
     const double inv_det = fast_rcp(det);  // |det| >= 1e-9
-    X[X_RELX + 2] = rel0;
-    X[X_RELX + 3] = rel1;
-    X[X_RELX + 0] = (Ee * Dq - B * Ff) * inv_det;
-    X[X_RELX + 1] = (A * Ff - Ee * Cq) * inv_det;
-    return go;
+    res.rel[2] = rel0;
+    res.rel[3] = rel1;
+    res.rel[0] = (Ee * Dq - B * Ff) * inv_det;
+    res.rel[1] = (A * Ff - Ee * Cq) * inv_det;
+    return res;
   }
+}
+
+// The glottis state of the sample: new displacements, interpolated controls (X_GP + 1, the lung
+// pressure, is the row phase's source term of section 0).
+AFS_HD inline void glottis_commit(double *X, const GlotRes &r) {
+  for (int k = 0; k < 6; ++k) X[X_GP + k] = r.gp[k];
+  for (int k = 0; k < 4; ++k) X[X_RELX + k] = r.rel[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -1385,32 +1408,37 @@ AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, doub
 
 template <int W, int MODEL, bool VARLOSS, class Xc>
 AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
-  GlotOut go{};
+  // the glottis of this sample: its loads first, its stores (displacements, interpolated
+  // controls) at the end of the block, so that the network and the targets need not wait for
+  // the glottis chain before they load
+  GlotRes g{};
   x.par_uniform([&](int gl, Lane<W> &R) { phase_interpolate<W>(gl, R, X, C, ratio); },
-                [&](Lane<W> &R) { (void)R; go = phase_glottis<MODEL>(X, C, ratio); });
+                [&](Lane<W> &R) {
+                  (void)R;
+                  const double p4[4] = {X[X_P4 + 0], X[X_P4 + 1], X[X_P4 + 2], X[X_P4 + 3]};
+                  g = glottis_eval<MODEL>(glottis_inputs(X), C, ratio, p4);
+                });
   x.mark(PH_GEOMETRY);  // (phase marks: cycle accounting of tools/phase_prof, no-ops otherwise)
   x.dyn_neighbors();
-  x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS>(gl, R, X, U, C, go); });
+  x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS>(gl, R, X, U, C, g.go); });
   x.mark(PH_NETWORK);
-  x.par([&](int gl, Lane<W> &R) { phase_targets<W>(x, gl, R, X, C, go.a1); });
+  x.par([&](int gl, Lane<W> &R) { phase_targets<W>(x, gl, R, X, C, g.go.a1); });
+  x.par_uniform([&](int gl, Lane<W> &R) { (void)gl; (void)R; },
+                [&](Lane<W> &R) { (void)R; glottis_commit(X, g); });
 }
 
-template <int W, class Xc>
+// One audio sample at `ratio` with glottis model MODEL (one kernel per model: a kernel holding
+// both models' code needs more registers than the SIMD has).
+template <int W, int MODEL, class Xc>
 AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio, bool defer_out) {
   static_assert(W >= TREE_CHAINS, "every solver chain needs a lane of the utterance");
   // geometry and network in one block (no LDS round trip between them): the interpolated
   // areas stay in the lanes, the neighbours' come by lane exchange, the glottis values are
   // lane-uniform
   // (one instantiation per glottis model and entrance-loss kind: no option branch in the block)
-  const bool two_mass = U.opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
   const bool varloss = U.opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE;
-  if (two_mass) {
-    if (varloss) geometry_network<W, AFS_GLOTTIS_TWO_MASS, true>(x, X, U, C, ratio);
-    else geometry_network<W, AFS_GLOTTIS_TWO_MASS, false>(x, X, U, C, ratio);
-  } else {
-    if (varloss) geometry_network<W, AFS_GLOTTIS_TRIANGULAR, true>(x, X, U, C, ratio);
-    else geometry_network<W, AFS_GLOTTIS_TRIANGULAR, false>(x, X, U, C, ratio);
-  }
+  if (varloss) geometry_network<W, MODEL, true>(x, X, U, C, ratio);
+  else geometry_network<W, MODEL, false>(x, X, U, C, ratio);
   x.sync();
   x.mark(PH_TARGETS);
   if (U.opt.generate_noise_sources) {
@@ -1457,6 +1485,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.mark(PH_UPDATE);
   x.mark(PH_OUTPUT);
 }
+
 
 }  // namespace tree
 }  // namespace afs

@@ -152,7 +152,7 @@ struct WaveLds {
 };
 
 // prof (PROF only): per wave, PH_COUNT cycle sums (s_memtime) over the launch.
-template <bool PROF>
+template <bool PROF, int MODEL>
 __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds, uint64_t *prof) {
   const int lane = threadIdx.x;  // 0 .. 64 WPB - 1
   const int g = lane / TW, gl = lane % TW;
@@ -193,7 +193,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
     R.planw = next;
     next = pl[(t + 1 < n ? t + 1 : t) * PLAN_WORDS];  // the next sample's word, a sample ahead
     const double ratio = (double)i / (double)hop;
-    sample_step<TW>(ex, X, a.uni, C, ratio, defer);
+    sample_step<TW, MODEL>(ex, X, a.uni, C, ratio, defer);
     if (valid && gl == 0) o[t] = R.sample;
     if (++i == hop) {
       if (defer && valid && gl == 0) output_filter_run(X, C, o + t0, (int)(t + 1 - t0));

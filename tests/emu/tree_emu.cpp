@@ -83,7 +83,10 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
       uint64_t w[PLAN_WORDS];  // K5's record of this sample (tree_plan.h)
       plan_sample(frames + k - 1, frames + k, ratio, T.consts.sec, opt.glottis_model == AFS_GLOTTIS_TWO_MASS, w);
       for (int gl = 0; gl < W; ++gl) R[gl].planw = w[gl % PLAN_WORDS];
-      sample_step<W>(ex, X.data(), T.uni, T.consts, ratio, defer);
+      if (opt.glottis_model == AFS_GLOTTIS_TWO_MASS)
+        sample_step<W, AFS_GLOTTIS_TWO_MASS>(ex, X.data(), T.uni, T.consts, ratio, defer);
+      else
+        sample_step<W, AFS_GLOTTIS_TRIANGULAR>(ex, X.data(), T.uni, T.consts, ratio, defer);
       out[t] = R[0].sample;
       if (t < ndump) {
         for (int gl = 0; gl < W; ++gl)

@@ -13,7 +13,7 @@ using namespace afs::tree;
 
 __global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_prof_kernel(TreeArgs a, uint64_t *prof) {
   __shared__ WaveLds lds;
-  tree_synth_body<true>(a, lds, prof);
+  tree_synth_body<true, AFS_GLOTTIS_TRIANGULAR>(a, lds, prof);  // (the profiler runs the default glottis)
 }
 
 #define CK(x)                                                                  \
