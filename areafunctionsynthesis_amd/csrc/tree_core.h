@@ -1069,7 +1069,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     const int s = s0 < 0 ? (dyn ? DYN0 : 0) : s0;
     const int i = s0 < 0 ? NODE_SINK : s;  // current i flows into section s
     const SecRec &q = rec[j];
-    const double *ks = C.stat[static_index(s)];
+    const double *ks = C.stat[dyn ? 0 : static_index(s)];  // (a dynamic slot has no row: row 0 stands in)
     const double LB = dyn ? X[X_L + s - DYN0] : ks[ST_L];
     const double RB = dyn ? X[X_R0 + s - DYN0] : ((s == S_FOSSA0 && !opt.piriform_fossa) ? C.h.fossa_R0 : ks[ST_R]);
     const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
@@ -1117,7 +1117,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     // radiation rows of s = 64 / 83 (TdsModel.cpp:1841-1911)
     const bool dyn = j < S::ND;
     const int s = slot_section<W>(j, gl);
-    const double *ks = C.stat[static_index(s)];
+    const double *ks = C.stat[dyn ? 0 : static_index(s)];
     const double LB = dyn ? X[X_L + s - DYN0] : ks[ST_L];
     const double R1B = dyn ? X[X_R1 + s - DYN0] : ks[ST_R];
     const double EB = dyn ? X[X_E + s - DYN0] : ks[ST_E], DB = X[X_D + s];

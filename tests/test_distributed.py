@@ -96,11 +96,13 @@ def test_gloo_world2_gather_matches_single_process():
 
 def test_shard_gather_loopback(tmp_path):
     """afs_gather.h -- the shard and gather logic libafs.so drives over RCCL -- over an
-    in-process loopback transport (one thread per rank): uneven shards, world 1..8."""
+    in-process loopback transport (one thread per rank): uneven shards, world 1..8, built with
+    AddressSanitizer and UndefinedBehaviorSanitizer."""
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     exe = str(tmp_path / "gather_main")
     subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-pthread",
+                           "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
                            "-I", os.path.join(root, "areafunctionsynthesis_amd", "csrc"),
                            os.path.join(root, "tests", "cpp", "gather_main.cpp"), "-o", exe])
     out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
