@@ -1455,7 +1455,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.sync();
   x.mark(PH_ROWS);
   constexpr int nr = TREE_ROUNDS;  // (build_tables checks the schedule against it)
-  // fill edges start at zero
+  // fill edges start at zero (zeroing them inside the row block instead: measured neutral)
   x.par([&](int gl, Lane<W> &R) {
     (void)R;
 #pragma unroll

@@ -1,0 +1,22 @@
+#!/bin/bash
+# A/B builds (development tool): libafs_TAG.so and libphase_prof_TAG.so from the current tree
+# with extra compiler flags (e.g. -DAFS_VAR_...), for tools/ab.sh.
+# usage: tools/build_variant.sh TAG "FLAGS"
+set -eu
+cd "$(dirname "$0")/.."
+TAG=$1
+FLAGS=${2:-}
+C=areafunctionsynthesis_amd/csrc
+O=/tmp/afs_variant_$TAG
+mkdir -p $O
+COMMON="-O3 -std=c++17 -fPIC -Wall -Wno-unused-function -ffp-contract=off -fno-strict-aliasing -Wno-unknown-pragmas --offload-arch=gfx950 $FLAGS"
+objs=""
+for s in afs_capi.cpp afs_comm.cpp afs_tables.cpp tds_lane.hip tds_tree.hip af_kernels.hip audio_kernels.hip; do
+  o=$O/${s%.*}.o
+  /opt/rocm/bin/hipcc -c -x hip $C/$s -o $o $COMMON &
+  objs="$objs $o"
+done
+wait
+/opt/rocm/bin/hipcc -shared -o areafunctionsynthesis_amd/libafs_$TAG.so --offload-arch=gfx950 -fPIC $objs -ldl
+/opt/rocm/bin/hipcc -shared -o tools/phase_prof/libphase_prof_$TAG.so $COMMON -I$C -Iinclude tools/phase_prof/phase_prof.hip -x hip $C/afs_tables.cpp $C/tds_tree.hip
+echo built $TAG
