@@ -94,6 +94,40 @@ struct SolveStep {
 struct alignas(16) StepRec {
   uint16_t c, n0, n1, e0, e1, e01, un0, un1;
 };
+// Arm solver (tree_core.h solve_arms; afs_tables.cpp arm_records).  The current graph is a
+// junction triangle {40, 41, 65} with three arms (A: 0..39 with the fossa 84..88 on {28, 29};
+// B: 42..64 with the radiation pair 93/94; C: 66..83 with the pair 95/96 and the sinus leaves
+// 89..92).  Each of the 16 lanes owns a segment of an arm at positions 0..ARM_P-1, right
+// aligned (its last node, the lane's boundary, at ARM_P-1; dummy positions in front), folds
+// the leaves of its segment (fold slot f joins a leaf to positions ARM_FOLD_POS[f] and +1),
+// eliminates the segment's other nodes in registers, and the boundaries are reduced lane to
+// lane by DPP.  Lane roles are fixed by the partition: the fossa lane folds 84 into the
+// boundaries 28 / 29 of ARM_L28 / ARM_L28 + 1, the junction lane solves the triangle.
+constexpr int ARM_P = 8, ARM_FOLDS = 4, ARM_MAXLEN = 7;  // ARM_MAXLEN: lanes of the longest arm
+constexpr int ARM_FOSSA = 14, ARM_JUNCTION = 15, ARM_L28 = 3;
+constexpr int ARM_END_A = 6, ARM_END_B = 10, ARM_END_C = 13;  // lanes of the arms' last boundaries
+AFS_HD constexpr int arm_fold_pos(int f) { return f == 0 ? 2 : f == 1 ? 3 : f == 2 ? 5 : 6; }
+enum : uint8_t { ARM_IN = 1, ARM_END = 2 };
+// LDS byte offsets (utterance block) of one lane's part; dummy positions and unused fold
+// slots point at the ONE pivot slot (1.0, rhs 0.0), the zero edge and the solution sink, so
+// that every lane runs the same code and a dummy step changes nothing.
+struct alignas(16) ArmRec {
+  uint16_t d[ARM_P];          // pivot (X_DIAG) of position p; its rhs at RHS_DELTA
+  uint16_t u[ARM_P];          // X_U slot of position p: its fill edge to the anchor, then x
+  uint16_t e[ARM_P - 1];      // edge p - p+1 (X_OFF)
+  uint16_t ea;                // edge anchor (previous lane's boundary) - first real node
+  uint16_t ld[ARM_FOLDS], le0[ARM_FOLDS], le1[ARM_FOLDS], lu[ARM_FOLDS];  // fold leaves
+  uint16_t fx0, fx1;          // fossa lane: edges 84-28, 84-29 (else the zero edge)
+  uint16_t ej;                // last lane of an arm: edge boundary - junction node
+  uint8_t start;              // first real position (ARM_P: none)
+  uint8_t idx, flags, pad0;   // position in the arm (0 = far end), ARM_IN / ARM_END
+  uint16_t pad[3];
+};
+static_assert(sizeof(ArmRec) == 96, "ArmRec: 96 bytes");
+// the junction triangle: pivots of 40, 41, 65, edges 40-41, 40-65, 41-65, X_U of 40, 41, 65
+struct alignas(8) ArmJunction {
+  uint16_t d[3], e[3], u[3], pad;
+};
 // Currents whose d/dt another lane reads (branch partners and radiation; tree_core.h X_UR).
 constexpr int NUR = 16;
 // Currents whose noise-filtered value another lane reads (outputs of the constriction
@@ -161,6 +195,8 @@ struct Uni {
 struct Consts {
   Hot h;
   StepRec step[TREE_MAX_ROUNDS][TREE_CHAINS];
+  ArmRec arm[TREE_CHAINS];
+  ArmJunction armj;
   int8_t ur_slot[NC];  // X_UR slot of a current, -1: none
   int8_t un_slot[NC];  // X_UN slot of a current, -1: none
   Topo topo[NS];

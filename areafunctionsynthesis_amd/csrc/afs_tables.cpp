@@ -293,6 +293,112 @@ bool tree_schedule(Tables *t) {
   return t->n_rounds == TREE_ROUNDS && t->fwd_carry == TREE_FWD_CARRY && t->bwd_carry == TREE_BWD_CARRY;
 }
 
+// The arm solver's lane records (afs_model.h ArmRec, tree_core.h solve_arms).  The partition
+// (tools/arm_solver_study.py checks the elimination on random SPD systems): per lane the
+// segment from the far end to its boundary, then the fold leaves.  The builder checks that
+// the roles it assigns use every edge of the current graph exactly once (chain edges, anchor
+// edges between consecutive lanes of an arm, fold edges, the fossa's two edges, the three
+// arm-to-junction edges, the triangle) and every current exactly once; with that, the
+// elimination the kernel performs is the exact LDL^T of the system.
+bool arm_records(Tables *t) {
+  static const int SEG[TREE_CHAINS][ARM_P] = {
+      // arm A (far end 0), walked upward
+      {0, 1, 2, 3, 4, 5, 6, -1}, {7, 8, 9, 10, 11, 12, 13, -1}, {14, 15, 16, 17, 18, 19, 20, -1},
+      {21, 22, 23, 24, 25, 26, 27, 28}, {29, -1}, {30, 31, 32, 33, 34, -1}, {35, 36, 37, 38, 39, -1},
+      // arm B (far end: the radiation pair), walked downward
+      {93, 64, 63, 62, 61, 60, -1}, {59, 58, 57, 56, 55, 54, -1}, {53, 52, 51, 50, 49, 48, -1},
+      {47, 46, 45, 44, 43, 42, -1},
+      // arm C (far end: the nostril pair)
+      {96, 83, 82, 81, 80, 79, -1}, {78, 77, 76, 75, 74, 73, -1}, {72, 71, 70, 69, 68, 67, 66, -1},
+      // fossa (84 is its boundary), junction (no segment)
+      {88, 87, 86, 85, 84, -1}, {-1}};
+  static const int ARM_OF[TREE_CHAINS] = {0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, -1, -1};
+  static const int LEAF[TREE_CHAINS][ARM_FOLDS] = {
+      {-1, -1, -1, -1}, {-1, -1, -1, -1}, {-1, -1, -1, -1}, {-1, -1, -1, -1}, {-1, -1, -1, -1},
+      {-1, -1, -1, -1}, {-1, -1, -1, -1}, {94, -1, -1, -1}, {-1, -1, -1, -1}, {-1, -1, -1, -1},
+      {-1, -1, -1, -1}, {95, -1, -1, -1}, {92, 91, 90, 89}, {-1, -1, -1, -1}, {-1, -1, -1, -1},
+      {-1, -1, -1, -1}};
+  static const int JN[3] = {40, 41, 65}, JEND[3] = {39, 42, 66};
+  static int16_t eid[NC][NC];
+  for (int i = 0; i < NC; ++i)
+    for (int j = 0; j < NC; ++j) eid[i][j] = -1;
+  for (int s = 0; s < NS; ++s) {
+    const int m[3] = {t->cin[s], t->cout0[s], t->cout1[s]};
+    const int pk[3][3] = {{-1, 0, 1}, {0, -1, 2}, {1, 2, -1}};
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b)
+        if (a != b && m[a] >= 0 && m[b] >= 0) eid[m[a]][m[b]] = t->edge[s][pk[a][b]];
+  }
+  using namespace tree;
+  auto off = [](int slot) { return (uint16_t)(slot * 8); };
+  const uint16_t ONE = off(X_DIAG + NC + 1), ZE = off(X_OFF + EDGE_ZERO), USINK = off(X_U + U_SINK);
+  std::vector<int> edge_uses(TREE_NE, 0), node_uses(NC, 0);
+  bool ok = true;
+  auto use_edge = [&](int a, int b) -> uint16_t {
+    if (a < 0 || b < 0 || a >= NC || b >= NC || eid[a][b] < 0 || eid[a][b] >= TREE_NE) { ok = false; return ZE; }
+    edge_uses[eid[a][b]]++;
+    return off(X_OFF + eid[a][b]);
+  };
+  int bound[TREE_CHAINS];
+  Consts &c = t->consts;
+  for (int k = 0; k < TREE_CHAINS; ++k) {
+    int n = 0;
+    while (n < ARM_P && SEG[k][n] >= 0) ++n;
+    ArmRec &r = c.arm[k];
+    std::memset(&r, 0, sizeof r);
+    const int start = ARM_P - n;
+    int pos[ARM_P];
+    for (int p = 0; p < ARM_P; ++p) pos[p] = p >= start ? SEG[k][p - start] : -1;
+    bound[k] = n ? pos[ARM_P - 1] : -1;
+    r.start = (uint8_t)start;
+    for (int p = 0; p < ARM_P; ++p) {
+      if (pos[p] >= 0) node_uses[pos[p]]++;
+      r.d[p] = pos[p] >= 0 ? off(X_DIAG + pos[p]) : ONE;
+      r.u[p] = pos[p] >= 0 ? off(X_U + pos[p]) : USINK;
+    }
+    for (int p = 0; p + 1 < ARM_P; ++p) r.e[p] = (pos[p] >= 0) ? use_edge(pos[p], pos[p + 1]) : ZE;
+    // anchor: the previous lane of the same arm
+    const bool anchored = ARM_OF[k] >= 0 && k > 0 && ARM_OF[k - 1] == ARM_OF[k];
+    r.ea = (anchored && n) ? use_edge(bound[k - 1], pos[start]) : ZE;
+    int idx = 0;
+    for (int j = k - 1; j >= 0 && ARM_OF[j] == ARM_OF[k] && ARM_OF[k] >= 0; --j) ++idx;
+    r.idx = (uint8_t)(ARM_OF[k] >= 0 ? idx : 0xff);
+    const bool last = ARM_OF[k] >= 0 && (k + 1 == TREE_CHAINS || ARM_OF[k + 1] != ARM_OF[k]);
+    r.flags = (uint8_t)((ARM_OF[k] >= 0 ? ARM_IN : 0) | (last ? ARM_END : 0));
+    r.ej = ZE;
+    if (last) r.ej = use_edge(JEND[ARM_OF[k]], JN[ARM_OF[k]]);
+    if (last && bound[k] != JEND[ARM_OF[k]]) ok = false;
+    for (int f = 0; f < ARM_FOLDS; ++f) {
+      const int leaf = LEAF[k][f], p = arm_fold_pos(f);
+      r.ld[f] = leaf >= 0 ? off(X_DIAG + leaf) : ONE;
+      r.lu[f] = leaf >= 0 ? off(X_U + leaf) : USINK;
+      r.le0[f] = leaf >= 0 ? use_edge(leaf, pos[p]) : ZE;
+      r.le1[f] = leaf >= 0 ? use_edge(leaf, pos[p + 1]) : ZE;
+      if (leaf >= 0) node_uses[leaf]++;
+    }
+    r.fx0 = r.fx1 = ZE;
+  }
+  // roles fixed in the kernel
+  if (bound[ARM_L28] != 28 || bound[ARM_L28 + 1] != 29 || bound[ARM_FOSSA] != 84 || bound[ARM_JUNCTION] != -1 ||
+      bound[ARM_END_A] != 39 || bound[ARM_END_B] != 42 || bound[ARM_END_C] != 66)
+    ok = false;
+  c.arm[ARM_FOSSA].fx0 = use_edge(84, 28);
+  c.arm[ARM_FOSSA].fx1 = use_edge(84, 29);
+  ArmJunction &j = c.armj;
+  std::memset(&j, 0, sizeof j);
+  for (int q = 0; q < 3; ++q) {
+    j.d[q] = off(X_DIAG + JN[q]);
+    j.u[q] = off(X_U + JN[q]);
+    node_uses[JN[q]]++;
+  }
+  j.e[0] = use_edge(40, 41);
+  j.e[1] = use_edge(40, 65);
+  j.e[2] = use_edge(41, 65);
+  for (int e = 0; e < TREE_NE; ++e) ok = ok && edge_uses[e] == 1;
+  for (int i = 0; i < NC; ++i) ok = ok && node_uses[i] == 1;
+  return ok;
+}
+
 }  // namespace
 
 // IirFilter::createChebyshev, IirFilter.cpp:286-432 (0.5 % ripple).
@@ -377,6 +483,7 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   t->fossa_R0 = 8.0 * MU * t->len[S_FOSSA0] * PI / (AMIN * AMIN);
   topology(t);
   t->n_rounds = tree_schedule(t) ? t->n_rounds : -1;
+  if (!arm_records(t)) t->n_rounds = -1;
   // packed copy for the cooperative kernel
   Consts &c = t->consts;
   Hot &h = c.h;

@@ -47,6 +47,11 @@ using std::sqrt;
 #define AFS_LDS_DRAIN() ((void)0)
 #endif
 
+// The per-sample solver: 1 = the arm solver (solve_arms), 0 = the LDS rounds.
+#ifndef AFS_ARM_SOLVER
+#define AFS_ARM_SOLVER 1
+#endif
+
 namespace afs {
 namespace tree {
 
@@ -136,6 +141,20 @@ struct SolveCarry {
   StepRec cur, next;  // this round's step and the next (prefetched)
   double d, y;        // forward: pivot and rhs of the last n0; backward: y = last solution
 };
+// Arm solver lane registers (solve_arms).
+struct ArmCarry {
+  double Db, Yb;      // pivot and rhs of the lane's boundary (reduced in place)
+  double dA, yA;      // the walk's update of the anchor's pivot and rhs
+  double F;           // edge anchor - boundary after the walk
+  double inv, x;      // 1 / pivot of the boundary after the arm reduction; its solution
+  double Fn, ej;      // F of the next lane; edge boundary - junction node (last lanes)
+  double e28, e29;    // fossa lane: edges 84-28, 84-29
+  double xJ;          // last lanes: the solution of their junction node (then the anchor's)
+  double jd[3], jy[3], je[3], xj[3];  // junction lane: triangle pivots, rhs, edges, solutions
+  int sf, sb, end;    // the arm steps this lane reduces in (forward) / solves in (back), -1: none
+};
+// Up to four doubles handed between lanes (x.pull).
+struct D4 { double v[4]; };
 
 
 // 1/d for the pivots: v_rcp_f64 and two Newton steps on the device (within an ulp of the
@@ -210,6 +229,7 @@ struct Lane {
   uint32_t racc[S::NDP];                                             // rand() sums of owned dipoles
   uint32_t rtmp[3];                                                  // rand() block scratch
   SolveCarry sc;                                                     // chain lanes, during the solve
+  ArmCarry ac;                                                       // arm solver, during the solve
   // per-sample values of the geometry/network block (not state: cleared before a save)
   double acur[S::ND], lcur[S::ND];                                   // area, length of the slots
   double anx[S::ND], apv[S::ND];                                     // areas of sections s+1, s-1
@@ -225,6 +245,8 @@ struct MinIdx { double v; int i; };
 // (s = the section of slot j; lanes' values as the interpolation left them).
 // x.scan_add<N>(f, g): f(gl, R) -> U4; inclusive prefix sums (mod 2^32) of the first N
 // components over lanes 0..gl are handed to g(gl, R, sums).
+// x.pull<K, N>(f, g): f(gl, R) -> D4; g(gl, R, v) gets the first N components of lane gl+K's
+// value (zeros when gl+K is outside the lane's group of 16: one DPP row on the device).
 struct U4 { uint32_t v[4]; };
 AFS_HD inline MinIdx min_idx_combine(MinIdx a, MinIdx b) {
   return (b.v < a.v || (b.v == a.v && b.i < a.i)) ? b : a;
@@ -1062,6 +1084,8 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
   SecRec rec[S::NSL];
   load_sec_recs<W>(gl, C, rec);
   Xw[X_OFF + EDGE_ZERO] = 0.0;  // the solver's zero edge (union slot; every lane stores it)
+  Xw[X_DIAG + NC + 1] = 1.0;    // the arm solver's dummy pivot and rhs
+  Xw[X_RHS + NC + 1] = 0.0;
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const bool dyn = j < S::ND;
@@ -1229,6 +1253,267 @@ AFS_HD inline void backward_rounds(Xc &x, double *X, const Consts &C) {
     x.sync();
     backward_rounds<W, R - 1>(x, X, C);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Arm solver (afs_model.h ArmRec; partition and checks in afs_tables.cpp arm_records).
+// The same LDL^T of the same matrix as the rounds above, in an order that keeps the
+// eliminations in registers: every lane folds the leaves of its segment and walks the segment
+// from the far end (each step eliminates one node whose neighbours are the next position and
+// the anchor, the previous lane's boundary, through the fill edge F), the boundaries of an arm
+// are then reduced lane to lane toward the junction by DPP row shifts, the junction lane
+// solves the triangle, and the solutions travel back the same way.  LDS is touched only to
+// load the rows' values and to keep the walk's factors for the back substitution.
+// ---------------------------------------------------------------------------
+AFS_HD inline double arm_recip(double d) { return (d < 0.0) ? NAN : pivot_recip(d); }
+
+// Phase A of a lane: the fold leaves, then the walk from the far end to the boundary.  Every
+// load comes before the first store, so that the loads issue back to back (the stores go to
+// LDS slots the compiler cannot tell apart from the loaded ones).
+AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
+  const ArmRec r = rr;
+  double D[ARM_P], Y[ARM_P], E[ARM_P - 1];
+  double dl[ARM_FOLDS], yl[ARM_FOLDS], l0[ARM_FOLDS], l1[ARM_FOLDS];
+#pragma unroll
+  for (int p = 0; p < ARM_P; ++p) {
+    D[p] = xat(X, r.d[p]);
+    Y[p] = xat(X, r.d[p] + RHS_DELTA);
+  }
+#pragma unroll
+  for (int p = 0; p < ARM_P - 1; ++p) E[p] = xat(X, r.e[p]);
+#pragma unroll
+  for (int f = 0; f < ARM_FOLDS; ++f) {
+    dl[f] = xat(X, r.ld[f]);
+    yl[f] = xat(X, r.ld[f] + RHS_DELTA);
+    l0[f] = xat(X, r.le0[f]);
+    l1[f] = xat(X, r.le1[f]);
+  }
+  const double ea = xat(X, r.ea);
+  a.e28 = xat(X, r.fx0);
+  a.e29 = xat(X, r.fx1);
+  a.ej = xat(X, r.ej);
+  const bool in = (r.flags & ARM_IN) != 0, end = (r.flags & ARM_END) != 0;
+  a.sf = in ? (int)r.idx : -1;
+  a.sb = (in && !end) ? (int)r.idx : -1;
+  a.end = end ? 1 : 0;
+  // fold slot f: the leaf joined to positions p, p+1 (an unused slot: pivot 1, zero edges)
+  double il[ARM_FOLDS];
+#pragma unroll
+  for (int f = 0; f < ARM_FOLDS; ++f) {
+    const int p = arm_fold_pos(f);
+    il[f] = arm_recip(dl[f]);
+    const double f0 = l0[f] * il[f], f1 = l1[f] * il[f];
+    D[p] -= f0 * l0[f];
+    Y[p] -= f0 * yl[f];
+    D[p + 1] -= f1 * l1[f];
+    Y[p + 1] -= f1 * yl[f];
+    E[p] -= f0 * l1[f];
+  }
+  // the walk: position p has neighbours p+1 (edge E[p]) and the anchor (edge F, which the
+  // anchor edge becomes at the first real position; dummy positions keep F = 0)
+  double F = 0.0, dA = 0.0, yA = 0.0;
+#pragma unroll
+  for (int p = 0; p < ARM_P - 1; ++p) {
+    F = (p == (int)r.start) ? ea : F;
+    const double inv = arm_recip(D[p]);
+    const double g = F * inv, h = E[p] * inv;
+    dA -= g * F;
+    yA -= g * Y[p];
+    D[p + 1] -= h * E[p];
+    Y[p + 1] -= h * Y[p];
+    xat(X, r.d[p]) = inv;                // factors for the back substitution
+    xat(X, r.d[p] + RHS_DELTA) = Y[p];
+    xat(X, r.u[p]) = F;
+    xat(X, r.e[p]) = E[p];
+    F = -(g * E[p]);                     // fill edge anchor - p+1
+  }
+#pragma unroll
+  for (int f = 0; f < ARM_FOLDS; ++f) xat(X, r.ld[f]) = il[f];
+  a.F = ((int)r.start == ARM_P - 1) ? ea : F;
+  a.Db = D[ARM_P - 1];
+  a.Yb = Y[ARM_P - 1];
+  a.dA = dA;
+  a.yA = yA;
+}
+
+// Back substitution of a lane's segment and leaves, from its boundary's solution a.x and the
+// anchor's xA (all loads first, as in the walk); the junction lane stores the triangle's
+// solutions here too (the other lanes into the sink).
+AFS_HD inline void arm_back(const ArmRec &rr, const ArmJunction &J, bool junction, double *X, const ArmCarry &a,
+                            double xA) {
+  const ArmRec r = rr;
+  double inv[ARM_P - 1], y[ARM_P - 1], Fp[ARM_P - 1], Ep[ARM_P - 1];
+  double il[ARM_FOLDS], yl[ARM_FOLDS], l0[ARM_FOLDS], l1[ARM_FOLDS];
+#pragma unroll
+  for (int p = 0; p < ARM_P - 1; ++p) {
+    inv[p] = xat(X, r.d[p]);
+    y[p] = xat(X, r.d[p] + RHS_DELTA);
+    Fp[p] = xat(X, r.u[p]);
+    Ep[p] = xat(X, r.e[p]);
+  }
+#pragma unroll
+  for (int f = 0; f < ARM_FOLDS; ++f) {
+    il[f] = xat(X, r.ld[f]);
+    yl[f] = xat(X, r.ld[f] + RHS_DELTA);
+    l0[f] = xat(X, r.le0[f]);
+    l1[f] = xat(X, r.le1[f]);
+  }
+  double xs[ARM_P];
+  xs[ARM_P - 1] = a.x;
+#pragma unroll
+  for (int p = ARM_P - 2; p >= 0; --p) {
+    double v = y[p];
+    v -= Ep[p] * xs[p + 1];
+    v -= Fp[p] * xA;
+    xs[p] = v * inv[p];
+  }
+#pragma unroll
+  for (int p = 0; p < ARM_P; ++p) xat(X, r.u[p]) = xs[p];
+#pragma unroll
+  for (int f = 0; f < ARM_FOLDS; ++f) {
+    const int p = arm_fold_pos(f);
+    double v = yl[f];
+    v -= l0[f] * xs[p];
+    v -= l1[f] * xs[p + 1];
+    xat(X, r.lu[f]) = v * il[f];
+  }
+  const uint32_t sink = (uint32_t)(X_U + U_SINK) * 8u;
+  xat(X, junction ? J.u[0] : sink) = a.xj[0];
+  xat(X, junction ? J.u[1] : sink) = a.xj[1];
+  xat(X, junction ? J.u[2] : sink) = a.xj[2];
+}
+
+template <int W, class Xc>
+AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
+  static_assert(TREE_CHAINS == 16, "the arm partition has 16 lanes (one DPP row)");
+  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_walk(C.arm[k], X, R.ac); });
+  // the junction triangle's values (every lane loads them; only the junction lane's matter)
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
+    const ArmJunction &J = C.armj;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      R.ac.jd[q] = xat(X, J.d[q]);
+      R.ac.jy[q] = xat(X, J.d[q] + RHS_DELTA);
+      R.ac.je[q] = xat(X, J.e[q]);
+    }
+    R.ac.xJ = 0.0;
+  });
+  // the anchors' updates: lane k's anchor is lane k-1's boundary (a first lane of an arm, the
+  // fossa and the junction lane send zeros)
+  x.template pull<1, 2>([&](int, Lane<W> &R) { return D4{{R.ac.dA, R.ac.yA, 0.0, 0.0}}; },
+                        [&](int, Lane<W> &R, const D4 &v) { R.ac.Db += v.v[0]; R.ac.Yb += v.v[1]; });
+  // the fossa lane folds 84 into 28 (lane ARM_L28) and 29 (lane ARM_L28 + 1); every other
+  // lane's fossa edges are zero, so it sends zeros
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.inv = arm_recip(R.ac.Db); });
+  x.template pull<ARM_FOSSA - ARM_L28, 2>(
+      [&](int, Lane<W> &R) {
+        const double c0 = R.ac.e28 * R.ac.inv;
+        return D4{{c0 * R.ac.e28, c0 * R.ac.Yb, 0.0, 0.0}};
+      },
+      [&](int, Lane<W> &R, const D4 &v) { R.ac.Db -= v.v[0]; R.ac.Yb -= v.v[1]; });
+  x.template pull<ARM_FOSSA - ARM_L28 - 1, 3>(
+      [&](int, Lane<W> &R) {
+        const double c0 = R.ac.e28 * R.ac.inv, c1 = R.ac.e29 * R.ac.inv;
+        return D4{{c1 * R.ac.e29, c1 * R.ac.Yb, c0 * R.ac.e29, 0.0}};
+      },
+      [&](int, Lane<W> &R, const D4 &v) { R.ac.Db -= v.v[0]; R.ac.Yb -= v.v[1]; R.ac.F -= v.v[2]; });
+  // arm reduction toward the junction: in step s the lanes at position s of their arm
+  // eliminate the previous boundary (lane k-1) from their own
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.inv = arm_recip(R.ac.Db); });
+#pragma unroll
+  for (int s = 1; s < ARM_MAXLEN; ++s) {
+    x.template pull<-1, 2>([&](int, Lane<W> &R) { return D4{{R.ac.inv, R.ac.Yb, 0.0, 0.0}}; },
+                           [&](int, Lane<W> &R, const D4 &v) {
+                             const bool on = R.ac.sf == s;
+                             const double f = R.ac.F * v.v[0];
+                             const double nd = R.ac.Db - f * R.ac.F, ny = R.ac.Yb - f * v.v[1];
+                             R.ac.Db = on ? nd : R.ac.Db;
+                             R.ac.Yb = on ? ny : R.ac.Yb;
+                             R.ac.inv = on ? arm_recip(nd) : R.ac.inv;
+                           });
+  }
+  // the junction lane takes the three arms' last boundaries (pivot inverse, rhs, edge) and
+  // solves the triangle: eliminate 65, then 41; solve 40 (uniform code on every lane)
+  auto give = [&](int, Lane<W> &R) { return D4{{R.ac.inv, R.ac.Yb, R.ac.ej, 0.0}}; };
+  auto take = [&](int q) {
+    return [&, q](int, Lane<W> &R, const D4 &v) {
+      const double g = v.v[2] * v.v[0];
+      R.ac.jd[q] -= g * v.v[2];
+      R.ac.jy[q] -= g * v.v[1];
+    };
+  };
+  x.template pull<ARM_END_A - ARM_JUNCTION, 3>(give, take(0));
+  x.template pull<ARM_END_B - ARM_JUNCTION, 3>(give, take(1));
+  x.template pull<ARM_END_C - ARM_JUNCTION, 3>(give, take(2));
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
+    double *d = R.ac.jd, *y = R.ac.jy;
+    double e01 = R.ac.je[0];
+    const double e02 = R.ac.je[1], e12 = R.ac.je[2];
+    const double i2 = arm_recip(d[2]);
+    const double g0 = e02 * i2, g1 = e12 * i2;
+    d[0] -= g0 * e02;
+    y[0] -= g0 * y[2];
+    d[1] -= g1 * e12;
+    y[1] -= g1 * y[2];
+    e01 -= g0 * e12;
+    const double i1 = arm_recip(d[1]);
+    const double h = e01 * i1;
+    d[0] -= h * e01;
+    y[0] -= h * y[1];
+    const double x0 = y[0] * arm_recip(d[0]);
+    double v1 = y[1];
+    v1 -= e01 * x0;
+    const double x1 = v1 * i1;
+    double v2 = y[2];
+    v2 -= e02 * x0;
+    v2 -= e12 * x1;
+    R.ac.xj[0] = x0;
+    R.ac.xj[1] = x1;
+    R.ac.xj[2] = v2 * i2;
+  });
+  x.template pull<ARM_JUNCTION - ARM_END_A, 1>([&](int, Lane<W> &R) { return D4{{R.ac.xj[0], 0.0, 0.0, 0.0}}; },
+                                               [&](int k, Lane<W> &R, const D4 &v) { if (k == ARM_END_A) R.ac.xJ = v.v[0]; });
+  x.template pull<ARM_JUNCTION - ARM_END_B, 1>([&](int, Lane<W> &R) { return D4{{R.ac.xj[1], 0.0, 0.0, 0.0}}; },
+                                               [&](int k, Lane<W> &R, const D4 &v) { if (k == ARM_END_B) R.ac.xJ = v.v[0]; });
+  x.template pull<ARM_JUNCTION - ARM_END_C, 1>([&](int, Lane<W> &R) { return D4{{R.ac.xj[2], 0.0, 0.0, 0.0}}; },
+                                               [&](int k, Lane<W> &R, const D4 &v) {
+                                                 R.ac.xJ = (k == ARM_END_C) ? v.v[0] : R.ac.xJ;
+                                               });
+  // back along the arms
+  x.template pull<1, 1>([&](int, Lane<W> &R) { return D4{{R.ac.F, 0.0, 0.0, 0.0}}; },
+                        [&](int, Lane<W> &R, const D4 &v) { R.ac.Fn = v.v[0]; });
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
+    double v = R.ac.Yb;
+    v -= R.ac.ej * R.ac.xJ;
+    R.ac.x = R.ac.end ? v * R.ac.inv : 0.0;
+  });
+#pragma unroll
+  for (int s = ARM_MAXLEN - 2; s >= 0; --s) {
+    x.template pull<1, 1>([&](int, Lane<W> &R) { return D4{{R.ac.x, 0.0, 0.0, 0.0}}; },
+                          [&](int, Lane<W> &R, const D4 &v) {
+                            const bool on = R.ac.sb == s;
+                            double t = R.ac.Yb;
+                            t -= R.ac.Fn * v.v[0];
+                            R.ac.x = on ? t * R.ac.inv : R.ac.x;
+                          });
+  }
+  // the fossa lane: 84 from 28 and 29
+  x.template pull<ARM_L28 - ARM_FOSSA, 1>([&](int, Lane<W> &R) { return D4{{R.ac.x, 0.0, 0.0, 0.0}}; },
+                                          [&](int, Lane<W> &R, const D4 &v) { R.ac.Fn = v.v[0]; });
+  x.template pull<ARM_L28 + 1 - ARM_FOSSA, 1>([&](int, Lane<W> &R) { return D4{{R.ac.x, 0.0, 0.0, 0.0}}; },
+                                              [&](int k, Lane<W> &R, const D4 &v) {
+                                                double t = R.ac.Yb;
+                                                t -= R.ac.e28 * R.ac.Fn;
+                                                t -= R.ac.e29 * v.v[0];
+                                                R.ac.x = (k == ARM_FOSSA) ? t * R.ac.inv : R.ac.x;
+                                              });
+  x.mark(PH_FORWARD);
+  // every lane's segment from its boundary and its anchor (lane k-1's boundary)
+  x.template pull<-1, 1>([&](int, Lane<W> &R) { return D4{{R.ac.x, 0.0, 0.0, 0.0}}; },
+                         [&](int, Lane<W> &R, const D4 &v) { R.ac.xJ = v.v[0]; });
+  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_back(C.arm[k], C.armj, k == ARM_JUNCTION, X, R.ac, R.ac.xJ); });
+  x.sync();
+  x.mark(PH_BACKWARD);
 }
 
 // ---------------------------------------------------------------------------
@@ -1454,6 +1739,9 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.par([&](int gl, Lane<W> &R) { phase_rows<W>(gl, R, X, X, U, C); });
   x.sync();
   x.mark(PH_ROWS);
+#if AFS_ARM_SOLVER
+  solve_arms<W>(x, X, C);
+#else
   constexpr int nr = TREE_ROUNDS;  // (build_tables checks the schedule against it)
   // fill edges start at zero (zeroing them inside the row block instead: measured neutral)
   x.par([&](int gl, Lane<W> &R) {
@@ -1478,6 +1766,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   AFS_LDS_DRAIN();
   backward_rounds<W, nr - 1>(x, X, C);
   x.mark(PH_BACKWARD);
+#endif
   // the state update and the output stage (lane-uniform: radiated flow, filters) in one phase
   x.par_uniform([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, X, U, C); },
                 [&](Lane<W> &R) { R.sample = phase_output(X, U, C, section_pressure(X, C, S_PHARYNX0), defer_out); });

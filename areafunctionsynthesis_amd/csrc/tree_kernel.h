@@ -37,7 +37,9 @@ struct GpuExec {
   // Per-lane work and lane-uniform work in one block: every lane also evaluates the uniform
   // part (same inputs, same values, same stores), so the two interleave without a branch.
   template <class F, class G> __device__ __forceinline__ void par_uniform(F f, G g) { f(gl, *R); g(*R); }
-  template <class F> __device__ __forceinline__ void lanes(int n, F f) { if (gl < n) f(gl, *R); }
+  template <class F> __device__ __forceinline__ void lanes(int n, F f) {
+    if (n >= TW || gl < n) f(gl, *R);  // (no branch when every lane takes part)
+  }
   __device__ __forceinline__ void sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -127,6 +129,22 @@ struct GpuExec {
     }
     g(gl, *R, v);
   }
+  // Lane gl+K's value inside the 16-lane row: row_shl K (K > 0) / row_shr -K, zero fill.
+  template <int K> __device__ __forceinline__ static double shift(double v) {
+    static_assert(K != 0 && K > -16 && K < 16, "row shift");
+    constexpr int CTRL = K > 0 ? 0x100 + K : 0x110 - K;
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, true);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  }
+  template <int K, int N, class F, class G> __device__ __forceinline__ void pull(F f, G g) {
+    const D4 v = f(gl, *R);
+    D4 o{{0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+    for (int i = 0; i < N; ++i) o.v[i] = shift<K>(v.v[i]);
+    g(gl, *R, o);
+  }
   // Word K of this sample's plan (tree_plan.h): lane K of each 16-lane row holds it
   // (R.planw), DPP row_newbcast hands it to the whole row.
   template <int K> __device__ __forceinline__ uint64_t rec() {
@@ -211,6 +229,8 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
     // last values are not kept alive through the time loop for this store)
 #pragma unroll
     for (int j = 0; j < Shape<TW>::ND; ++j) R.acur[j] = R.lcur[j] = R.anx[j] = R.apv[j] = 0.0;
+    R.ac = ArmCarry{};
+    R.sc = SolveCarry{};
     ((Lane<TW> *)a.lane_state)[(int64_t)u * TW + gl] = R;
     double *ws = a.lds_state + (int64_t)u * X_TOTAL;
     for (int k = gl; k < X_TOTAL; k += TW) ws[k] = X[k];

@@ -55,6 +55,17 @@ struct CpuExec {
     }
     for (int gl = 0; gl < W; ++gl) g(gl, R[gl], out[gl]);
   }
+  template <int K, int N, class F, class G> void pull(F f, G g) {
+    std::vector<D4> v(W);
+    for (int gl = 0; gl < W; ++gl) v[gl] = f(gl, R[gl]);
+    for (int gl = 0; gl < W; ++gl) {
+      const int src = gl + K;
+      D4 o{{0.0, 0.0, 0.0, 0.0}};
+      if (src >= 0 && src < W && src / 16 == gl / 16)  // (one 16-lane DPP row on the device)
+        for (int i = 0; i < N; ++i) o.v[i] = v[src].v[i];
+      g(gl, R[gl], o);
+    }
+  }
   template <class F> double max_value(F f) {
     double b = f(0, R[0]);
     for (int gl = 1; gl < W; ++gl) b = max_combine(b, f(gl, R[gl]));
