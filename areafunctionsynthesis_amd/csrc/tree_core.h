@@ -32,6 +32,7 @@ using std::log10;
 using std::isfinite;
 using std::pow;
 using std::sqrt;
+using std::fma;
 #endif
 
 #include "afs_model.h"
@@ -152,6 +153,7 @@ struct ArmCarry {
   double xJ;          // last lanes: the solution of their junction node (then the anchor's)
   double jd[3], jy[3], je[3], xj[3];  // junction lane: triangle pivots, rhs, edges, solutions
   int sf, sb, end;    // the arm steps this lane reduces in (forward) / solves in (back), -1: none
+  double dmin;        // smallest pivot this lane met (negative: the system is not positive definite)
 };
 // Up to four doubles handed between lanes (x.pull).
 struct D4 { double v[4]; };
@@ -1265,7 +1267,10 @@ AFS_HD inline void backward_rounds(Xc &x, double *X, const Consts &C) {
 // solves the triangle, and the solutions travel back the same way.  LDS is touched only to
 // load the rows' values and to keep the walk's factors for the back substitution.
 // ---------------------------------------------------------------------------
-AFS_HD inline double arm_recip(double d) { return (d < 0.0) ? NAN : pivot_recip(d); }
+// (A negative pivot -- the reference's Cholesky takes the square root of it -- is not
+// checked on the elimination chain: every lane keeps the smallest pivot it met in dmin and a
+// lane that met a negative one hands NaN into the back substitution.)
+AFS_HD inline double arm_min(double a, double b) { return b < a ? b : a; }
 
 // Phase A of a lane: the fold leaves, then the walk from the far end to the boundary.  Every
 // load comes before the first store, so that the loads issue back to back (the stores go to
@@ -1297,17 +1302,18 @@ AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
   a.sb = (in && !end) ? (int)r.idx : -1;
   a.end = end ? 1 : 0;
   // fold slot f: the leaf joined to positions p, p+1 (an unused slot: pivot 1, zero edges)
-  double il[ARM_FOLDS];
+  double il[ARM_FOLDS], dmin = 1.0;
 #pragma unroll
   for (int f = 0; f < ARM_FOLDS; ++f) {
     const int p = arm_fold_pos(f);
-    il[f] = arm_recip(dl[f]);
+    il[f] = pivot_recip(dl[f]);
+    dmin = arm_min(dmin, dl[f]);
     const double f0 = l0[f] * il[f], f1 = l1[f] * il[f];
-    D[p] -= f0 * l0[f];
-    Y[p] -= f0 * yl[f];
-    D[p + 1] -= f1 * l1[f];
-    Y[p + 1] -= f1 * yl[f];
-    E[p] -= f0 * l1[f];
+    D[p] = fma(-f0, l0[f], D[p]);
+    Y[p] = fma(-f0, yl[f], Y[p]);
+    D[p + 1] = fma(-f1, l1[f], D[p + 1]);
+    Y[p + 1] = fma(-f1, yl[f], Y[p + 1]);
+    E[p] = fma(-f0, l1[f], E[p]);
   }
   // the walk: position p has neighbours p+1 (edge E[p]) and the anchor (edge F, which the
   // anchor edge becomes at the first real position; dummy positions keep F = 0)
@@ -1315,12 +1321,14 @@ AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
 #pragma unroll
   for (int p = 0; p < ARM_P - 1; ++p) {
     F = (p == (int)r.start) ? ea : F;
-    const double inv = arm_recip(D[p]);
+    const double e2 = E[p] * E[p];       // (off the pivot chain: D[p+1] waits for inv only)
+    const double inv = pivot_recip(D[p]);
+    dmin = arm_min(dmin, D[p]);
     const double g = F * inv, h = E[p] * inv;
-    dA -= g * F;
-    yA -= g * Y[p];
-    D[p + 1] -= h * E[p];
-    Y[p + 1] -= h * Y[p];
+    dA = fma(-g, F, dA);
+    yA = fma(-g, Y[p], yA);
+    D[p + 1] = fma(-e2, inv, D[p + 1]);
+    Y[p + 1] = fma(-h, Y[p], Y[p + 1]);
     xat(X, r.d[p]) = inv;                // factors for the back substitution
     xat(X, r.d[p] + RHS_DELTA) = Y[p];
     xat(X, r.u[p]) = F;
@@ -1334,6 +1342,7 @@ AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
   a.Yb = Y[ARM_P - 1];
   a.dA = dA;
   a.yA = yA;
+  a.dmin = dmin;
 }
 
 // Back substitution of a lane's segment and leaves, from its boundary's solution a.x and the
@@ -1362,20 +1371,14 @@ AFS_HD inline void arm_back(const ArmRec &rr, const ArmJunction &J, bool junctio
   xs[ARM_P - 1] = a.x;
 #pragma unroll
   for (int p = ARM_P - 2; p >= 0; --p) {
-    double v = y[p];
-    v -= Ep[p] * xs[p + 1];
-    v -= Fp[p] * xA;
-    xs[p] = v * inv[p];
+    xs[p] = fma(-Fp[p], xA, fma(-Ep[p], xs[p + 1], y[p])) * inv[p];
   }
 #pragma unroll
   for (int p = 0; p < ARM_P; ++p) xat(X, r.u[p]) = xs[p];
 #pragma unroll
   for (int f = 0; f < ARM_FOLDS; ++f) {
     const int p = arm_fold_pos(f);
-    double v = yl[f];
-    v -= l0[f] * xs[p];
-    v -= l1[f] * xs[p + 1];
-    xat(X, r.lu[f]) = v * il[f];
+    xat(X, r.lu[f]) = fma(-l1[f], xs[p + 1], fma(-l0[f], xs[p], yl[f])) * il[f];
   }
   const uint32_t sink = (uint32_t)(X_U + U_SINK) * 8u;
   xat(X, junction ? J.u[0] : sink) = a.xj[0];
@@ -1404,7 +1407,7 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
                         [&](int, Lane<W> &R, const D4 &v) { R.ac.Db += v.v[0]; R.ac.Yb += v.v[1]; });
   // the fossa lane folds 84 into 28 (lane ARM_L28) and 29 (lane ARM_L28 + 1); every other
   // lane's fossa edges are zero, so it sends zeros
-  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.inv = arm_recip(R.ac.Db); });
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.inv = pivot_recip(R.ac.Db); });
   x.template pull<ARM_FOSSA - ARM_L28, 2>(
       [&](int, Lane<W> &R) {
         const double c0 = R.ac.e28 * R.ac.inv;
@@ -1417,29 +1420,31 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
         return D4{{c1 * R.ac.e29, c1 * R.ac.Yb, c0 * R.ac.e29, 0.0}};
       },
       [&](int, Lane<W> &R, const D4 &v) { R.ac.Db -= v.v[0]; R.ac.Yb -= v.v[1]; R.ac.F -= v.v[2]; });
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.dmin = arm_min(R.ac.dmin, R.ac.Db); });
   // arm reduction toward the junction: in step s the lanes at position s of their arm
   // eliminate the previous boundary (lane k-1) from their own
-  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.inv = arm_recip(R.ac.Db); });
+  // (a lane off its step updates with a zero edge: no change, the same reciprocal again)
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.inv = pivot_recip(R.ac.Db); });
 #pragma unroll
   for (int s = 1; s < ARM_MAXLEN; ++s) {
     x.template pull<-1, 2>([&](int, Lane<W> &R) { return D4{{R.ac.inv, R.ac.Yb, 0.0, 0.0}}; },
                            [&](int, Lane<W> &R, const D4 &v) {
-                             const bool on = R.ac.sf == s;
-                             const double f = R.ac.F * v.v[0];
-                             const double nd = R.ac.Db - f * R.ac.F, ny = R.ac.Yb - f * v.v[1];
-                             R.ac.Db = on ? nd : R.ac.Db;
-                             R.ac.Yb = on ? ny : R.ac.Yb;
-                             R.ac.inv = on ? arm_recip(nd) : R.ac.inv;
+                             const double Fs = (R.ac.sf == s) ? R.ac.F : 0.0;
+                             const double F2 = Fs * Fs, f = Fs * v.v[0];
+                             R.ac.Db = fma(-F2, v.v[0], R.ac.Db);
+                             R.ac.Yb = fma(-f, v.v[1], R.ac.Yb);
+                             R.ac.inv = pivot_recip(R.ac.Db);
                            });
   }
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.dmin = arm_min(R.ac.dmin, R.ac.Db); });
   // the junction lane takes the three arms' last boundaries (pivot inverse, rhs, edge) and
   // solves the triangle: eliminate 65, then 41; solve 40 (uniform code on every lane)
   auto give = [&](int, Lane<W> &R) { return D4{{R.ac.inv, R.ac.Yb, R.ac.ej, 0.0}}; };
   auto take = [&](int q) {
     return [&, q](int, Lane<W> &R, const D4 &v) {
       const double g = v.v[2] * v.v[0];
-      R.ac.jd[q] -= g * v.v[2];
-      R.ac.jy[q] -= g * v.v[1];
+      R.ac.jd[q] = fma(-g, v.v[2], R.ac.jd[q]);
+      R.ac.jy[q] = fma(-g, v.v[1], R.ac.jy[q]);
     };
   };
   x.template pull<ARM_END_A - ARM_JUNCTION, 3>(give, take(0));
@@ -1449,27 +1454,23 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
     double *d = R.ac.jd, *y = R.ac.jy;
     double e01 = R.ac.je[0];
     const double e02 = R.ac.je[1], e12 = R.ac.je[2];
-    const double i2 = arm_recip(d[2]);
+    const double i2 = pivot_recip(d[2]);
     const double g0 = e02 * i2, g1 = e12 * i2;
-    d[0] -= g0 * e02;
-    y[0] -= g0 * y[2];
-    d[1] -= g1 * e12;
-    y[1] -= g1 * y[2];
-    e01 -= g0 * e12;
-    const double i1 = arm_recip(d[1]);
+    d[0] = fma(-g0, e02, d[0]);
+    y[0] = fma(-g0, y[2], y[0]);
+    d[1] = fma(-g1, e12, d[1]);
+    y[1] = fma(-g1, y[2], y[1]);
+    e01 = fma(-g0, e12, e01);
+    const double i1 = pivot_recip(d[1]);
     const double h = e01 * i1;
-    d[0] -= h * e01;
-    y[0] -= h * y[1];
-    const double x0 = y[0] * arm_recip(d[0]);
-    double v1 = y[1];
-    v1 -= e01 * x0;
-    const double x1 = v1 * i1;
-    double v2 = y[2];
-    v2 -= e02 * x0;
-    v2 -= e12 * x1;
+    d[0] = fma(-h, e01, d[0]);
+    y[0] = fma(-h, y[1], y[0]);
+    const double dm = arm_min(arm_min(d[0], d[1]), d[2]);
+    const double x0 = (dm < 0.0) ? NAN : y[0] * pivot_recip(d[0]);
+    const double x1 = fma(-e01, x0, y[1]) * i1;
     R.ac.xj[0] = x0;
     R.ac.xj[1] = x1;
-    R.ac.xj[2] = v2 * i2;
+    R.ac.xj[2] = fma(-e12, x1, fma(-e02, x0, y[2])) * i2;
   });
   x.template pull<ARM_JUNCTION - ARM_END_A, 1>([&](int, Lane<W> &R) { return D4{{R.ac.xj[0], 0.0, 0.0, 0.0}}; },
                                                [&](int k, Lane<W> &R, const D4 &v) { if (k == ARM_END_A) R.ac.xJ = v.v[0]; });
@@ -1483,18 +1484,14 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
   x.template pull<1, 1>([&](int, Lane<W> &R) { return D4{{R.ac.F, 0.0, 0.0, 0.0}}; },
                         [&](int, Lane<W> &R, const D4 &v) { R.ac.Fn = v.v[0]; });
   x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
-    double v = R.ac.Yb;
-    v -= R.ac.ej * R.ac.xJ;
-    R.ac.x = R.ac.end ? v * R.ac.inv : 0.0;
+    R.ac.x = R.ac.end ? fma(-R.ac.ej, R.ac.xJ, R.ac.Yb) * R.ac.inv : 0.0;
   });
 #pragma unroll
   for (int s = ARM_MAXLEN - 2; s >= 0; --s) {
     x.template pull<1, 1>([&](int, Lane<W> &R) { return D4{{R.ac.x, 0.0, 0.0, 0.0}}; },
                           [&](int, Lane<W> &R, const D4 &v) {
                             const bool on = R.ac.sb == s;
-                            double t = R.ac.Yb;
-                            t -= R.ac.Fn * v.v[0];
-                            R.ac.x = on ? t * R.ac.inv : R.ac.x;
+                            R.ac.x = on ? fma(-R.ac.Fn, v.v[0], R.ac.Yb) * R.ac.inv : R.ac.x;
                           });
   }
   // the fossa lane: 84 from 28 and 29
@@ -1502,11 +1499,17 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
                                           [&](int, Lane<W> &R, const D4 &v) { R.ac.Fn = v.v[0]; });
   x.template pull<ARM_L28 + 1 - ARM_FOSSA, 1>([&](int, Lane<W> &R) { return D4{{R.ac.x, 0.0, 0.0, 0.0}}; },
                                               [&](int k, Lane<W> &R, const D4 &v) {
-                                                double t = R.ac.Yb;
-                                                t -= R.ac.e28 * R.ac.Fn;
-                                                t -= R.ac.e29 * v.v[0];
+                                                const double t = fma(-R.ac.e29, v.v[0], fma(-R.ac.e28, R.ac.Fn, R.ac.Yb));
                                                 R.ac.x = (k == ARM_FOSSA) ? t * R.ac.inv : R.ac.x;
                                               });
+  // a negative pivot anywhere: every solution of this sample is NaN (as the reference's
+  // Cholesky produces from the square root of a negative pivot on)
+  const bool bad = x.ballot([&](int gl, Lane<W> &R) { return gl < TREE_CHAINS && R.ac.dmin < 0.0; }) != 0;
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
+    R.ac.x = bad ? NAN : R.ac.x;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) R.ac.xj[q] = bad ? NAN : R.ac.xj[q];
+  });
   x.mark(PH_FORWARD);
   // every lane's segment from its boundary and its anchor (lane k-1's boundary)
   x.template pull<-1, 1>([&](int, Lane<W> &R) { return D4{{R.ac.x, 0.0, 0.0, 0.0}}; },
