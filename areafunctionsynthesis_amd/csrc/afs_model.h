@@ -67,33 +67,11 @@ AFS_HD constexpr bool is_static_section(int s) {
   return s <= S_LAST_TRACHEA || (s >= S_NOSE0 + 4);
 }
 
-// LDL^T schedule for the per-sample system (tree solver, afs_tables.cpp tree_schedule).
-// Edges of the current graph: for section s with in-current a and out-currents b (c),
-// edge[s][0] = (a,b), edge[s][1] = (a,c), edge[s][2] = (b,c).  In round r, chain lane k
-// eliminates step[r][k].c, whose remaining neighbours are n0 (and n1) through edges e0
-// (e1); e01 is the edge n0-n1 that receives the update (a fill edge when n0 and n1 were not
-// adjacent).  Edge storage ids: 0..TREE_NE-1 = X_OFF slots, TREE_NE + f = fill edge f
-// (X_FILL slot f, zeroed before the forward pass).  c = -1: idle.
-constexpr int TREE_CHAINS = 16;
-constexpr int TREE_MAX_ROUNDS = 14;
-// The plan's round count and the rounds whose pivot (forward) / neighbour solution (backward)
-// stays in registers; the kernel unrolls the rounds with these, and build_tables checks that
-// the schedule it derives from the plan has exactly these values.
-constexpr int TREE_ROUNDS = 12;
-constexpr uint64_t TREE_FWD_CARRY = 0xfd0, TREE_BWD_CARRY = 0x480;
-constexpr int TREE_NFILL = 64;  // fill edges (tree_core.h X_FILL)
+// Edges of the current graph (afs_tables.cpp edge_numbering): for section s with in-current
+// a and out-currents b (c), edge[s][0] = (a,b), edge[s][1] = (a,c), edge[s][2] = (b,c);
+// TREE_NE of them, each with its own LDS slot.
+constexpr int TREE_CHAINS = 16;  // lanes of the per-sample solver
 constexpr int TREE_NE = 104;
-struct SolveStep {
-  int16_t c, n0, n1, e0, e1, e01;
-};
-// The kernel's form of a step: LDS byte offsets inside the utterance block, 16 bytes = one
-// LDS load.  c/n0/n1 address the pivot (rhs at a fixed distance), e0/e1/e01 the edges,
-// un0/un1 the solutions of n0/n1.  Absent neighbours and idle lanes point at sink slots
-// (written, never read for real work) or zero slots (0.0, never written), so a round has
-// no branches.
-struct alignas(16) StepRec {
-  uint16_t c, n0, n1, e0, e1, e01, un0, un1;
-};
 // Arm solver (tree_core.h solve_arms; afs_tables.cpp arm_records).  The current graph is a
 // junction triangle {40, 41, 65} with three arms (A: 0..39 with the fossa 84..88 on {28, 29};
 // B: 42..64 with the radiation pair 93/94; C: 66..83 with the pair 95/96 and the sinus leaves
@@ -188,13 +166,10 @@ struct Hot {
 // Values that steer branches in the time loop: kernel arguments on the device, so the
 // compiler keeps them in scalar registers and branches on them uniformly.
 struct Uni {
-  int32_t n_rounds;
-  uint64_t fwd_carry, bwd_carry;
   afs_options opt;
 };
 struct Consts {
   Hot h;
-  StepRec step[TREE_MAX_ROUNDS][TREE_CHAINS];
   ArmRec arm[TREE_CHAINS];
   ArmJunction armj;
   int8_t ur_slot[NC];  // X_UR slot of a current, -1: none
@@ -233,13 +208,10 @@ struct Tables {
   // SOR rows: filledRowIndex (TdsModel.cpp:340-357), ascending columns, at most 16
   int16_t row_n[NC], row[NC][16];
 
-  // tree solver
+  // tree solver: edge numbering; n_rounds = the arm solver's sequential reduction steps
+  // (ARM_MAXLEN - 1), -1 when the tables fail their checks
   int16_t edge[NS][3];
   int32_t n_edges, n_rounds;
-  // bit r: in forward (backward) round r every active chain lane finds the pivot (the
-  // solution of n0) in its registers -- uniform per round, see tree_schedule.
-  uint64_t fwd_carry, bwd_carry;
-  SolveStep step[TREE_MAX_ROUNDS][TREE_CHAINS];
   Consts consts;
   Uni uni;
 

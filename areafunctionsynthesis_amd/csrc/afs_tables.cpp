@@ -146,31 +146,9 @@ void topology(Tables *t) {
   }
 }
 
-// Edges of the current graph and the elimination schedule of the tree solver.
-// Sixteen lanes eliminate up to sixteen unknowns per round.  An unknown can go when it has
-// at most two remaining neighbours; the lanes of a round touch disjoint unknowns and edges;
-// eliminating c with non-adjacent neighbours n0, n1 creates the fill edge n0-n1 (its own
-// X_FILL slot).  Like a path (which loses at most a third of its nodes per round under these
-// rules), the graph needs 12 rounds; the plan below was found by a randomised greedy list
-// schedule (tools/sched_search.py) and assigns each step to the lane that eliminated its
-// neighbour the round before where it can, so that the pivot stays in registers.  The
-// builder re-derives every step symbolically and rejects a plan that breaks a rule.
-static const int8_t TREE_PLAN[12][TREE_CHAINS] = {
-    {0, 3, 6, 9, 12, 15, 93, 18, 61, 95, 21, 58, 81, 24, 55, 88},
-    {1, 92, 5, 10, 53, 14, 94, 19, 62, 96, 27, 57, 80, 23, 50, 87},
-    {2, 78, 90, 8, 52, 16, 64, 30, 72, 83, 48, 59, 33, 22, 45, 86},
-    {4, 91, 89, 70, 54, 13, 63, 31, 35, 82, 47, 67, 43, 25, 38, 85},
-    {7, -1, 74, 69, -1, -1, 60, -1, 34, 79, 49, -1, 42, 20, 39, 84},
-    {11, 76, -1, 71, -1, -1, 56, -1, -1, -1, -1, -1, 44, -1, 37, 29},
-    {17, 77, -1, 68, -1, -1, 51, -1, -1, -1, -1, -1, -1, -1, -1, 32},
-    {26, 75, -1, -1, -1, -1, 46, -1, -1, -1, -1, -1, -1, -1, -1, -1},
-    {28, 73, -1, -1, -1, -1, 41, -1, -1, -1, -1, -1, -1, -1, -1, -1},
-    {36, 66, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1},
-    {-1, 65, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1},
-    {-1, 40, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1},
-};
-
-bool tree_schedule(Tables *t) {
+// Edge numbering of the current graph (afs_model.h); the arm solver's records address the
+// edges' LDS slots by these ids.
+bool edge_numbering(Tables *t) {
   int e = 0;
   for (int s = 0; s < NS; ++s) {
     t->edge[s][0] = t->edge[s][1] = t->edge[s][2] = -1;
@@ -181,116 +159,7 @@ bool tree_schedule(Tables *t) {
     }
   }
   t->n_edges = e;
-  if (e != TREE_NE) return false;
-  // current graph: edge storage id per pair (-1: not adjacent)
-  static int16_t eid[NC][NC];
-  for (int i = 0; i < NC; ++i)
-    for (int j = 0; j < NC; ++j) eid[i][j] = -1;
-  for (int s = 0; s < NS; ++s) {
-    const int m[3] = {t->cin[s], t->cout0[s], t->cout1[s]};
-    const int pk[3][3] = {{-1, 0, 1}, {0, -1, 2}, {1, 2, -1}};  // edge index of pair (a,b)
-    for (int a = 0; a < 3; ++a)
-      for (int b = 0; b < 3; ++b)
-        if (a != b && m[a] >= 0 && m[b] >= 0) eid[m[a]][m[b]] = t->edge[s][pk[a][b]];
-  }
-  int prog[TREE_MAX_ROUNDS][TREE_CHAINS];
-  int order[NC];
-  for (int i = 0; i < NC; ++i) order[i] = -1;
-  for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
-    for (int k = 0; k < TREE_CHAINS; ++k) prog[r][k] = -1;
-  const int rounds = (int)(sizeof(TREE_PLAN) / sizeof(TREE_PLAN[0]));
-  if (rounds > TREE_MAX_ROUNDS - 2) return false;
-  for (int r = 0; r < rounds; ++r)
-    for (int k = 0; k < TREE_CHAINS; ++k) {
-      const int c = TREE_PLAN[r][k];
-      if (c < 0) continue;
-      if (c >= NC || order[c] != -1) return false;
-      prog[r][k] = c;
-      order[c] = r;
-    }
-  for (int i = 0; i < NC; ++i)
-    if (order[i] < 0) return false;
-  t->n_rounds = rounds;
-  // Symbolic elimination in lock step: at most two remaining neighbours per step, lanes of a
-  // round touch disjoint unknowns and edges, every fill edge gets its own X_FILL slot.
-  bool gone[NC] = {false};
-  int nfill = 0;
-  for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
-    for (int k = 0; k < TREE_CHAINS; ++k) t->step[r][k] = SolveStep{-1, -1, -1, -1, -1, -1};
-  for (int r = 0; r < rounds; ++r) {
-    std::vector<int> wr[TREE_CHAINS], rd[TREE_CHAINS];  // ids: unknowns, 1000 + edge storage
-    for (int k = 0; k < TREE_CHAINS; ++k) {
-      const int c = prog[r][k];
-      if (c < 0) continue;
-      int nb[NC], n = 0;
-      for (int j = 0; j < NC; ++j)
-        if (!gone[j] && j != c && eid[c][j] >= 0) nb[n++] = j;
-      if (n > 2) return false;
-      const int nxt = (r + 1 < rounds) ? prog[r + 1][k] : -1;
-      if (n == 2 && nb[1] == nxt) std::swap(nb[0], nb[1]);
-      SolveStep st{(int16_t)c, -1, -1, -1, -1, -1};
-      if (n >= 1) { st.n0 = (int16_t)nb[0]; st.e0 = eid[c][nb[0]]; }
-      if (n == 2) { st.n1 = (int16_t)nb[1]; st.e1 = eid[c][nb[1]]; st.e01 = eid[nb[0]][nb[1]]; }
-      for (int q : {(int)st.c, (int)st.n0, (int)st.n1}) if (q >= 0) { wr[k].push_back(q); rd[k].push_back(q); }
-      for (int q : {(int)st.e0, (int)st.e1}) if (q >= 0) rd[k].push_back(1000 + q);
-      if (st.e01 >= 0) { wr[k].push_back(1000 + st.e01); rd[k].push_back(1000 + st.e01); }
-      t->step[r][k] = st;
-    }
-    for (int a = 0; a < TREE_CHAINS; ++a)
-      for (int b = 0; b < TREE_CHAINS; ++b)
-        if (a != b)
-          for (int x : wr[a])
-            for (int y : rd[b])
-              if (x == y) return false;
-    // apply: fill edges, eliminations
-    for (int k = 0; k < TREE_CHAINS; ++k) {
-      SolveStep &st = t->step[r][k];
-      if (st.c < 0) continue;
-      if (st.n1 >= 0 && st.e01 < 0) {
-        if (nfill >= TREE_NFILL) return false;
-        const int id = TREE_NE + nfill++;
-        eid[st.n0][st.n1] = eid[st.n1][st.n0] = (int16_t)id;
-        st.e01 = (int16_t)id;
-      }
-    }
-    for (int k = 0; k < TREE_CHAINS; ++k)
-      if (t->step[r][k].c >= 0) gone[t->step[r][k].c] = true;
-  }
-  // Register carries (tree_core.h solve_forward / solve_backward).  Forward: after a step
-  // the lane holds the new pivot of its n0, valid until another lane touches that unknown;
-  // an idle round (sink step) overwrites it.  Backward: the lane holds the solution of the
-  // unknown it solved last; a round is flagged when every active lane's n0 is that unknown.
-  t->fwd_carry = 0;
-  int carry[TREE_CHAINS];
-  for (int k = 0; k < TREE_CHAINS; ++k) carry[k] = -1;
-  for (int r = 0; r < rounds; ++r) {
-    bool all = true;
-    for (int k = 0; k < TREE_CHAINS; ++k) {
-      const SolveStep &st = t->step[r][k];
-      if (st.c >= 0 && st.c != carry[k]) all = false;
-    }
-    if (all) t->fwd_carry |= 1ull << r;
-    for (int k = 0; k < TREE_CHAINS; ++k) {
-      const SolveStep &st = t->step[r][k];
-      carry[k] = st.c >= 0 ? st.n0 : -1;
-      for (int q : {(int)st.c, (int)st.n0, (int)st.n1})  // touched by lane k: others' carries die
-        for (int j = 0; j < TREE_CHAINS; ++j)
-          if (j != k && q >= 0 && carry[j] == q) carry[j] = -1;
-    }
-  }
-  t->bwd_carry = 0;
-  for (int k = 0; k < TREE_CHAINS; ++k) carry[k] = -1;
-  for (int r = rounds - 1; r >= 0; --r) {
-    bool all = true;
-    for (int k = 0; k < TREE_CHAINS; ++k) {
-      const SolveStep &st = t->step[r][k];
-      if (st.c >= 0 && (st.n0 < 0 || st.n0 != carry[k])) all = false;
-    }
-    if (all) t->bwd_carry |= 1ull << r;
-    for (int k = 0; k < TREE_CHAINS; ++k) carry[k] = t->step[r][k].c;
-  }
-  // the tree kernel unrolls the rounds with these values compiled in (afs_model.h)
-  return t->n_rounds == TREE_ROUNDS && t->fwd_carry == TREE_FWD_CARRY && t->bwd_carry == TREE_BWD_CARRY;
+  return e == TREE_NE;
 }
 
 // The arm solver's lane records (afs_model.h ArmRec, tree_core.h solve_arms).  The partition
@@ -482,8 +351,7 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   static_network(t);
   t->fossa_R0 = 8.0 * MU * t->len[S_FOSSA0] * PI / (AMIN * AMIN);
   topology(t);
-  t->n_rounds = tree_schedule(t) ? t->n_rounds : -1;
-  if (!arm_records(t)) t->n_rounds = -1;
+  t->n_rounds = (edge_numbering(t) && arm_records(t)) ? ARM_MAXLEN - 1 : -1;
   // packed copy for the cooperative kernel
   Consts &c = t->consts;
   Hot &h = c.h;
@@ -508,21 +376,6 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   // step records: LDS byte offsets of the tree kernel's utterance block (tree_core.h)
   using namespace tree;
   auto off = [](int slot) { return (uint16_t)(slot * 8); };
-  auto eoff = [&](int id) { return id < TREE_NE ? off(X_OFF + id) : off(X_FILL + (id - TREE_NE)); };
-  for (int r = 0; r < TREE_MAX_ROUNDS; ++r)
-    for (int k = 0; k < TREE_CHAINS; ++k) {
-      const SolveStep &st = t->step[r][k];
-      const bool on = r < t->n_rounds && st.c >= 0;
-      StepRec &q = c.step[r][k];
-      q.c = off(X_DIAG + (on ? st.c : NODE_SINK));
-      q.n0 = off(X_DIAG + (on && st.n0 >= 0 ? st.n0 : NODE_SINK));
-      q.n1 = off(X_DIAG + (on && st.n1 >= 0 ? st.n1 : NODE_SINK));
-      q.e0 = on && st.n0 >= 0 ? eoff(st.e0) : off(X_OFF + EDGE_ZERO);
-      q.e1 = on && st.n1 >= 0 ? eoff(st.e1) : off(X_OFF + EDGE_ZERO);
-      q.e01 = on && st.n0 >= 0 && st.n1 >= 0 ? eoff(st.e01) : off(X_OFF + EDGE_SINK);
-      q.un0 = off(X_U + (on && st.n0 >= 0 ? st.n0 : U_ZERO));
-      q.un1 = off(X_U + (on && st.n1 >= 0 ? st.n1 : U_ZERO));
-    }
   // X_UR slots: both outputs of every bifurcation (their partner reads d/dt of the flow)
   std::memset(c.ur_slot, -1, sizeof c.ur_slot);
   int nur = 0;
@@ -543,9 +396,6 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   for (int s = S_GLOT_UP; s <= S_LAST_MOUTH; ++s) { add_un(t->cout0[s]); add_un(t->cout1[s]); }
   add_un(t->cout0[S_LAST_NOSE]);
   add_un(t->cout1[S_LAST_NOSE]);
-  t->uni.n_rounds = t->n_rounds;
-  t->uni.fwd_carry = t->fwd_carry;
-  t->uni.bwd_carry = t->bwd_carry;
   t->uni.opt = t->opt;
   for (int s = 0; s < NS; ++s) {
     Topo &q = c.topo[s];

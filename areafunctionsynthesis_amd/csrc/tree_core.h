@@ -48,11 +48,6 @@ using std::fma;
 #define AFS_LDS_DRAIN() ((void)0)
 #endif
 
-// The per-sample solver: 1 = the arm solver (solve_arms), 0 = the LDS rounds.
-#ifndef AFS_ARM_SOLVER
-#define AFS_ARM_SOLVER 1
-#endif
-
 namespace afs {
 namespace tree {
 
@@ -80,9 +75,10 @@ enum : int {
   //   sink slots of the phases before the rows (n): stores of lanes / slots with nothing to store
   X_ACT = X_UNION, X_NOISE_END = X_ACT + 16,
   //   solver
-  //   (pivot / rhs with a sink slot at NC; edges with EDGE_ZERO and EDGE_SINK after TREE_NE)
-  X_DIAG = X_UNION, X_RHS = X_DIAG + NC + 2, X_OFF = X_RHS + NC + 2, X_FILL = X_OFF + TREE_NE + 2,
-  X_SOLVE_END = X_FILL + TREE_NFILL,
+  //   (pivot / rhs with a sink slot at NC and the dummy pivot at NC+1; edges with EDGE_ZERO
+  //   and EDGE_SINK after TREE_NE)
+  X_DIAG = X_UNION, X_RHS = X_DIAG + NC + 2, X_OFF = X_RHS + NC + 2,
+  X_SOLVE_END = X_OFF + TREE_NE + 2,
   X_AFTER = (X_NOISE_END > X_SOLVE_END ? X_NOISE_END : X_SOLVE_END),
   // frame-rate values written by lane 0 at every frame transition
   X_FRAME = X_AFTER,           // teethL, teethR, velL, velR, gL[6], gR[6]
@@ -114,10 +110,9 @@ enum : int {
   PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_TARGETS, PH_COUNT
 };
 
-// Solver sink / zero slots (see StepRec).
+// Solver sink / zero slots (see ArmRec).
 constexpr int NODE_SINK = NC, U_SINK = NC, U_ZERO = NC + 1, EDGE_ZERO = TREE_NE, EDGE_SINK = TREE_NE + 1;
 constexpr uint32_t RHS_DELTA = (uint32_t)(X_RHS - X_DIAG) * 8u;  // bytes from a pivot to its rhs
-constexpr uint32_t U_DELTA = (uint32_t)(X_DIAG - X_U) * 8u;      // bytes from a pivot to its solution
 
 template <int W>
 struct Shape {
@@ -136,12 +131,6 @@ AFS_HD inline int static_section(int W, int j, int gl) {
   return k < NSTATS ? (k < 23 ? k : k + 46) : -1;
 }
 
-// Solver chain lane registers: the next step (prefetched) and the unknown this lane updated
-// last together with its new pivot / right-hand side (forward) or solution (backward).
-struct SolveCarry {
-  StepRec cur, next;  // this round's step and the next (prefetched)
-  double d, y;        // forward: pivot and rhs of the last n0; backward: y = last solution
-};
 // Arm solver lane registers (solve_arms).
 struct ArmCarry {
   double Db, Yb;      // pivot and rhs of the lane's boundary (reduced in place)
@@ -208,7 +197,7 @@ AFS_HD inline double fast_div(double a, double b) {
 #endif
 }
 
-// The double at LDS byte offset b of an utterance block (SecRec / StepRec fields).
+// The double at LDS byte offset b of an utterance block (SecRec / ArmRec fields).
 AFS_HD inline double &xat(double *X, uint32_t b) { return *reinterpret_cast<double *>(reinterpret_cast<char *>(X) + b); }
 AFS_HD inline const double &xat(const double *X, uint32_t b) {
   return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(X) + b);
@@ -230,7 +219,6 @@ struct Lane {
   uint64_t planw;                                                    // word gl of this sample's plan (tree_plan.h)
   uint32_t racc[S::NDP];                                             // rand() sums of owned dipoles
   uint32_t rtmp[3];                                                  // rand() block scratch
-  SolveCarry sc;                                                     // chain lanes, during the solve
   ArmCarry ac;                                                       // arm solver, during the solve
   // per-sample values of the geometry/network block (not state: cleared before a save)
   double acur[S::ND], lcur[S::ND];                                   // area, length of the slots
@@ -1172,92 +1160,6 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
 }
 
 // ---------------------------------------------------------------------------
-// Solver rounds (chain lanes 0 .. TREE_CHAINS-1).
-// ---------------------------------------------------------------------------
-AFS_HD inline double &lds_at(double *X, uint32_t byte_off) {
-  return *reinterpret_cast<double *>(reinterpret_cast<char *>(X) + byte_off);
-}
-
-// Forward round of chain lane k: eliminate c, update n0 and n1 (the sink when absent) and
-// the edge n0-n1.  Rounds touch disjoint unknowns (checked when the schedule is built), so
-// the pivot and right-hand side this lane computes for n0 stay exact until another lane
-// touches that unknown: in the rounds of U.fwd_carry every active lane continues its chain
-// with them from registers (a uniform branch).  (Loading the next round's operands ahead
-// was measured slower: the extra live registers cost more than the latency they hide.)
-// The round body, instantiated separately for a pivot from registers and from LDS so that
-// the reciprocal of a carried pivot does not wait for the neighbours' loads.
-template <bool CARRIED>
-AFS_HD inline void forward_body(const StepRec &s, double *X, SolveCarry &cr) {
-  double d0 = lds_at(X, s.n0), y0 = lds_at(X, s.n0 + RHS_DELTA);
-  const double d1 = lds_at(X, s.n1), y1 = lds_at(X, s.n1 + RHS_DELTA);
-  const double a0 = lds_at(X, s.e0), a1 = lds_at(X, s.e1), a01 = lds_at(X, s.e01);
-  const double d = CARRIED ? cr.d : lds_at(X, s.c);
-  const double y = CARRIED ? cr.y : lds_at(X, s.c + RHS_DELTA);
-  const double inv = (d < 0.0) ? NAN : pivot_recip(d);  // the reference takes sqrt of a negative pivot
-  lds_at(X, s.c) = inv;  // the rhs slot of c already holds y (written by whoever updated it last)
-  const double f0 = a0 * inv, f1 = a1 * inv;
-  d0 -= f0 * a0;
-  y0 -= f0 * y;
-  lds_at(X, s.n0) = d0;
-  lds_at(X, s.n0 + RHS_DELTA) = y0;
-  cr.d = d0;
-  cr.y = y0;
-  lds_at(X, s.n1) = d1 - f1 * a1;
-  lds_at(X, s.n1 + RHS_DELTA) = y1 - f1 * y;
-  lds_at(X, s.e01) = a01 - f0 * a1;
-}
-
-template <int R>
-AFS_HD inline void solve_forward(int k, double *X, const Consts &C, SolveCarry &cr) {
-  const StepRec s = cr.cur;
-  cr.cur = cr.next;
-  cr.next = C.step[R + 2 < TREE_MAX_ROUNDS ? R + 2 : TREE_MAX_ROUNDS - 1][k];
-  forward_body<((TREE_FWD_CARRY >> R) & 1) != 0>(s, X, cr);
-}
-
-// Backward round (descending): x_c = (y_c - a0 x_n0 - a1 x_n1) / d_c (absent neighbours read
-// a zero edge and a zero solution).  In the rounds of U.bwd_carry x_n0 is the solution this
-// lane produced last (registers).
-template <bool CARRIED>
-AFS_HD inline void backward_body(const StepRec &s, double *X, SolveCarry &cr) {
-  double y = lds_at(X, s.c + RHS_DELTA);
-  const double inv = lds_at(X, s.c);
-  const double a0 = lds_at(X, s.e0), a1 = lds_at(X, s.e1), x1 = lds_at(X, s.un1);
-  const double x0 = CARRIED ? cr.y : lds_at(X, s.un0);
-  y -= a0 * x0;
-  y -= a1 * x1;
-  const double xc = y * inv;
-  lds_at(X, s.c - U_DELTA) = xc;
-  cr.y = xc;
-}
-
-template <int R>
-AFS_HD inline void solve_backward(int k, double *X, const Consts &C, SolveCarry &cr) {
-  const StepRec s = cr.cur;
-  cr.cur = cr.next;
-  cr.next = C.step[R >= 2 ? R - 2 : 0][k];
-  backward_body<((TREE_BWD_CARRY >> R) & 1) != 0>(s, X, cr);
-}
-
-// The rounds, unrolled (TREE_ROUNDS, the carried rounds compiled in: no loop and no branch).
-template <int W, int R, class Xc>
-AFS_HD inline void forward_rounds(Xc &x, double *X, const Consts &C) {
-  if constexpr (R < TREE_ROUNDS) {
-    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &L) { solve_forward<R>(k, X, C, L.sc); });
-    x.sync();
-    forward_rounds<W, R + 1>(x, X, C);
-  }
-}
-template <int W, int R, class Xc>
-AFS_HD inline void backward_rounds(Xc &x, double *X, const Consts &C) {
-  if constexpr (R >= 0) {
-    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &L) { solve_backward<R>(k, X, C, L.sc); });
-    x.sync();
-    backward_rounds<W, R - 1>(x, X, C);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Arm solver (afs_model.h ArmRec; partition and checks in afs_tables.cpp arm_records).
 // The same LDL^T of the same matrix as the rounds above, in an order that keeps the
 // eliminations in registers: every lane folds the leaves of its segment and walks the segment
@@ -1719,7 +1621,7 @@ AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts
 // both models' code needs more registers than the SIMD has).
 template <int W, int MODEL, class Xc>
 AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio, bool defer_out) {
-  static_assert(W >= TREE_CHAINS, "every solver chain needs a lane of the utterance");
+  static_assert(W >= TREE_CHAINS, "every solver lane needs a lane of the utterance");
   // geometry and network in one block (no LDS round trip between them): the interpolated
   // areas stay in the lanes, the neighbours' come by lane exchange, the glottis values are
   // lane-uniform
@@ -1742,34 +1644,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.par([&](int gl, Lane<W> &R) { phase_rows<W>(gl, R, X, X, U, C); });
   x.sync();
   x.mark(PH_ROWS);
-#if AFS_ARM_SOLVER
   solve_arms<W>(x, X, C);
-#else
-  constexpr int nr = TREE_ROUNDS;  // (build_tables checks the schedule against it)
-  // fill edges start at zero (zeroing them inside the row block instead: measured neutral)
-  x.par([&](int gl, Lane<W> &R) {
-    (void)R;
-#pragma unroll
-    for (int i = gl; i < TREE_NFILL; i += W) X[X_FILL + i] = 0.0;
-  });
-  x.sync();
-  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) {
-    R.sc.cur = C.step[0][k];
-    R.sc.next = C.step[1][k];
-    R.sc.d = R.sc.y = 0.0;
-  });
-  AFS_LDS_DRAIN();  // the first round must not wait for the previous round's stores
-  forward_rounds<W, 0>(x, X, C);
-  x.mark(PH_FORWARD);
-  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) {
-    R.sc.cur = C.step[nr - 1][k];
-    R.sc.next = C.step[nr >= 2 ? nr - 2 : 0][k];
-    R.sc.y = 0.0;
-  });
-  AFS_LDS_DRAIN();
-  backward_rounds<W, nr - 1>(x, X, C);
-  x.mark(PH_BACKWARD);
-#endif
   // the state update and the output stage (lane-uniform: radiated flow, filters) in one phase
   x.par_uniform([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, X, U, C); },
                 [&](Lane<W> &R) { R.sample = phase_output(X, U, C, section_pressure(X, C, S_PHARYNX0), defer_out); });

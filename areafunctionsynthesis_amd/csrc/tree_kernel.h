@@ -230,7 +230,6 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
 #pragma unroll
     for (int j = 0; j < Shape<TW>::ND; ++j) R.acur[j] = R.lcur[j] = R.anx[j] = R.apv[j] = 0.0;
     R.ac = ArmCarry{};
-    R.sc = SolveCarry{};
     ((Lane<TW> *)a.lane_state)[(int64_t)u * TW + gl] = R;
     double *ws = a.lds_state + (int64_t)u * X_TOTAL;
     for (int k = gl; k < X_TOTAL; k += TW) ws[k] = X[k];

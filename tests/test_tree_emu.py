@@ -1,6 +1,6 @@
 """CPU check of the cooperative tree kernel's decomposition (test-only host build of
 csrc/tree_core.h, see tests/emu/tree_emu.cpp): lane ownership, LDS exchange and the
-fill-free LDL^T schedule reproduce the oracle to rounding level, for any lane width."""
+arm-solver LDL^T reproduce the oracle to rounding level, for any lane width."""
 import ctypes
 import os
 import subprocess
@@ -55,8 +55,9 @@ def emu():
 
 
 def test_schedule_is_valid(emu):
-    # build_tables verifies fill-freeness / round conflicts and reports -1 otherwise
-    assert emu.lib.emu_tree_rounds(22050.0) == 12  # 16-lane plan (afs_tables.cpp tree_schedule)
+    # build_tables checks the arm partition (every current and every edge of the graph in
+    # exactly one role) and reports -1 otherwise; else the arm reduction's 6 sequential steps
+    assert emu.lib.emu_tree_rounds(22050.0) == 6  # afs_tables.cpp arm_records
 
 
 def test_golden_utterances(emu, golden_dir):
