@@ -86,27 +86,26 @@ constexpr int ARM_FOSSA = 14, ARM_JUNCTION = 15, ARM_L28 = 3;
 constexpr int ARM_END_A = 6, ARM_END_B = 10, ARM_END_C = 13;  // lanes of the arms' last boundaries
 AFS_HD constexpr int arm_fold_pos(int f) { return f == 0 ? 2 : f == 1 ? 3 : f == 2 ? 5 : 6; }
 enum : uint8_t { ARM_IN = 1, ARM_END = 2 };
-// LDS layout of the solver (tree_core.h X_ASP / X_ALF / X_ABK): one block of ARM_BLK doubles
-// per lane (the junction lane, which has no segment, shares the block of lane ARM_L28 + 1,
-// whose positions 0..6 are dummies), four leaf bases of 16 (ARM_LEAF_DUMMY for the lanes
-// without leaves), ASP_N special slots.
-constexpr int ARM_BLK = 23, ARM_BLOCKS = 15, ARM_LEAF_BASES = 4, ARM_LEAF_DUMMY = 3, ASP_N = 37;
-constexpr int ARM_SPECIAL_N = 16;  // anchor, fossa and junction edges
-// One lane's part as LDS byte offsets of the utterance block.  The positions' pivots, rhs and
-// edges and the fold leaves come from the lane's block and leaf base (fixed offsets from
-// two addresses); the solutions go to the currents' X_U slots (the solution sink for
-// dummy positions and unused fold slots).
+// LDS byte offsets (utterance block) of one lane's part; dummy positions and unused fold
+// slots point at the ONE pivot slot (1.0, rhs 0.0), the zero edge and the solution sink, so
+// that every lane runs the same code and a dummy step changes nothing.
 struct alignas(16) ArmRec {
-  uint16_t blk, lf;           // the lane's block and leaf base
+  uint16_t d[ARM_P];          // pivot (X_DIAG) of position p; its rhs at RHS_DELTA
   uint16_t u[ARM_P];          // X_U slot of position p: its fill edge to the anchor, then x
-  uint16_t lu[ARM_FOLDS];     // X_U slots of the fold leaves
+  uint16_t e[ARM_P - 1];      // edge p - p+1 (X_OFF)
   uint16_t ea;                // edge anchor (previous lane's boundary) - first real node
+  uint16_t ld[ARM_FOLDS], le0[ARM_FOLDS], le1[ARM_FOLDS], lu[ARM_FOLDS];  // fold leaves
   uint16_t fx0, fx1;          // fossa lane: edges 84-28, 84-29 (else the zero edge)
   uint16_t ej;                // last lane of an arm: edge boundary - junction node
   uint8_t start;              // first real position (ARM_P: none)
   uint8_t idx, flags, pad0;   // position in the arm (0 = far end), ARM_IN / ARM_END
+  uint16_t pad[3];
 };
-static_assert(sizeof(ArmRec) == 48, "ArmRec: 48 bytes");
+static_assert(sizeof(ArmRec) == 96, "ArmRec: 96 bytes");
+// the junction triangle: pivots of 40, 41, 65, edges 40-41, 40-65, 41-65, X_U of 40, 41, 65
+struct alignas(8) ArmJunction {
+  uint16_t d[3], e[3], u[3], pad;
+};
 // Currents whose d/dt another lane reads (branch partners and radiation; tree_core.h X_UR).
 constexpr int NUR = 16;
 // Currents whose noise-filtered value another lane reads (outputs of the constriction
@@ -131,7 +130,7 @@ struct alignas(8) Topo {
 //   row:    x_la/x_ra/x_ea = L, R1, E of the source section when it is dynamic (X_L, X_R1,
 //           X_E), c_la/c_ra/c_ea the same constants when it is static (else 0.0); x_da = its
 //           D; x_ub/x_urb = flow and d/dt of the bifurcation partner; x_sx = the source term
-//           (dipole sample, lung pressure); x_e0..x_e2 = the section's edges (solver slots).
+//           (dipole sample, lung pressure); x_e0..x_e2 = the section's edges (X_OFF).
 //   update: x_o0/x_o1 = flows of the output currents; x_ur/x_un/x_p4 = where d/dt and the
 //           noise-smoothed value of the in-current and the pressure are published.
 enum : uint16_t { SR_BIF = 1, SR_JUNCTION = 2, SR_RADIATION = 4 };
@@ -147,8 +146,6 @@ struct alignas(16) SecRec {
   // radiation sections (SR_RADIATION): flow, d/dt and noise-smoothed flow of the two
   // radiation currents (X_U + rc, X_U + lc, X_UR.., X_UR.., X_UN.., X_UN..)
   uint16_t x_rad[6];
-  // the pivot of the section's in-current (its rhs RHS_DELTA further on)
-  uint16_t x_piv, pad_piv;
   // (80-byte stride: the 16 sections a 16-lane ds_read_b128 group reads start on 16 distinct
   // 16-byte bank slots; at 64 bytes, sections s and s+4 share banks: 4-way conflicts)
 };
@@ -174,7 +171,7 @@ struct Uni {
 struct Consts {
   Hot h;
   ArmRec arm[TREE_CHAINS];
-  uint16_t piv[NC + 1];  // LDS byte offset of each current's pivot (index NC: the sink)
+  ArmJunction armj;
   int8_t ur_slot[NC];  // X_UR slot of a current, -1: none
   int8_t un_slot[NC];  // X_UN slot of a current, -1: none
   Topo topo[NS];
@@ -215,8 +212,6 @@ struct Tables {
   // (ARM_MAXLEN - 1), -1 when the tables fail their checks
   int16_t edge[NS][3];
   int32_t n_edges, n_rounds;
-  int16_t edge_slot[TREE_NE];  // LDS slot (double index in the utterance block) of each edge
-  int16_t piv_slot[NC + 1];    // ... of each current's pivot (index NC: the sink)
   Consts consts;
   Uni uni;
 

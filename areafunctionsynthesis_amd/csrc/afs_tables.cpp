@@ -188,7 +188,6 @@ bool arm_records(Tables *t) {
       {-1, -1, -1, -1}, {95, -1, -1, -1}, {92, 91, 90, 89}, {-1, -1, -1, -1}, {-1, -1, -1, -1},
       {-1, -1, -1, -1}};
   static const int JN[3] = {40, 41, 65}, JEND[3] = {39, 42, 66};
-  static const int LEAF_BASE[TREE_CHAINS] = {3, 3, 3, 3, 3, 3, 3, 0, 3, 3, 3, 1, 2, 3, 3, 3};
   static int16_t eid[NC][NC];
   for (int i = 0; i < NC; ++i)
     for (int j = 0; j < NC; ++j) eid[i][j] = -1;
@@ -201,27 +200,14 @@ bool arm_records(Tables *t) {
   }
   using namespace tree;
   auto off = [](int slot) { return (uint16_t)(slot * 8); };
-  const uint16_t ZE = off(ASP_EZERO), USINK = off(X_U + U_SINK);
+  const uint16_t ONE = off(X_DIAG + NC + 1), ZE = off(X_OFF + EDGE_ZERO), USINK = off(X_U + U_SINK);
+  std::vector<int> edge_uses(TREE_NE, 0), node_uses(NC, 0);
   bool ok = true;
-  for (int e = 0; e < TREE_NE; ++e) t->edge_slot[e] = -1;
-  for (int i = 0; i <= NC; ++i) t->piv_slot[i] = -1;
-  t->piv_slot[NC] = (int16_t)ASP_PIV_SINK;
-  // every edge gets exactly one slot, in the role the solver reads it in
-  auto put_edge = [&](int a, int b, int slot) -> uint16_t {
-    if (a < 0 || b < 0 || a >= NC || b >= NC || eid[a][b] < 0 || eid[a][b] >= TREE_NE ||
-        t->edge_slot[eid[a][b]] >= 0) {
-      ok = false;
-      return ZE;
-    }
-    t->edge_slot[eid[a][b]] = (int16_t)slot;
-    return off(slot);
+  auto use_edge = [&](int a, int b) -> uint16_t {
+    if (a < 0 || b < 0 || a >= NC || b >= NC || eid[a][b] < 0 || eid[a][b] >= TREE_NE) { ok = false; return ZE; }
+    edge_uses[eid[a][b]]++;
+    return off(X_OFF + eid[a][b]);
   };
-  auto put_piv = [&](int n, int slot) {
-    if (n < 0 || n >= NC || t->piv_slot[n] >= 0) { ok = false; return; }
-    t->piv_slot[n] = (int16_t)slot;
-  };
-  int special = 0;
-  auto special_slot = [&]() { return ASP_SPECIAL + (special < ARM_SPECIAL_N ? special++ : (ok = false, 0)); };
   int bound[TREE_CHAINS];
   Consts &c = t->consts;
   for (int k = 0; k < TREE_CHAINS; ++k) {
@@ -234,51 +220,51 @@ bool arm_records(Tables *t) {
     for (int p = 0; p < ARM_P; ++p) pos[p] = p >= start ? SEG[k][p - start] : -1;
     bound[k] = n ? pos[ARM_P - 1] : -1;
     r.start = (uint8_t)start;
-    // the junction lane reads the block of lane ARM_L28 + 1 (dummies but its boundary 29)
-    const int b = k == ARM_JUNCTION ? ARM_L28 + 1 : k;
-    if (b >= ARM_BLOCKS) ok = false;
-    const int blk = X_ABK + b * ARM_BLK, lf = X_ALF + LEAF_BASE[k] * 16;
-    r.blk = off(blk);
-    r.lf = off(lf);
     for (int p = 0; p < ARM_P; ++p) {
-      if (pos[p] >= 0) put_piv(pos[p], blk + p);
+      if (pos[p] >= 0) node_uses[pos[p]]++;
+      r.d[p] = pos[p] >= 0 ? off(X_DIAG + pos[p]) : ONE;
       r.u[p] = pos[p] >= 0 ? off(X_U + pos[p]) : USINK;
     }
-    for (int p = 0; p + 1 < ARM_P; ++p)
-      if (pos[p] >= 0) put_edge(pos[p], pos[p + 1], blk + 16 + p);
+    for (int p = 0; p + 1 < ARM_P; ++p) r.e[p] = (pos[p] >= 0) ? use_edge(pos[p], pos[p + 1]) : ZE;
     // anchor: the previous lane of the same arm
     const bool anchored = ARM_OF[k] >= 0 && k > 0 && ARM_OF[k - 1] == ARM_OF[k];
-    r.ea = (anchored && n) ? put_edge(bound[k - 1], pos[start], special_slot()) : ZE;
+    r.ea = (anchored && n) ? use_edge(bound[k - 1], pos[start]) : ZE;
     int idx = 0;
     for (int j = k - 1; j >= 0 && ARM_OF[j] == ARM_OF[k] && ARM_OF[k] >= 0; --j) ++idx;
     r.idx = (uint8_t)(ARM_OF[k] >= 0 ? idx : 0xff);
     const bool last = ARM_OF[k] >= 0 && (k + 1 == TREE_CHAINS || ARM_OF[k + 1] != ARM_OF[k]);
     r.flags = (uint8_t)((ARM_OF[k] >= 0 ? ARM_IN : 0) | (last ? ARM_END : 0));
-    r.ej = last ? put_edge(JEND[ARM_OF[k]], JN[ARM_OF[k]], special_slot()) : ZE;
+    r.ej = ZE;
+    if (last) r.ej = use_edge(JEND[ARM_OF[k]], JN[ARM_OF[k]]);
     if (last && bound[k] != JEND[ARM_OF[k]]) ok = false;
     for (int f = 0; f < ARM_FOLDS; ++f) {
       const int leaf = LEAF[k][f], p = arm_fold_pos(f);
-      if (leaf >= 0 && LEAF_BASE[k] == ARM_LEAF_DUMMY) ok = false;
+      r.ld[f] = leaf >= 0 ? off(X_DIAG + leaf) : ONE;
       r.lu[f] = leaf >= 0 ? off(X_U + leaf) : USINK;
-      if (leaf < 0) continue;
-      put_piv(leaf, lf + f);
-      put_edge(leaf, pos[p], lf + 4 + f);
-      put_edge(leaf, pos[p + 1], lf + 12 + f);
+      r.le0[f] = leaf >= 0 ? use_edge(leaf, pos[p]) : ZE;
+      r.le1[f] = leaf >= 0 ? use_edge(leaf, pos[p + 1]) : ZE;
+      if (leaf >= 0) node_uses[leaf]++;
     }
     r.fx0 = r.fx1 = ZE;
   }
+  // roles fixed in the kernel
   if (bound[ARM_L28] != 28 || bound[ARM_L28 + 1] != 29 || bound[ARM_FOSSA] != 84 || bound[ARM_JUNCTION] != -1 ||
       bound[ARM_END_A] != 39 || bound[ARM_END_B] != 42 || bound[ARM_END_C] != 66)
     ok = false;
-  c.arm[ARM_FOSSA].fx0 = put_edge(84, 28, special_slot());
-  c.arm[ARM_FOSSA].fx1 = put_edge(84, 29, special_slot());
-  for (int q = 0; q < 3; ++q) put_piv(JN[q], X_ASP + q);
-  put_edge(40, 41, ASP_TRI + 0);
-  put_edge(40, 65, ASP_TRI + 1);
-  put_edge(41, 65, ASP_TRI + 2);
-  for (int e = 0; e < TREE_NE; ++e) ok = ok && t->edge_slot[e] >= 0;
-  for (int i = 0; i < NC; ++i) ok = ok && t->piv_slot[i] >= 0;
-  for (int i = 0; i <= NC; ++i) c.piv[i] = off(t->piv_slot[i] < 0 ? ASP_PIV_SINK : t->piv_slot[i]);
+  c.arm[ARM_FOSSA].fx0 = use_edge(84, 28);
+  c.arm[ARM_FOSSA].fx1 = use_edge(84, 29);
+  ArmJunction &j = c.armj;
+  std::memset(&j, 0, sizeof j);
+  for (int q = 0; q < 3; ++q) {
+    j.d[q] = off(X_DIAG + JN[q]);
+    j.u[q] = off(X_U + JN[q]);
+    node_uses[JN[q]]++;
+  }
+  j.e[0] = use_edge(40, 41);
+  j.e[1] = use_edge(40, 65);
+  j.e[2] = use_edge(41, 65);
+  for (int e = 0; e < TREE_NE; ++e) ok = ok && edge_uses[e] == 1;
+  for (int i = 0; i < NC; ++i) ok = ok && node_uses[i] == 1;
   return ok;
 }
 
@@ -451,12 +437,10 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
     q.x_sx = (s >= S_PHARYNX0 && s <= S_LAST_MOUTH) ? (int16_t)(X_SMP + s - S_PHARYNX0)
              : (real && s == 0)                    ? (int16_t)(X_GP + 1)
                                                    : zero;
-    const int16_t esink = (int16_t)tree::ASP_ESINK;
-    auto eslot = [&](int e) { return (e >= 0 && t->edge_slot[e] >= 0) ? t->edge_slot[e] : esink; };
-    q.x_e0 = real && t->edge[s][0] >= 0 ? eslot(t->edge[s][0]) : esink;
-    q.x_e1 = real && t->edge[s][1] >= 0 ? eslot(t->edge[s][1]) : esink;
-    q.x_e2 = real && t->edge[s][1] >= 0 && t->edge[s][2] >= 0 ? eslot(t->edge[s][2]) : esink;
-    q.x_piv = (uint16_t)(t->piv_slot[real ? s : NC] >= 0 ? t->piv_slot[real ? s : NC] : tree::ASP_PIV_SINK);
+    const int16_t esink = (int16_t)(X_OFF + EDGE_SINK);
+    q.x_e0 = real && t->edge[s][0] >= 0 ? (int16_t)(X_OFF + t->edge[s][0]) : esink;
+    q.x_e1 = real && t->edge[s][1] >= 0 ? (int16_t)(X_OFF + t->edge[s][1]) : esink;
+    q.x_e2 = real && t->edge[s][1] >= 0 && t->edge[s][2] >= 0 ? (int16_t)(X_OFF + t->edge[s][2]) : esink;
     const int o0 = real ? t->cout0[s] : -1, o1 = real ? t->cout1[s] : -1;
     q.x_o0 = (int16_t)(X_U + (o0 >= 0 ? o0 : U_ZERO));
     q.x_o1 = (int16_t)(X_U + (o1 >= 0 ? o1 : U_ZERO));
@@ -479,7 +463,7 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
                          (s == S_LAST_MOUTH || s == S_LAST_NOSE ? SR_RADIATION : 0));
     // block slots -> LDS byte offsets
     for (uint16_t *f : {&q.x_la, &q.x_ra, &q.x_ea, &q.x_da, &q.x_ub, &q.x_urb, &q.x_sx, &q.x_e0, &q.x_e1,
-                        &q.x_e2, &q.x_o0, &q.x_o1, &q.x_ur, &q.x_un, &q.x_p4, &q.x_uo0, &q.x_uo1, &q.x_piv})
+                        &q.x_e2, &q.x_o0, &q.x_o1, &q.x_ur, &q.x_un, &q.x_p4, &q.x_uo0, &q.x_uo1})
       *f = (uint16_t)(*f * 8);
     for (int k = 0; k < 6; ++k) q.x_rad[k] = (uint16_t)(q.x_rad[k] * 8);
   }

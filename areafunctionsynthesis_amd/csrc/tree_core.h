@@ -74,18 +74,11 @@ enum : int {
   X_UNION = X_SMP + NDIP,
   //   sink slots of the phases before the rows (n): stores of lanes / slots with nothing to store
   X_ACT = X_UNION, X_NOISE_END = X_ACT + 16,
-  //   solver (afs_model.h ArmRec): every pivot has its rhs 8 doubles further on
-  //   X_ASP: special slots written by the row phase each sample (the first 16 alias the noise
-  //     scratch): pivots of 40, 41, 65 at +0..2, the sink pivot at +4 (rhs +8..); the
-  //     triangle's edges at +16..18, the zero and the sink edge at +19 / +20; the anchor,
-  //     fossa and junction edges from +21
-  //   X_ALF: fold leaves, 16 doubles per base (pivots +f, edges to p at +4+f, rhs +8+f,
-  //     edges to p+1 at +12+f); base ARM_LEAF_DUMMY: pivots 1, zeros (kept from the reset)
-  //   X_ABK: one block per lane: pivots D[p] +p, rhs +8+p, edges p - p+1 at +16+p; its
-  //     dummy positions hold pivot 1 and zeros from the reset on (the row phase writes only
-  //     the real ones; the solver writes back what it read)
-  X_ASP = X_UNION, X_ALF = X_ASP + ASP_N, X_ABK = X_ALF + ARM_LEAF_BASES * 16,
-  X_SOLVE_END = X_ABK + ARM_BLOCKS * ARM_BLK,
+  //   solver
+  //   (pivot / rhs with a sink slot at NC and the dummy pivot at NC+1; edges with EDGE_ZERO
+  //   and EDGE_SINK after TREE_NE)
+  X_DIAG = X_UNION, X_RHS = X_DIAG + NC + 2, X_OFF = X_RHS + NC + 2,
+  X_SOLVE_END = X_OFF + TREE_NE + 2,
   X_AFTER = (X_NOISE_END > X_SOLVE_END ? X_NOISE_END : X_SOLVE_END),
   // frame-rate values written by lane 0 at every frame transition
   X_FRAME = X_AFTER,           // teethL, teethR, velL, velR, gL[6], gR[6]
@@ -117,11 +110,9 @@ enum : int {
   PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_TARGETS, PH_COUNT
 };
 
-// Solution sink / zero slots (X_U); special solver slots (X_ASP); bytes from a pivot to its rhs.
-constexpr int U_SINK = NC, U_ZERO = NC + 1;
-constexpr int ASP_PIV_SINK = X_ASP + 4, ASP_TRI = X_ASP + 16, ASP_EZERO = X_ASP + 19, ASP_ESINK = X_ASP + 20;
-constexpr int ASP_SPECIAL = X_ASP + 21;
-constexpr uint32_t RHS_DELTA = 64u;
+// Solver sink / zero slots (see ArmRec).
+constexpr int NODE_SINK = NC, U_SINK = NC, U_ZERO = NC + 1, EDGE_ZERO = TREE_NE, EDGE_SINK = TREE_NE + 1;
+constexpr uint32_t RHS_DELTA = (uint32_t)(X_RHS - X_DIAG) * 8u;  // bytes from a pivot to its rhs
 
 template <int W>
 struct Shape {
@@ -488,12 +479,6 @@ AFS_HD inline void reset_lane(int gl, Lane<W> &R) {
 AFS_HD inline void reset_lds(double *X, uint32_t seed) {
   for (int k = 0; k < X_TOTAL; ++k) X[k] = 0.0;
   rng_ring_seed((uint32_t *)(X + X_RNG), seed);
-  // the solver's dummy pivots (lane blocks, leaf bases): 1.0; the row phase overwrites the
-  // real ones every sample
-  for (int b = 0; b < ARM_BLOCKS; ++b)
-    for (int p = 0; p < ARM_P; ++p) X[X_ABK + b * ARM_BLK + p] = 1.0;
-  for (int b = 0; b < ARM_LEAF_BASES; ++b)
-    for (int f = 0; f < ARM_FOLDS; ++f) X[X_ALF + b * 16 + f] = 1.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1080,7 +1065,7 @@ template <int W>
 AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, double *__restrict__ Xw,
                               const Uni &U, const Consts &C) {
   // X (reads) and Xw (writes) are the same utterance block; the phase writes only the
-  // solver arrays (X_ASP, X_ALF, X_ABK), which it never reads.  The slot loop is one
+  // solver arrays (X_DIAG, X_RHS, X_OFF), which it never reads.  The slot loop is one
   // branch-free block: both row forms are evaluated and selected per lane, an absent slot
   // writes into the sink slots; the radiation rows follow.
   using S = Shape<W>;
@@ -1088,12 +1073,15 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
   const afs_options &opt = U.opt;
   SecRec rec[S::NSL];
   load_sec_recs<W>(gl, C, rec);
-  Xw[ASP_EZERO] = 0.0;  // the solver's zero edge (every lane stores it)
+  Xw[X_OFF + EDGE_ZERO] = 0.0;  // the solver's zero edge (union slot; every lane stores it)
+  Xw[X_DIAG + NC + 1] = 1.0;    // the arm solver's dummy pivot and rhs
+  Xw[X_RHS + NC + 1] = 0.0;
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const bool dyn = j < S::ND;
     const int s0 = slot_section<W>(j, gl);
     const int s = s0 < 0 ? (dyn ? DYN0 : 0) : s0;
+    const int i = s0 < 0 ? NODE_SINK : s;  // current i flows into section s
     const SecRec &q = rec[j];
     const double *ks = C.stat[dyn ? 0 : static_index(s)];  // (a dynamic slot has no row: row 0 stands in)
     const double LB = dyn ? X[X_L + s - DYN0] : ks[ST_L];
@@ -1128,8 +1116,8 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     double rhs = H + DB;
     rhs -= DA;  // 0.0 without a source
     const bool bif = (q.flags & SR_BIF) != 0;
-    xat(Xw, q.x_piv) = -(bif ? mb : m);  // (current s flows into section s; absent: the sink)
-    xat(Xw, q.x_piv + RHS_DELTA) = -(bif ? rb : rhs);
+    Xw[X_DIAG + i] = -(bif ? mb : m);
+    Xw[X_RHS + i] = -(bif ? rb : rhs);
     // edges of section s: (in, out0) = -E, (in, out1) = -E, (out0, out1) = E + L/(dt th) + R1
     xat(Xw, q.x_e0) = -EB;
     xat(Xw, q.x_e1) = -EB;
@@ -1157,16 +1145,16 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
       const double Rrad = dyn ? X[X_RRAD] : C.h.rrad_nose;  // (network phase / tables)
       double F = LA2 * idt + RA2 + Rrad;
       double H = -(LA2 * idt) * (uR + uL) - (LA2 * (TH1 / TH)) * (uRr + uLr) + Sr;
-      xat(Xw, C.piv[rc]) = -(-EB - F);
-      xat(Xw, C.piv[rc] + RHS_DELTA) = -(H - DB);
+      Xw[X_DIAG + rc] = -(-EB - F);
+      Xw[X_RHS + rc] = -(H - DB);
     }
     {
       const double Lrad = dyn ? X[X_RRAD + 1] : C.h.lrad_nose;
       double LAB2 = LA2 + Lrad;
       double G = LAB2 * idt + RA2;
       double H = -idt * (LA2 * uR + LAB2 * uL) - (TH1 / TH) * (LA2 * uRr + LAB2 * uLr) + Sr;
-      xat(Xw, C.piv[lc]) = -(-EB - G);
-      xat(Xw, C.piv[lc] + RHS_DELTA) = -(H - DB);
+      Xw[X_DIAG + lc] = -(-EB - G);
+      Xw[X_RHS + lc] = -(H - DB);
     }
   }
 }
@@ -1191,22 +1179,21 @@ AFS_HD inline double arm_min(double a, double b) { return b < a ? b : a; }
 // LDS slots the compiler cannot tell apart from the loaded ones).
 AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
   const ArmRec r = rr;
-  double *B = &xat(X, r.blk), *L = &xat(X, r.lf);  // the lane's block and leaf base
   double D[ARM_P], Y[ARM_P], E[ARM_P - 1];
   double dl[ARM_FOLDS], yl[ARM_FOLDS], l0[ARM_FOLDS], l1[ARM_FOLDS];
 #pragma unroll
   for (int p = 0; p < ARM_P; ++p) {
-    D[p] = B[p];
-    Y[p] = B[8 + p];
+    D[p] = xat(X, r.d[p]);
+    Y[p] = xat(X, r.d[p] + RHS_DELTA);
   }
 #pragma unroll
-  for (int p = 0; p < ARM_P - 1; ++p) E[p] = B[16 + p];
+  for (int p = 0; p < ARM_P - 1; ++p) E[p] = xat(X, r.e[p]);
 #pragma unroll
   for (int f = 0; f < ARM_FOLDS; ++f) {
-    dl[f] = L[f];
-    l0[f] = L[4 + f];
-    yl[f] = L[8 + f];
-    l1[f] = L[12 + f];
+    dl[f] = xat(X, r.ld[f]);
+    yl[f] = xat(X, r.ld[f] + RHS_DELTA);
+    l0[f] = xat(X, r.le0[f]);
+    l1[f] = xat(X, r.le1[f]);
   }
   const double ea = xat(X, r.ea);
   a.e28 = xat(X, r.fx0);
@@ -1244,14 +1231,14 @@ AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
     yA = fma(-g, Y[p], yA);
     D[p + 1] = fma(-e2, inv, D[p + 1]);
     Y[p + 1] = fma(-h, Y[p], Y[p + 1]);
-    B[p] = inv;                          // factors for the back substitution
-    B[8 + p] = Y[p];
-    B[16 + p] = E[p];
+    xat(X, r.d[p]) = inv;                // factors for the back substitution
+    xat(X, r.d[p] + RHS_DELTA) = Y[p];
     xat(X, r.u[p]) = F;
+    xat(X, r.e[p]) = E[p];
     F = -(g * E[p]);                     // fill edge anchor - p+1
   }
 #pragma unroll
-  for (int f = 0; f < ARM_FOLDS; ++f) L[f] = il[f];
+  for (int f = 0; f < ARM_FOLDS; ++f) xat(X, r.ld[f]) = il[f];
   a.F = ((int)r.start == ARM_P - 1) ? ea : F;
   a.Db = D[ARM_P - 1];
   a.Yb = Y[ARM_P - 1];
@@ -1263,24 +1250,24 @@ AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
 // Back substitution of a lane's segment and leaves, from its boundary's solution a.x and the
 // anchor's xA (all loads first, as in the walk); the junction lane stores the triangle's
 // solutions here too (the other lanes into the sink).
-AFS_HD inline void arm_back(const ArmRec &rr, bool junction, double *X, const ArmCarry &a, double xA) {
+AFS_HD inline void arm_back(const ArmRec &rr, const ArmJunction &J, bool junction, double *X, const ArmCarry &a,
+                            double xA) {
   const ArmRec r = rr;
-  const double *B = &xat(X, r.blk), *L = &xat(X, r.lf);
   double inv[ARM_P - 1], y[ARM_P - 1], Fp[ARM_P - 1], Ep[ARM_P - 1];
   double il[ARM_FOLDS], yl[ARM_FOLDS], l0[ARM_FOLDS], l1[ARM_FOLDS];
 #pragma unroll
   for (int p = 0; p < ARM_P - 1; ++p) {
-    inv[p] = B[p];
-    y[p] = B[8 + p];
-    Ep[p] = B[16 + p];
+    inv[p] = xat(X, r.d[p]);
+    y[p] = xat(X, r.d[p] + RHS_DELTA);
     Fp[p] = xat(X, r.u[p]);
+    Ep[p] = xat(X, r.e[p]);
   }
 #pragma unroll
   for (int f = 0; f < ARM_FOLDS; ++f) {
-    il[f] = L[f];
-    l0[f] = L[4 + f];
-    yl[f] = L[8 + f];
-    l1[f] = L[12 + f];
+    il[f] = xat(X, r.ld[f]);
+    yl[f] = xat(X, r.ld[f] + RHS_DELTA);
+    l0[f] = xat(X, r.le0[f]);
+    l1[f] = xat(X, r.le1[f]);
   }
   double xs[ARM_P];
   xs[ARM_P - 1] = a.x;
@@ -1295,10 +1282,10 @@ AFS_HD inline void arm_back(const ArmRec &rr, bool junction, double *X, const Ar
     const int p = arm_fold_pos(f);
     xat(X, r.lu[f]) = fma(-l1[f], xs[p + 1], fma(-l0[f], xs[p], yl[f])) * il[f];
   }
-  // (the junction lane: 40, 41, 65; the others into the sink)
-  X[junction ? X_U + 40 : X_U + U_SINK] = a.xj[0];
-  X[junction ? X_U + 41 : X_U + U_SINK] = a.xj[1];
-  X[junction ? X_U + 65 : X_U + U_SINK] = a.xj[2];
+  const uint32_t sink = (uint32_t)(X_U + U_SINK) * 8u;
+  xat(X, junction ? J.u[0] : sink) = a.xj[0];
+  xat(X, junction ? J.u[1] : sink) = a.xj[1];
+  xat(X, junction ? J.u[2] : sink) = a.xj[2];
 }
 
 template <int W, class Xc>
@@ -1307,11 +1294,12 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
   x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_walk(C.arm[k], X, R.ac); });
   // the junction triangle's values (every lane loads them; only the junction lane's matter)
   x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
+    const ArmJunction &J = C.armj;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      R.ac.jd[q] = X[X_ASP + q];
-      R.ac.jy[q] = X[X_ASP + 8 + q];
-      R.ac.je[q] = X[ASP_TRI + q];
+      R.ac.jd[q] = xat(X, J.d[q]);
+      R.ac.jy[q] = xat(X, J.d[q] + RHS_DELTA);
+      R.ac.je[q] = xat(X, J.e[q]);
     }
     R.ac.xJ = 0.0;
   });
@@ -1428,7 +1416,7 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
   // every lane's segment from its boundary and its anchor (lane k-1's boundary)
   x.template pull<-1, 1>([&](int, Lane<W> &R) { return D4{{R.ac.x, 0.0, 0.0, 0.0}}; },
                          [&](int, Lane<W> &R, const D4 &v) { R.ac.xJ = v.v[0]; });
-  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_back(C.arm[k], k == ARM_JUNCTION, X, R.ac, R.ac.xJ); });
+  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_back(C.arm[k], C.armj, k == ARM_JUNCTION, X, R.ac, R.ac.xJ); });
   x.sync();
   x.mark(PH_BACKWARD);
 }
