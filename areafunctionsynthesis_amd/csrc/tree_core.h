@@ -5,8 +5,8 @@
 // NST static ones (trachea, nose, fossa, sinuses) with their in-currents; the persistent
 // state of those sections/currents (pressure, wall motion, flows) lives in the lane's
 // registers for the whole utterance.  Lanes exchange neighbour data through a per-utterance
-// LDS block.  The per-sample system is solved with a fill-free leaf-first LDL^T whose four
-// independent chains are eliminated by four lanes in lock step (schedule in Tables).
+// LDS block.  The per-sample system is solved with an LDL^T in arm order (solve_arms): every
+// lane eliminates one segment of the tube in registers and DPP row shifts join the segments.
 //
 // The step is a sequence of phases.  A phase either runs on every lane (`par`), on the
 // utterance's lane 0 (`one`) or on the first k lanes (`lanes`), and phases are separated

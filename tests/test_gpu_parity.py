@@ -3,7 +3,7 @@ vectors of the reference build.
 
 Two kernels are checked: "cholesky" keeps the reference's operation order (differences only
 from device libm: exp for noise cutoffs below the 2 kHz clamp, pow for the aspiration
-gain); "tree" solves the same system with a fill-free LDL^T (rounding-level differences,
+gain); "tree" solves the same system with an LDL^T in arm order (rounding-level differences,
 ~1e-12 on the CPU emulator).  Such differences are amplified by the chaotic glottis/tube
 dynamics (trap 3).  Bounds used below:
   * golden / oracle, first 2048 samples:   max |err| <= 1e-9

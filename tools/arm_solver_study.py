@@ -1,8 +1,8 @@
 """Design study (not product code): an arm-wise segment solver for the per-sample 97-unknown
 system, to replace the 12+12-round LDS elimination of the tree kernel.
 
-The current solver (afs_tables.cpp tree_schedule) eliminates at most one unknown per lane and
-round with every operand in LDS; a round costs the LDS round trip plus the pivot reciprocal
+The round-2 solver it replaced (afs_tables.cpp tree_schedule, removed) eliminated at most one
+unknown per lane and round with every operand in LDS; a round costs the LDS round trip plus the pivot reciprocal
 (~370 cycles forward, ~180 backward; 6.6 k of 29.9 k cycles per sample).  Here the graph is
 cut into arms that meet at the junction triangle {40, 41, 65}:
 

@@ -136,7 +136,8 @@ if __name__ == "__main__":
 
 
 def check_programs(lanes, nslot=1, verbose=True):
-    """The C++ builder's check (afs_tables.cpp tree_schedule) for lane programs
+    """The C++ builder's check (afs_tables.cpp tree_schedule, the LDS-rounds solver that the arm
+    solver replaced; this tool is kept for its topology() and as the record of that search) for lane programs
     [[(start_round, [nodes...]), ...], ...]: returns (rounds, fwd_carry_count, bwd_carry_count)
     or raises ValueError."""
     adj = [set(a) for a in topology()]
