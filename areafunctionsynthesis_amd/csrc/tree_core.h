@@ -1161,8 +1161,8 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
 
 // ---------------------------------------------------------------------------
 // Arm solver (afs_model.h ArmRec; partition and checks in afs_tables.cpp arm_records).
-// The same LDL^T of the same matrix as the rounds above, in an order that keeps the
-// eliminations in registers: every lane folds the leaves of its segment and walks the segment
+// The LDL^T of the per-sample matrix (the reference factors the same matrix by an envelope
+// Cholesky, TdsModel.cpp:2231-2314), in an order that keeps the eliminations in registers: every lane folds the leaves of its segment and walks the segment
 // from the far end (each step eliminates one node whose neighbours are the next position and
 // the anchor, the previous lane's boundary, through the fill edge F), the boundaries of an arm
 // are then reduced lane to lane toward the junction by DPP row shifts, the junction lane
@@ -1170,8 +1170,8 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
 // load the rows' values and to keep the walk's factors for the back substitution.
 // ---------------------------------------------------------------------------
 // (A negative pivot -- the reference's Cholesky takes the square root of it -- is not
-// checked on the elimination chain: every lane keeps the smallest pivot it met in dmin and a
-// lane that met a negative one hands NaN into the back substitution.)
+// checked on the elimination chain: every lane keeps the smallest pivot it met in dmin, and
+// after the forward pass a ballot over the utterance's lanes makes every solution NaN.)
 AFS_HD inline double arm_min(double a, double b) { return b < a ? b : a; }
 
 // Phase A of a lane: the fold leaves, then the walk from the far end to the boundary.  Every
