@@ -19,10 +19,15 @@ HEADERS = ["afs_model.h", "afs_ctx.h", "afs_gather.h", "afs_af.h", "afs_lane.h",
            os.path.join("..", "..", "include", "afs.h")]
 # Per-source extra flags.  (Contracting a*b+c in the tree kernel was measured: ~1 % faster,
 # and it moves some chaotic utterances past the 1e-9 parity bound -- not used.)
-PER_SOURCE: dict = {}
+# The tree kernel is built without machine-level loop-invariant code motion: hoisting the
+# lanes' loop-invariant comparisons out of the time loop kept ~50 lane masks alive in SGPR
+# pairs, more than the wave has, and their spills cost ~100 v_readlane/v_writelane and ~130
+# AGPR moves per sample (A/B: 89.0 vs 89.25 ms per launch).
+TREE_FLAGS = ["-mllvm", "-disable-machine-licm"]
+PER_SOURCE: dict = {"tds_tree.hip": list(TREE_FLAGS)}
 # (AFS_TREE_FLAGS: extra compiler flags for the tree kernel, for A/B builds of scheduler options)
 if os.environ.get("AFS_TREE_FLAGS"):
-    PER_SOURCE["tds_tree.hip"] = os.environ["AFS_TREE_FLAGS"].split()
+    PER_SOURCE["tds_tree.hip"] = TREE_FLAGS + os.environ["AFS_TREE_FLAGS"].split()
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
           # keep the reference's rounding: no contraction of a*b+c into fma
