@@ -1435,27 +1435,36 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
   const double c = C.h.noise_lp_c, idt = C.h.inv_dtTH;
   SecRec rec[S::NSL];
   load_sec_recs<W>(gl, C, rec);
+  // every slot's loads first (the solution, the output flows, D and E), then the arithmetic
+  double unew[S::NSL], cout[S::NSL], Ds[S::NSL], Es[S::NSL];
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const int s0 = slot_section<W>(j, gl);
     const int s = s0 < 0 ? (j < S::ND ? DYN0 : 0) : s0;
-    const SecRec &q = rec[j];
+    unew[j] = X[X_U + s];
+    cout[j] = 0.0;
+    cout[j] += xat(X, rec[j].x_o0);  // 0.0 for an absent output
+    cout[j] += xat(X, rec[j].x_o1);
+    Ds[j] = X[X_D + s];
+    Es[j] = j < S::ND ? X[X_E + s - DYN0] : C.stat[static_index(s)][ST_E];
+  }
+#pragma unroll
+  for (int j = 0; j < S::NSL; ++j) {
+    const int s0 = slot_section<W>(j, gl);
+    const int s = s0 < 0 ? (j < S::ND ? DYN0 : 0) : s0;
     double alpha, beta;
     if (j < S::ND) { alpha = R.al[j]; beta = R.be[j]; }
     else { alpha = C.stat[static_index(s)][ST_ALPHA]; beta = static_beta<W>(R, j, U, C, s); }  // same values as phase_network
-    const double unew = X[X_U + s];
+    const double un = unew[j];
     const double uold = R.u[j];
-    R.u[j] = unew;
-    R.ur[j] = (unew - uold) * idt - (TH1 / TH) * R.ur[j];
-    R.un[j] = (1.0 - c) * unew + c * R.un[j];
+    R.u[j] = un;
+    R.ur[j] = (un - uold) * idt - (TH1 / TH) * R.ur[j];
+    R.un[j] = (1.0 - c) * un + c * R.un[j];
     double cin = 0.0;
-    cin += unew;
-    double cout = 0.0;
-    cout += xat(X, q.x_o0);  // 0.0 for an absent output
-    cout += xat(X, q.x_o1);
-    double net = cin - cout;
+    cin += un;
+    double net = cin - cout[j];
     double old = R.p[j];
-    double p = X[X_D + s] + (j < S::ND ? X[X_E + s - DYN0] : C.stat[static_index(s)][ST_E]) * net;
+    double p = Ds[j] + Es[j] * net;
     R.p[j] = p;
     double prr = (p - old) * idt - R.pr[j] * (TH1 / TH);
     R.pr[j] = prr;
