@@ -1076,6 +1076,21 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
   Xw[X_OFF + EDGE_ZERO] = 0.0;  // the solver's zero edge (union slot; every lane stores it)
   Xw[X_DIAG + NC + 1] = 1.0;    // the arm solver's dummy pivot and rhs
   Xw[X_RHS + NC + 1] = 0.0;
+  // the loads through the records' offsets (source section, partner flows, dipole sample),
+  // every slot's before the arithmetic
+  double xla[S::NSL], xra[S::NSL], xea[S::NSL], xda[S::NSL], xsx[S::NSL], xub[S::NSL], xurb[S::NSL], xrad[S::NSL];
+#pragma unroll
+  for (int j = 0; j < S::NSL; ++j) {
+    const SecRec &q = rec[j];
+    xla[j] = xat(X, q.x_la);
+    xra[j] = xat(X, q.x_ra);
+    xea[j] = xat(X, q.x_ea);
+    xda[j] = xat(X, q.x_da);
+    xsx[j] = xat(X, q.x_sx);
+    xub[j] = xat(X, q.x_ub);
+    xurb[j] = xat(X, q.x_urb);
+    xrad[j] = j < S::ND ? xat(X, q.x_la + (X_RAD - X_L) * 8) : 0.0;
+  }
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const bool dyn = j < S::ND;
@@ -1090,14 +1105,14 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     const double EB = dyn ? X[X_E + s - DYN0] : ks[ST_E], DB = X[X_D + s];
     // source section a: a static source's constants come from the record, a dynamic one's
     // from X (the other term is an exact 0.0; no source: both are)
-    const double LA = q.c_la + xat(X, q.x_la), RA = q.c_ra + xat(X, q.x_ra), EA = q.c_ea + xat(X, q.x_ea);
-    const double DA = xat(X, q.x_da);
+    const double LA = q.c_la + xla[j], RA = q.c_ra + xra[j], EA = q.c_ea + xea[j];
+    const double DA = xda[j];
     const double LAB0 = LA + LB, RAB = RA + RB;
     double Sx = 0.0;
-    Sx -= xat(X, q.x_sx);  // dipole sample (pharynx/mouth) or the lung pressure (section 0)
+    Sx -= xsx[j];  // dipole sample (pharynx/mouth) or the lung pressure (section 0)
     const double uu = R.u[j], uur = R.ur[j];
     // the source section bifurcates: its other output is current br
-    const double uD = xat(X, q.x_ub), uDr = xat(X, q.x_urb);
+    const double uD = xub[j], uDr = xurb[j];
     const double Fb = LAB0 * idt + RAB;
     const double Hb = -idt * (LAB0 * uu + LA * uD) - (TH1 / TH) * (LAB0 * uur + LA * uDr) + Sx;
     const double mb = -EB - EA - Fb;
@@ -1105,7 +1120,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     // simple junction, with Sondhi's inner length correction between pharynx/mouth sections
     double LAB = LAB0;
     if (dyn) {
-      const double jl = junction_l(xat(X, q.x_la + (X_RAD - X_L) * 8), X[X_RAD + s - DYN0]);
+      const double jl = junction_l(xrad[j], X[X_RAD + s - DYN0]);
       const bool use = (opt.inner_length_corrections != 0) & ((q.flags & SR_JUNCTION) != 0);
       LAB = use ? LAB + jl : LAB;  // (a select: no branch around the radii loads)
     }
