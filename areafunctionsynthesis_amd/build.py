@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libafs.so")
 ARCH = os.environ.get("AFS_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["afs_capi.cpp", "afs_comm.cpp", "afs_tables.cpp", "tds_lane.hip", "tds_tree.hip", "af_kernels.hip", "audio_kernels.hip"]
+SOURCES = ["afs_capi.cpp", "afs_comm.cpp", "afs_tables.cpp", "tds_lane.hip", "tds_tree.hip", "tds_plan.hip", "af_kernels.hip", "audio_kernels.hip"]
 HEADERS = ["afs_model.h", "afs_ctx.h", "afs_gather.h", "afs_af.h", "afs_lane.h", "afs_tree.h", "afs_audio.h", "tree_core.h", "tree_plan.h", "tree_kernel.h",
            os.path.join("..", "..", "include", "afs.h")]
 # Per-source extra flags.  (Contracting a*b+c in the tree kernel was measured: ~1 % faster,

@@ -1,0 +1,74 @@
+// tds_plan.hip -- the noise-source plan kernel (K5): the constriction scans of every sample
+// ahead of the time loop (tree_plan.h), one thread per (frame row, sample).  A file of its own
+// so that it is compiled with its own flags (build.py).
+#include "afs_tree.h"
+#include "tree_plan.h"
+
+namespace afs {
+
+using namespace tree;
+
+namespace {
+
+// Grid (rows, sample blocks of PLAN_BLOCK): one thread per (frame row, sample), a block of
+// consecutive samples of one row.  When the block's samples span at most PLAN_STAGE frames
+// (hops >= 128), the frames are staged in LDS first: the plan's scans read every section's
+// area / length / articulator several times, and from LDS those reads cost a fraction of the
+// cache-hit latency of global loads.  Shorter hops (target sequences, hop 1) read the frames
+// from global memory.  The block's records are contiguous in memory: they are assembled in LDS
+// and written with one 16-byte store per lane and step over the whole range (a thread's own
+// 128-B record written directly would spread each store instruction over 64 lines).
+constexpr int PLAN_BLOCK = 256, PLAN_STAGE = 4, PLAN_PITCH = PLAN_WORDS + 1;  // (odd pitch: fewer bank conflicts)
+constexpr int FRAME_WORDS = (int)(sizeof(afs_frame) / 8);
+static_assert(sizeof(afs_frame) % 8 == 0, "frames are copied as 8-byte words");
+
+__global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
+  __shared__ uint64_t fr_lds[PLAN_STAGE][FRAME_WORDS];
+  __shared__ uint64_t rec_lds[PLAN_BLOCK * PLAN_PITCH];
+  const int64_t n = a.s_end - a.s_begin;
+  const int64_t row = blockIdx.x;
+  const int64_t t_first = (int64_t)blockIdx.y * PLAN_BLOCK;
+  const int64_t t_last = (t_first + PLAN_BLOCK < n ? t_first + PLAN_BLOCK : n) - 1;
+  const int64_t t = t_first + threadIdx.x;
+  const afs_frame *f = a.frames + row * a.frame_stride;
+  // sample s plays frames s / hop and s / hop + 1
+  const int64_t k_lo = (a.s_begin + t_first) / a.hop, k_hi = (a.s_begin + t_last) / a.hop + 1;
+  const bool staged = k_hi - k_lo + 1 <= PLAN_STAGE;  // uniform over the block
+  if (staged) {
+    const uint64_t *src = (const uint64_t *)(f + k_lo);
+    const int words = (int)(k_hi - k_lo + 1) * FRAME_WORDS;
+    for (int w = threadIdx.x; w < words; w += PLAN_BLOCK) (&fr_lds[0][0])[w] = src[w];
+    __syncthreads();
+  }
+  if (t < n) {
+    const int64_t s = a.s_begin + t;
+    const int64_t k = s / a.hop + 1;
+    const int i = (int)(s - (k - 1) * a.hop);
+    const afs_frame *fl = staged ? (const afs_frame *)fr_lds[k - 1 - k_lo] : f + (k - 1);
+    const afs_frame *fr = staged ? (const afs_frame *)fr_lds[k - k_lo] : f + k;
+    uint64_t w[PLAN_WORDS];
+    plan_sample(fl, fr, (double)i / (double)a.hop, a.tab->consts.sec, a.two_mass != 0, w);
+#pragma unroll
+    for (int q = 0; q < PLAN_WORDS; ++q) rec_lds[threadIdx.x * PLAN_PITCH + q] = w[q];
+  }
+  __syncthreads();
+  // the block's (t_last - t_first + 1) records, 16 bytes per lane and step
+  const int chunks = (int)(t_last - t_first + 1) * (PLAN_WORDS / 2);
+  ulonglong2 *o = (ulonglong2 *)(a.plan + (row * a.plan_stride + t_first) * PLAN_WORDS);
+  for (int c = threadIdx.x; c < chunks; c += PLAN_BLOCK) {
+    const int r = c / (PLAN_WORDS / 2), q = 2 * (c % (PLAN_WORDS / 2));
+    o[c] = make_ulonglong2(rec_lds[r * PLAN_PITCH + q], rec_lds[r * PLAN_PITCH + q + 1]);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
+  const int64_t n = a.s_end - a.s_begin;
+  if (n <= 0 || a.rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(plan_kernel, dim3((unsigned)a.rows, (unsigned)((n + PLAN_BLOCK - 1) / PLAN_BLOCK)),
+                     dim3(PLAN_BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace afs
