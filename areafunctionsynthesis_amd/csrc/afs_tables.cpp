@@ -375,7 +375,6 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   h.g_smk1 = std::sqrt(G_MASS1 * G_K1);
   // step records: LDS byte offsets of the tree kernel's utterance block (tree_core.h)
   using namespace tree;
-  auto off = [](int slot) { return (uint16_t)(slot * 8); };
   // X_UR slots: both outputs of every bifurcation (their partner reads d/dt of the flow)
   std::memset(c.ur_slot, -1, sizeof c.ur_slot);
   int nur = 0;
