@@ -18,7 +18,10 @@ namespace {
 // from global memory.  The block's records are contiguous in memory: they are assembled in LDS
 // and written with one 16-byte store per lane and step over the whole range (a thread's own
 // 128-B record written directly would spread each store instruction over 64 lines).
-constexpr int PLAN_BLOCK = 256, PLAN_STAGE = 4, PLAN_PITCH = PLAN_WORDS + 1;  // (odd pitch: fewer bank conflicts)
+#ifndef AFS_PLAN_BLOCK
+#define AFS_PLAN_BLOCK 256
+#endif
+constexpr int PLAN_BLOCK = AFS_PLAN_BLOCK, PLAN_STAGE = 4, PLAN_PITCH = PLAN_WORDS + 1;  // (odd pitch: fewer bank conflicts)
 constexpr int FRAME_WORDS = (int)(sizeof(afs_frame) / 8);
 static_assert(sizeof(afs_frame) % 8 == 0, "frames are copied as 8-byte words");
 
@@ -44,10 +47,15 @@ __global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
     const int64_t s = a.s_begin + t;
     const int64_t k = s / a.hop + 1;
     const int i = (int)(s - (k - 1) * a.hop);
-    const afs_frame *fl = staged ? (const afs_frame *)fr_lds[k - 1 - k_lo] : f + (k - 1);
-    const afs_frame *fr = staged ? (const afs_frame *)fr_lds[k - k_lo] : f + k;
+    const double ratio = (double)i / (double)a.hop;
     uint64_t w[PLAN_WORDS];
-    plan_sample(fl, fr, (double)i / (double)a.hop, a.tab->consts.sec, a.two_mass != 0, w);
+    // two instantiations of the scans: LDS frames (ds_read) and global frames (global loads);
+    // one pointer that may point at either would make every frame read a flat load
+    if (staged)
+      plan_sample((const afs_frame *)fr_lds[k - 1 - k_lo], (const afs_frame *)fr_lds[k - k_lo], ratio,
+                  a.tab->consts.sec, a.two_mass != 0, w);
+    else
+      plan_sample(f + (k - 1), f + k, ratio, a.tab->consts.sec, a.two_mass != 0, w);
 #pragma unroll
     for (int q = 0; q < PLAN_WORDS; ++q) rec_lds[threadIdx.x * PLAN_PITCH + q] = w[q];
   }
