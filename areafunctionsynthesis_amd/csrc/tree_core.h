@@ -92,6 +92,7 @@ enum : int {
   X_NDRAW = X_NONFIN + 1,      // rand() calls so far (u64; diagnostics: afs_rng_draws)
   X_RNG = X_NDRAW + 1,         // rand(): value ring, prefix-sum ring (64 u32 each), head, pending (65 doubles)
   X_GP = X_RNG + 65,           // interpolated glottis controls (6), 2 spare
+  X_RNG_SINK = X_GP + 6,       //   (spare: the sink of rng_ahead's idle stores, outside the solver arrays)
   X_TGLOT = X_GP + 8,          // transglottal-pressure filter x1..x4, y1..y4 (variable entrance loss)
   X_TVEL = X_TGLOT + 8,        // transvelar coupling filters H1, H2: x1..x4, y1..y4 each
   X_TVP = X_TVEL + 16,         // p[43], p[67] after the last update (transvelar filter inputs)
@@ -434,7 +435,7 @@ AFS_HD inline void rng_seed(int32_t *r, uint32_t seed) {
 // values (RNG_R, index = sequence number mod 64), the inclusive prefix sums of the outputs
 // S_i = sum_{i' <= i} (r_i' >> 1) (RNG_S, same indexing; sums of draws are differences of
 // two of them), RNG_HEAD = ring index of the next value to generate and RNG_PEND = how many
-// generated values have not been drawn yet (< one block).
+// generated values have not been drawn yet (< two blocks: rng_ahead).
 constexpr int RNG_RING = 64, RNG_R = 0, RNG_S = 64, RNG_HEAD = 128, RNG_PEND = 129;
 // values per generation block: 3 residue chains x min(W, 10) lanes (<= 30 keeps every
 // term of the block in the 31-value history)
@@ -908,12 +909,55 @@ AFS_HD inline void phase_targets(Xc &x, int gl, Lane<W> &R, const double *X, con
   }
 }
 
+// One block of the rand() stream: RNG_BLOCK = 3 RJ values at ring index head, the next 10 of
+// each residue chain c (i = head + 3j + c): r_{head+3j+c} = r_{head+c-3} + sum_{t<=j}
+// r_{head+3t+c-31}, an inclusive prefix sum over the lanes j = 0..9 of history values, then the
+// prefix sums of the outputs in sequence order.  gen == false (per utterance): everything is
+// evaluated and the stores go to the sink.  The caller advances head.
+template <int W, class Xc>
+AFS_HD inline void rng_block(Xc &x, uint32_t *g, uint32_t *sink, int head, bool gen) {
+  constexpr int RJ = rng_lanes<W>();
+  const uint32_t b0 = g[RNG_R + ((head - 3) & (RNG_RING - 1))], b1 = g[RNG_R + ((head - 2) & (RNG_RING - 1))],
+                 b2 = g[RNG_R + ((head - 1) & (RNG_RING - 1))], sb = g[RNG_S + ((head - 1) & (RNG_RING - 1))];
+  x.template scan_add<3>(
+      [&](int gl, Lane<W> &R) {
+        (void)R;
+        // (every lane loads; lanes past RJ only feed their own, discarded, prefix sums)
+        U4 v{{0u, 0u, 0u, 0u}};
+        for (int c = 0; c < 3; ++c) v.v[c] = g[RNG_R + ((head + 3 * gl + c - 31) & (RNG_RING - 1))];
+        return v;
+      },
+      [&](int gl, Lane<W> &R, const U4 &p) {
+        const bool on = gen && gl < RJ;  // the others store into the sink
+        const uint32_t n0 = b0 + p.v[0], n1 = b1 + p.v[1], n2 = b2 + p.v[2];
+        *(on ? &g[RNG_R + ((head + 3 * gl) & (RNG_RING - 1))] : sink) = n0;
+        *(on ? &g[RNG_R + ((head + 3 * gl + 1) & (RNG_RING - 1))] : sink) = n1;
+        *(on ? &g[RNG_R + ((head + 3 * gl + 2) & (RNG_RING - 1))] : sink) = n2;
+        R.rtmp[0] = n0 >> 1; R.rtmp[1] = n1 >> 1; R.rtmp[2] = n2 >> 1;
+      });
+  x.template scan_add<1>(
+      [&](int gl, Lane<W> &R) {
+        (void)gl;
+        U4 v{{0u, 0u, 0u, 0u}};
+        v.v[0] = R.rtmp[0] + R.rtmp[1] + R.rtmp[2];
+        return v;
+      },
+      [&](int gl, Lane<W> &R, const U4 &p) {
+        const bool on = gen && gl < RJ;
+        const uint32_t s2 = sb + p.v[0], s1 = s2 - R.rtmp[2], s0 = s1 - R.rtmp[1];
+        *(on ? &g[RNG_S + ((head + 3 * gl) & (RNG_RING - 1))] : sink) = s0;
+        *(on ? &g[RNG_S + ((head + 3 * gl + 1) & (RNG_RING - 1))] : sink) = s1;
+        *(on ? &g[RNG_S + ((head + 3 * gl + 2) & (RNG_RING - 1))] : sink) = s2;
+      });
+}
+
 // Phase N: noise sources (TdsModel.cpp:1630-1708), after phase_targets smoothed the
 // amplitudes: the rand() draws: source d, the q-th active one in source order, takes
 // draws 12q .. 12q+11 of this sample; the lanes generate the stream 30 values at a time
 // (lane scans instead of one draw after another) and each source's sum of 12 draws is a
 // difference of two output prefix sums.  Then the one-pole shaping filter of the owned
-// active dipoles.
+// active dipoles.  The values come from the ones generated ahead (rng_ahead, at least
+// RNG_BLOCK pending); a sample that needs more generates further blocks here.
 template <int W, class Xc>
 AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) {
   using S = Shape<W>;
@@ -952,58 +996,16 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
     });
   };
   int avail = pend;
-  consume(0, avail);  // (with avail == 0 it adds nothing)
   int head = head0;
-  constexpr int RJ = rng_lanes<W>(), RNG_BLOCK = 3 * RJ;
-  // One block of 3 RJ values = the next 10 of each residue chain c (i = head + 3j + c):
-  // r_{head+3j+c} = r_{head+c-3} + sum_{t<=j} r_{head+3t+c-31}, an inclusive prefix sum over
-  // the lanes j = 0..9 of history values.  gen == false (per utterance): everything is
-  // evaluated, the stores go to a sink and nothing advances.
-  auto block = [&](bool gen) {
-    const uint32_t b0 = g[RNG_R + ((head - 3) & (RNG_RING - 1))], b1 = g[RNG_R + ((head - 2) & (RNG_RING - 1))],
-                   b2 = g[RNG_R + ((head - 1) & (RNG_RING - 1))], sb = g[RNG_S + ((head - 1) & (RNG_RING - 1))];
-    x.template scan_add<3>(
-        [&](int gl, Lane<W> &R) {
-          (void)R;
-          // (every lane loads; lanes past RJ only feed their own, discarded, prefix sums)
-          U4 v{{0u, 0u, 0u, 0u}};
-          for (int c = 0; c < 3; ++c) v.v[c] = g[RNG_R + ((head + 3 * gl + c - 31) & (RNG_RING - 1))];
-          return v;
-        },
-        [&](int gl, Lane<W> &R, const U4 &p) {
-          const bool on = gen && gl < RJ;  // the others store into a sink
-          uint32_t *sink = (uint32_t *)(X + X_ACT + 8);
-          const uint32_t n0 = b0 + p.v[0], n1 = b1 + p.v[1], n2 = b2 + p.v[2];
-          *(on ? &g[RNG_R + ((head + 3 * gl) & (RNG_RING - 1))] : sink) = n0;
-          *(on ? &g[RNG_R + ((head + 3 * gl + 1) & (RNG_RING - 1))] : sink) = n1;
-          *(on ? &g[RNG_R + ((head + 3 * gl + 2) & (RNG_RING - 1))] : sink) = n2;
-          R.rtmp[0] = n0 >> 1; R.rtmp[1] = n1 >> 1; R.rtmp[2] = n2 >> 1;
-        });
-    // prefix sums of the outputs in sequence order
-    x.template scan_add<1>(
-        [&](int gl, Lane<W> &R) {
-          (void)gl;
-          U4 v{{0u, 0u, 0u, 0u}};
-          v.v[0] = R.rtmp[0] + R.rtmp[1] + R.rtmp[2];
-          return v;
-        },
-        [&](int gl, Lane<W> &R, const U4 &p) {
-          const bool on = gen && gl < RJ;
-          uint32_t *sink = (uint32_t *)(X + X_ACT + 8);
-          const uint32_t s2 = sb + p.v[0], s1 = s2 - R.rtmp[2], s0 = s1 - R.rtmp[1];
-          *(on ? &g[RNG_S + ((head + 3 * gl) & (RNG_RING - 1))] : sink) = s0;
-          *(on ? &g[RNG_S + ((head + 3 * gl + 1) & (RNG_RING - 1))] : sink) = s1;
-          *(on ? &g[RNG_S + ((head + 3 * gl + 2) & (RNG_RING - 1))] : sink) = s2;
-        });
+  consume(0, avail);  // (the pending values are consumed before a block here overwrites them)
+  constexpr int RNG_BLOCK = 3 * rng_lanes<W>();
+  while (avail < need) {  // (three or more active sources, or nothing pending yet)
+    rng_block<W>(x, g, (uint32_t *)(X + X_ACT + 8), head, true);
     x.sync();
-    consume(avail, gen ? avail + RNG_BLOCK : avail);
-    avail += gen ? RNG_BLOCK : 0;
-    head = gen ? (head + RNG_BLOCK) & (RNG_RING - 1) : head;
-  };
-  // the first block as straight-line code (most samples of a wave need one in some
-  // utterance), further ones in a loop (three or more active sources)
-  block(avail < need);
-  while (avail < need) block(true);
+    consume(avail, avail + RNG_BLOCK);
+    avail += RNG_BLOCK;
+    head = (head + RNG_BLOCK) & (RNG_RING - 1);
+  }
   x.sync();
   x.mark(PH_N_RNG);
   // (every lane stores the same ring head / pending count; the shaping filter is branch-free
@@ -1033,6 +1035,29 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
       R.dout[k] = on ? y : R.dout[k];
       X[d < NDIP ? X_SMP + d : X_ACT + 2] = on ? y * R.damp[k] : 0.0;
     }
+  });
+}
+
+// The rand() stream generated ahead of its use: one block whenever fewer than RNG_BLOCK values
+// are pending, so that the noise phase of the next sample (one or two active sources: 12 or
+// 24 draws) finds its draws generated.  It depends on the ring alone, not on the acoustic
+// state, so it runs in the update block after the solver, beside the update's own chains
+// instead of on the noise phase's.  The block overwrites ring entries head - 64 .. head - 35: with fewer than 30
+// values pending, none of them (nor the prefix sum before the oldest) is still needed.  Draws
+// are counted when consumed (phase_noise), so the rand() call count is the reference's.
+template <int W, class Xc>
+AFS_HD inline void rng_ahead(Xc &x, double *X) {
+  constexpr int RNG_BLOCK = 3 * rng_lanes<W>();
+  static_assert(2 * RNG_BLOCK <= RNG_RING, "pending values (< RNG_BLOCK), the prefix sum before them and a block fit");
+  uint32_t *g = (uint32_t *)(X + X_RNG);
+  int32_t *c = (int32_t *)g;
+  const int head = c[RNG_HEAD], pend = c[RNG_PEND];
+  const bool gen = pend < RNG_BLOCK;
+  rng_block<W>(x, g, (uint32_t *)(X + X_RNG_SINK), head, gen);
+  x.par([&](int gl, Lane<W> &R) {
+    (void)gl; (void)R;
+    c[RNG_HEAD] = gen ? ((head + RNG_BLOCK) & (RNG_RING - 1)) : head;
+    c[RNG_PEND] = gen ? pend + RNG_BLOCK : pend;
   });
 }
 
@@ -1669,6 +1694,9 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.sync();
   x.mark(PH_ROWS);
   solve_arms<W>(x, X, C);
+  // the rand() stream ahead of the next sample's noise phase (independent of the acoustic
+  // state; here it measured best: before the rows +0.9 %, inside the solver +0.3 %)
+  rng_ahead<W>(x, X);
   // the state update and the output stage (lane-uniform: radiated flow, filters) in one phase
   x.par_uniform([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, X, U, C); },
                 [&](Lane<W> &R) { R.sample = phase_output(X, U, C, section_pressure(X, C, S_PHARYNX0), defer_out); });
