@@ -143,7 +143,7 @@ struct ArmCarry {
   double xJ;          // last lanes: the solution of their junction node (then the anchor's)
   double jd[3], jy[3], je[3], xj[3];  // junction lane: triangle pivots, rhs, edges, solutions
   int sf, sb, end;    // the arm steps this lane reduces in (forward) / solves in (back), -1: none
-  double dmin;        // smallest pivot this lane met (negative: the system is not positive definite)
+  bool neg;           // a pivot this lane met was negative (the system is not positive definite)
 };
 // Up to four doubles handed between lanes (x.pull).
 struct D4 { double v[4]; };
@@ -1210,9 +1210,8 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
 // load the rows' values and to keep the walk's factors for the back substitution.
 // ---------------------------------------------------------------------------
 // (A negative pivot -- the reference's Cholesky takes the square root of it -- is not
-// checked on the elimination chain: every lane keeps the smallest pivot it met in dmin, and
+// checked on the elimination chain: every lane keeps whether a pivot it met was negative, and
 // after the forward pass a ballot over the utterance's lanes makes every solution NaN.)
-AFS_HD inline double arm_min(double a, double b) { return b < a ? b : a; }
 
 // Phase A of a lane: the fold leaves, then the walk from the far end to the boundary.  Every
 // load comes before the first store, so that the loads issue back to back (the stores go to
@@ -1244,12 +1243,13 @@ AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
   a.sb = (in && !end) ? (int)r.idx : -1;
   a.end = end ? 1 : 0;
   // fold slot f: the leaf joined to positions p, p+1 (an unused slot: pivot 1, zero edges)
-  double il[ARM_FOLDS], dmin = 1.0;
+  double il[ARM_FOLDS];
+  bool neg = false;  // (lane masks: one compare per pivot, no select)
 #pragma unroll
   for (int f = 0; f < ARM_FOLDS; ++f) {
     const int p = arm_fold_pos(f);
     il[f] = pivot_recip(dl[f]);
-    dmin = arm_min(dmin, dl[f]);
+    neg = neg | (dl[f] < 0.0);
     const double f0 = l0[f] * il[f], f1 = l1[f] * il[f];
     D[p] = fma(-f0, l0[f], D[p]);
     Y[p] = fma(-f0, yl[f], Y[p]);
@@ -1265,7 +1265,7 @@ AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
     F = (p == (int)r.start) ? ea : F;
     const double e2 = E[p] * E[p];       // (off the pivot chain: D[p+1] waits for inv only)
     const double inv = pivot_recip(D[p]);
-    dmin = arm_min(dmin, D[p]);
+    neg = neg | (D[p] < 0.0);
     const double g = F * inv, h = E[p] * inv;
     dA = fma(-g, F, dA);
     yA = fma(-g, Y[p], yA);
@@ -1284,7 +1284,7 @@ AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
   a.Yb = Y[ARM_P - 1];
   a.dA = dA;
   a.yA = yA;
-  a.dmin = dmin;
+  a.neg = neg;
 }
 
 // Back substitution of a lane's segment and leaves, from its boundary's solution a.x and the
@@ -1362,7 +1362,7 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
         return D4{{c1 * R.ac.e29, c1 * R.ac.Yb, c0 * R.ac.e29, 0.0}};
       },
       [&](int, Lane<W> &R, const D4 &v) { R.ac.Db -= v.v[0]; R.ac.Yb -= v.v[1]; R.ac.F -= v.v[2]; });
-  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.dmin = arm_min(R.ac.dmin, R.ac.Db); });
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.neg = R.ac.neg | (R.ac.Db < 0.0); });
   // arm reduction toward the junction: in step s the lanes at position s of their arm
   // eliminate the previous boundary (lane k-1) from their own
   // (a lane off its step updates with a zero edge: no change, the same reciprocal again)
@@ -1378,7 +1378,7 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
                              R.ac.inv = pivot_recip(R.ac.Db);
                            });
   }
-  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.dmin = arm_min(R.ac.dmin, R.ac.Db); });
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.neg = R.ac.neg | (R.ac.Db < 0.0); });
   // the junction lane takes the three arms' last boundaries (pivot inverse, rhs, edge) and
   // solves the triangle: eliminate 65, then 41; solve 40 (uniform code on every lane)
   auto give = [&](int, Lane<W> &R) { return D4{{R.ac.inv, R.ac.Yb, R.ac.ej, 0.0}}; };
@@ -1407,8 +1407,8 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
     const double h = e01 * i1;
     d[0] = fma(-h, e01, d[0]);
     y[0] = fma(-h, y[1], y[0]);
-    const double dm = arm_min(arm_min(d[0], d[1]), d[2]);
-    const double x0 = (dm < 0.0) ? NAN : y[0] * pivot_recip(d[0]);
+    const bool dneg = (d[0] < 0.0) | (d[1] < 0.0) | (d[2] < 0.0);
+    const double x0 = dneg ? NAN : y[0] * pivot_recip(d[0]);
     const double x1 = fma(-e01, x0, y[1]) * i1;
     R.ac.xj[0] = x0;
     R.ac.xj[1] = x1;
@@ -1446,7 +1446,7 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
                                               });
   // a negative pivot anywhere: every solution of this sample is NaN (as the reference's
   // Cholesky produces from the square root of a negative pivot on)
-  const bool bad = x.ballot([&](int gl, Lane<W> &R) { return gl < TREE_CHAINS && R.ac.dmin < 0.0; }) != 0;
+  const bool bad = x.ballot([&](int gl, Lane<W> &R) { return gl < TREE_CHAINS && R.ac.neg; }) != 0;
   x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
     R.ac.x = bad ? NAN : R.ac.x;
 #pragma unroll
