@@ -17,20 +17,26 @@ ARCH = os.environ.get("AFS_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["afs_capi.cpp", "afs_comm.cpp", "afs_tables.cpp", "tds_lane.hip", "tds_tree.hip", "tds_plan.hip", "af_kernels.hip", "audio_kernels.hip"]
 HEADERS = ["afs_model.h", "afs_ctx.h", "afs_gather.h", "afs_af.h", "afs_lane.h", "afs_tree.h", "afs_audio.h", "tree_core.h", "tree_plan.h", "tree_kernel.h",
            os.path.join("..", "..", "include", "afs.h")]
-# Per-source extra flags.  (Contracting a*b+c in the tree kernel was measured: ~1 % faster,
-# and it moves some chaotic utterances past the 1e-9 parity bound -- not used.)
+# Per-source extra flags.
+# The tree kernel contracts a*b+c into fma (-ffp-contract=fast after COMMON's =off): 8 % fewer
+# VALU instructions in its time loop, +3.5 % end to end (A/B, profiles/r02ac_contract_ab.txt);
+# its results stay within the parity tolerances (the reference's own build with FMA
+# contraction differs from its -O2 build by up to 5.7e-9 over a second).  The
+# plan kernel (K5, the reference's discrete constriction decisions) and the lane kernel (the
+# reference's operation order) keep COMMON's -ffp-contract=off.
 # The tree kernel is built without machine-level loop-invariant code motion: hoisting the
 # lanes' loop-invariant comparisons out of the time loop kept ~50 lane masks alive in SGPR
 # pairs, more than the wave has, and their spills cost ~100 v_readlane/v_writelane and ~130
 # AGPR moves per sample (A/B: 89.0 vs 89.25 ms per launch).
-TREE_FLAGS = ["-mllvm", "-disable-machine-licm"]
+TREE_FLAGS = ["-mllvm", "-disable-machine-licm", "-ffp-contract=fast"]
 PER_SOURCE: dict = {"tds_tree.hip": list(TREE_FLAGS)}
 # (AFS_TREE_FLAGS: extra compiler flags for the tree kernel, for A/B builds of scheduler options)
 if os.environ.get("AFS_TREE_FLAGS"):
     PER_SOURCE["tds_tree.hip"] = TREE_FLAGS + os.environ["AFS_TREE_FLAGS"].split()
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-          # keep the reference's rounding: no contraction of a*b+c into fma
+          # keep the reference's rounding: no contraction of a*b+c into fma (except the tree
+          # kernel, TREE_FLAGS)
           "-ffp-contract=off", "-fno-strict-aliasing", "-Wno-unknown-pragmas"]
 
 
@@ -45,6 +51,8 @@ def _stale() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
+    if os.path.getmtime(os.path.abspath(__file__)) > t:  # (flags changed)
+        return True
     for f in SOURCES + HEADERS:
         if os.path.getmtime(os.path.join(CSRC, f)) > t:
             return True

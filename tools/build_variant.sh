@@ -14,12 +14,12 @@ objs=""
 for s in afs_capi.cpp afs_comm.cpp afs_tables.cpp tds_lane.hip tds_tree.hip tds_plan.hip af_kernels.hip audio_kernels.hip; do
   o=$O/${s%.*}.o
   extra=""
-  [ $s = tds_tree.hip ] && extra="-mllvm -disable-machine-licm ${TREE_EXTRA:-}"  # (as build.py)
+  [ $s = tds_tree.hip ] && extra="-mllvm -disable-machine-licm -ffp-contract=fast ${TREE_EXTRA:-}"  # (as build.py)
   [ $s = tds_plan.hip ] && extra="${PLAN_EXTRA:-}"
   /opt/rocm/bin/hipcc -c -x hip $C/$s -o $o $COMMON $extra &
   objs="$objs $o"
 done
 wait
 /opt/rocm/bin/hipcc -shared -o areafunctionsynthesis_amd/libafs_$TAG.so --offload-arch=gfx950 -fPIC $objs -ldl
-/opt/rocm/bin/hipcc -shared -o tools/phase_prof/libphase_prof_$TAG.so $COMMON -mllvm -disable-machine-licm -I$C -Iinclude ${TREE_EXTRA:-} tools/phase_prof/phase_prof.hip -x hip $C/afs_tables.cpp $C/tds_tree.hip $C/tds_plan.hip
+/opt/rocm/bin/hipcc -shared -o tools/phase_prof/libphase_prof_$TAG.so $COMMON -mllvm -disable-machine-licm -ffp-contract=fast -I$C -Iinclude ${TREE_EXTRA:-} tools/phase_prof/phase_prof.hip -x hip $C/afs_tables.cpp $C/tds_tree.hip $C/tds_plan.hip
 echo built $TAG
