@@ -82,6 +82,9 @@ constexpr int TREE_NE = 104;
 // lane by DPP.  Lane roles are fixed by the partition: the fossa lane folds 84 into the
 // boundaries 28 / 29 of ARM_L28 / ARM_L28 + 1, the junction lane solves the triangle.
 constexpr int ARM_P = 8, ARM_FOLDS = 4, ARM_MAXLEN = 7;  // ARM_MAXLEN: lanes of the longest arm
+// a segment's first real position is at most ARM_START_MAX, or ARM_P - 1 (a one-node segment,
+// its boundary) or ARM_P (none): the walk sets its anchor edge only at positions up to it
+constexpr int ARM_START_MAX = 3;
 constexpr int ARM_FOSSA = 14, ARM_JUNCTION = 15, ARM_L28 = 3;
 constexpr int ARM_END_A = 6, ARM_END_B = 10, ARM_END_C = 13;  // lanes of the arms' last boundaries
 AFS_HD constexpr int arm_fold_pos(int f) { return f == 0 ? 2 : f == 1 ? 3 : f == 2 ? 5 : 6; }

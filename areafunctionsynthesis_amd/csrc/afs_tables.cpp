@@ -220,6 +220,7 @@ bool arm_records(Tables *t) {
     for (int p = 0; p < ARM_P; ++p) pos[p] = p >= start ? SEG[k][p - start] : -1;
     bound[k] = n ? pos[ARM_P - 1] : -1;
     r.start = (uint8_t)start;
+    if (start > ARM_START_MAX && start < ARM_P - 1) ok = false;  // (the walk's anchor-edge positions)
     for (int p = 0; p < ARM_P; ++p) {
       if (pos[p] >= 0) node_uses[pos[p]]++;
       r.d[p] = pos[p] >= 0 ? off(X_DIAG + pos[p]) : ONE;

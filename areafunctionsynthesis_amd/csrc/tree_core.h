@@ -1262,7 +1262,7 @@ AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
   double F = 0.0, dA = 0.0, yA = 0.0;
 #pragma unroll
   for (int p = 0; p < ARM_P - 1; ++p) {
-    F = (p == (int)r.start) ? ea : F;
+    if (p <= ARM_START_MAX) F = (p == (int)r.start) ? ea : F;  // (no segment starts later, arm_records)
     const double e2 = E[p] * E[p];       // (off the pivot chain: D[p+1] waits for inv only)
     const double inv = pivot_recip(D[p]);
     neg = neg | (D[p] < 0.0);
