@@ -26,6 +26,7 @@ struct afs_comm {
   hipStream_t cs = nullptr;  // the gathers' own stream
   hipEvent_t ready = nullptr, done = nullptr;
   bool pending = false;      // a gather was queued since the last fence
+  bool aborted = false;      // the communicator was aborted after a failed group (comm_abort)
 };
 
 namespace {
@@ -36,6 +37,7 @@ struct Rccl {
   ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*CommInitAll)(ncclComm_t *, int, const int *) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
@@ -65,6 +67,7 @@ const Rccl &rccl() {
     sym(r.CommInitRank, "ncclCommInitRank");
     sym(r.CommInitAll, "ncclCommInitAll");
     sym(r.CommDestroy, "ncclCommDestroy");
+    sym(r.CommAbort, "ncclCommAbort");
     sym(r.Send, "ncclSend");
     sym(r.Recv, "ncclRecv");
     sym(r.GroupStart, "ncclGroupStart");
@@ -103,23 +106,55 @@ afs_status comm_setup(afs_comm *m) {
   return AFS_OK;
 }
 
-// queue the gather on the comm's stream behind the context stream's work (no group end of
-// its own when called inside an outer group)
-afs_status gather_enqueue(afs_comm *m, const int16_t *local, int64_t count, int16_t *root_out,
-                          const int64_t *root_counts) {
+// The gather in two parts, so that a caller driving several communicators in one RCCL group
+// can run every fallible HIP step before the group opens: gather_prepare makes the comm's
+// stream wait for the work queued so far on the context's stream; gather_post queues only the
+// RCCL sends / receives (and rank 0's local copy).
+afs_status gather_prepare(afs_comm *m) {
   afs_ctx *c = m->ctx;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   HIP_TRY(c, hipEventRecord(m->ready, c->stream));
   HIP_TRY(c, hipStreamWaitEvent(m->cs, m->ready, 0));
+  return AFS_OK;
+}
+
+afs_status gather_post(afs_comm *m, const int16_t *local, int64_t count, int16_t *root_out,
+                       const std::vector<size_t> &root_bytes) {
+  RcclTransport t{m};
+  const int e = afs::gather_to_root(t, local, (size_t)count * sizeof(int16_t), root_out,
+                                    root_bytes.empty() ? nullptr : root_bytes.data());
+  if (e) return nccl_fail(m->ctx, e, "afs_gather_pcm");
+  return AFS_OK;
+}
+
+std::vector<size_t> root_bytes_of(const afs_comm *m, const int64_t *root_counts) {
   std::vector<size_t> rb;
   if (m->rank == 0 && root_counts) {
     rb.resize((size_t)m->world);
     for (int r = 0; r < m->world; ++r) rb[(size_t)r] = (size_t)root_counts[r] * sizeof(int16_t);
   }
-  RcclTransport t{m};
-  const int e = afs::gather_to_root(t, local, (size_t)count * sizeof(int16_t), root_out, rb.empty() ? nullptr : rb.data());
-  if (e) return nccl_fail(c, e, "afs_gather_pcm");
-  return AFS_OK;
+  return rb;
+}
+
+// The HIP device that owns p (-1: host memory or unknown).
+int device_of(const void *p) {
+  if (!p) return -1;
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged) ? at.device : -1;
+}
+
+// After a failed group: abort the RCCL communicator (its kernels stop) and mark the comm so that
+// afs_comm_destroy does not wait on its stream.
+void comm_abort(afs_comm *m) {
+  if (!m || !m->nc) return;
+  (void)hipSetDevice(m->ctx->cfg.device);
+  if (rccl().CommAbort) (void)rccl().CommAbort(m->nc);
+  m->nc = nullptr;
+  m->aborted = true;
 }
 
 afs_status gather_finish(afs_comm *m) {
@@ -208,7 +243,7 @@ afs_status afs_comm_create_all(afs_ctx *const *ctxs, int32_t n, afs_comm **comms
 void afs_comm_destroy(afs_comm *m) {
   if (!m) return;
   (void)hipSetDevice(m->ctx->cfg.device);
-  if (m->cs) (void)hipStreamSynchronize(m->cs);
+  if (m->cs && !m->aborted) (void)hipStreamSynchronize(m->cs);
   if (m->nc) (void)rccl().CommDestroy(m->nc);
   if (m->ready) (void)hipEventDestroy(m->ready);
   if (m->done) (void)hipEventDestroy(m->done);
@@ -219,7 +254,14 @@ void afs_comm_destroy(afs_comm *m) {
 afs_status afs_gather_pcm(afs_comm *m, const int16_t *local, int64_t count, int16_t *root_out,
                           const int64_t *root_counts) {
   if (!m || count < 0 || (count > 0 && !local) || (m->rank == 0 && !root_out)) return AFS_ERR_INVALID_ARGUMENT;
-  afs_status s = gather_enqueue(m, local, count, root_out, root_counts);
+  if (m->aborted) return afs::fail(m->ctx, AFS_ERR_HIP, "afs_gather_pcm: the communicator was aborted");
+  // rank 0 receives into device memory of its own GPU (a buffer of another device would be a
+  // fault or a silent peer write)
+  if (m->rank == 0 && device_of(root_out) != m->ctx->cfg.device)
+    return afs::fail(m->ctx, AFS_ERR_INVALID_ARGUMENT, "afs_gather_pcm: root_out is not device memory of device %d",
+                     m->ctx->cfg.device);
+  afs_status s = gather_prepare(m);
+  if (s == AFS_OK) s = gather_post(m, local, count, root_out, root_bytes_of(m, root_counts));
   return s == AFS_OK ? gather_finish(m) : s;
 }
 
@@ -251,6 +293,8 @@ afs_status afs_multi_synthesize(afs_ctx *const *ctxs, afs_comm *const *comms, in
   for (int i = 0; i < n; ++i)
     if (!ctxs[i] || !comms[i] || comms[i]->ctx != ctxs[i] || comms[i]->rank != i || comms[i]->world != n)
       return afs::fail(c0, AFS_ERR_INVALID_ARGUMENT, "afs_multi_synthesize: comms[i] must be rank i of n on ctxs[i]");
+  for (int i = 0; i < n; ++i)
+    if (comms[i]->aborted) return afs::fail(c0, AFS_ERR_HIP, "afs_multi_synthesize: communicator %d was aborted", i);
   if (afs::is_device_ptr(frames) || (seeds && afs::is_device_ptr(seeds)) || (nonfinite && afs::is_device_ptr(nonfinite)))
     return afs::fail(c0, AFS_ERR_INVALID_ARGUMENT, "afs_multi_synthesize: frames, seeds and nonfinite are host arrays");
   const int64_t T = (int64_t)(F - 1) * hop;
@@ -280,7 +324,11 @@ afs_status afs_multi_synthesize(afs_ctx *const *ctxs, afs_comm *const *comms, in
   }
   for (int i = 0; i < n; ++i) HIP_TRY(ctxs[i], hipEventRecord(ctxs[i]->ev1, ctxs[i]->stream));
   int16_t *root = pcm_out;
-  const bool host_out = !afs::is_device_ptr(pcm_out);
+  const int out_dev = device_of(pcm_out);
+  const bool host_out = out_dev < 0;
+  if (!host_out && out_dev != c0->cfg.device)
+    return afs::fail(c0, AFS_ERR_INVALID_ARGUMENT, "afs_multi_synthesize: pcm_out is device memory of device %d, not of "
+                     "ctxs[0]'s device %d", out_dev, c0->cfg.device);
   if (host_out) {
     HIP_TRY(c0, hipSetDevice(c0->cfg.device));
     if ((s = afs::ensure(c0, &c0->m_root, &c0->m_root_bytes, (size_t)B * (size_t)T * sizeof(int16_t))) != AFS_OK)
@@ -289,15 +337,24 @@ afs_status afs_multi_synthesize(afs_ctx *const *ctxs, afs_comm *const *comms, in
   }
   std::vector<int64_t> counts((size_t)n);
   for (int i = 0; i < n; ++i) counts[(size_t)i] = cnt[(size_t)i] * T;
-  // every rank's sends / receives in one group (one host thread drives all communicators)
+  // every rank's sends / receives in one group (one host thread drives all communicators); the
+  // HIP steps that can fail (events, stream waits) all run before the group opens, so a failure
+  // never leaves a receive without its send
+  for (int i = 0; i < n; ++i)
+    if ((s = gather_prepare(comms[i])) != AFS_OK) return s;
+  const std::vector<size_t> rb0 = root_bytes_of(comms[0], counts.data());
   if (rccl().GroupStart() != ncclSuccess) return afs::fail(c0, AFS_ERR_HIP, "ncclGroupStart failed");
   afs_status gs = AFS_OK;
   for (int i = 0; i < n && gs == AFS_OK; ++i)
-    gs = gather_enqueue(comms[i], (const int16_t *)ctxs[i]->m_pcm, counts[(size_t)i], i == 0 ? root : nullptr,
-                        i == 0 ? counts.data() : nullptr);
+    gs = gather_post(comms[i], (const int16_t *)ctxs[i]->m_pcm, counts[(size_t)i], i == 0 ? root : nullptr,
+                     i == 0 ? rb0 : std::vector<size_t>());
   const ncclResult_t ge = rccl().GroupEnd();
-  if (gs != AFS_OK) return gs;
-  if (ge != ncclSuccess) return nccl_fail(c0, (int)ge, "ncclGroupEnd");
+  if (gs != AFS_OK || ge != ncclSuccess) {
+    // an incomplete group can leave a receive without its send: abort the communicators
+    // (afs_comm_destroy then skips the stream wait that would block on it)
+    for (int i = 0; i < n; ++i) comm_abort(comms[i]);
+    return gs != AFS_OK ? gs : nccl_fail(c0, (int)ge, "ncclGroupEnd");
+  }
   for (int i = 0; i < n; ++i)
     if ((s = gather_finish(comms[i])) != AFS_OK) return s;
   HIP_TRY(c0, hipSetDevice(c0->cfg.device));

@@ -1,0 +1,130 @@
+// seg_emu.cpp -- TEST-ONLY host execution of the segment-aligned kernel's phase code.
+//
+// Runs csrc/seg_core.h's seg_sample_step with the 16 lanes of each phase executed one after
+// another (cross-lane values are gathered from every lane before any lane consumes them, as a
+// DPP row operation delivers them), so the lane partition, the static condensation and the
+// dynamic walks can be checked against the oracle on the CPU.  Never part of the product;
+// libafs.so does not contain it.
+#include <cstring>
+#include <vector>
+
+#include "seg_core.h"
+
+using namespace afs;
+using namespace afs::seg;
+
+namespace {
+
+struct SegCpuExec {
+  SegLane *R;
+  template <class F> void par(F f) { for (int gl = 0; gl < SW; ++gl) f(gl, R[gl]); }
+  template <class F, class G> void par_uniform(F f, G g) { par(f); g(R[0]); }
+  void sync() {}
+  void mark(int) {}
+  template <int K> uint64_t rec() { return R[K].planw; }
+  template <class F> uint64_t ballot(F f) {
+    uint64_t m = 0;
+    for (int gl = 0; gl < SW; ++gl)
+      if (f(gl, R[gl])) m |= 1ull << gl;
+    return m;
+  }
+  template <class F> uint64_t or64(F f) {
+    uint64_t m = 0;
+    for (int gl = 0; gl < SW; ++gl) m |= f(gl, R[gl]);
+    return m;
+  }
+  template <int N, class F, class G> void scan_add(F f, G g) {
+    std::vector<tree::U4> out(SW);
+    tree::U4 acc{{0u, 0u, 0u, 0u}};
+    for (int gl = 0; gl < SW; ++gl) {
+      const tree::U4 v = f(gl, R[gl]);
+      for (int i = 0; i < N; ++i) acc.v[i] += v.v[i];
+      out[gl] = acc;
+    }
+    for (int gl = 0; gl < SW; ++gl) g(gl, R[gl], out[gl]);
+  }
+  template <int K, int N, class F, class G> void pull(F f, G g) {
+    std::vector<tree::D4> v(SW);
+    for (int gl = 0; gl < SW; ++gl) v[gl] = f(gl, R[gl]);
+    for (int gl = 0; gl < SW; ++gl) {
+      const int src = gl + K;
+      tree::D4 o{{0.0, 0.0, 0.0, 0.0}};
+      if (src >= 0 && src < SW)
+        for (int i = 0; i < N; ++i) o.v[i] = v[src].v[i];
+      g(gl, R[gl], o);
+    }
+  }
+  template <int K, int N, class F, class G> void bcast(F f, G g) {
+    std::vector<tree::D4> v(SW);
+    for (int gl = 0; gl < SW; ++gl) v[gl] = f(gl, R[gl]);
+    tree::D4 o{{0.0, 0.0, 0.0, 0.0}};
+    for (int i = 0; i < N; ++i) o.v[i] = v[K].v[i];
+    for (int gl = 0; gl < SW; ++gl) g(gl, R[gl], o);
+  }
+};
+
+long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, const afs_options &opt, double *out,
+         int64_t *draws) {
+  static Tables T;
+  static SegTables S;
+  build_tables(&T, fs, opt);
+  build_seg_tables(T, &S);
+  if (!S.ok) return -3;
+  std::vector<SegLane> R(SW);
+  for (int gl = 0; gl < SW; ++gl) seg_reset_lane(R[gl]);
+  std::vector<double> X(SX_STRIDE);
+  seg_reset_lds(X.data(), seed);
+  seg_init_lds(X.data(), S);
+  SegCpuExec ex{R.data()};
+  const bool defer = hop >= tree::OUT_DEFER_MIN_HOP;
+  const bool two = opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
+  long t = 0;
+  for (int k = 1; k < F; ++k) {
+    for (int gl = 0; gl < SW; ++gl) seg_frame_load(gl, R[gl], X.data(), S.c, frames + k - 1, frames + k);
+    const long t0 = t;
+    for (int i = 0; i < hop; ++i) {
+      const double ratio = (double)i / (double)hop;
+      uint64_t w[tree::PLAN_WORDS];
+      tree::plan_sample(frames + k - 1, frames + k, ratio, S.uo, two, w);
+      for (int gl = 0; gl < SW; ++gl) R[gl].planw = w[gl % tree::PLAN_WORDS];
+      if (two) seg_sample_step<AFS_GLOTTIS_TWO_MASS>(ex, X.data(), T.uni, T.consts, S.c, ratio, defer);
+      else seg_sample_step<AFS_GLOTTIS_TRIANGULAR>(ex, X.data(), T.uni, T.consts, S.c, ratio, defer);
+      out[t] = R[0].sample;
+      ++t;
+    }
+    if (defer) seg_output_filter_run(X.data(), T.consts, out + t0, hop);
+  }
+  if (draws) *draws = (int64_t) * (const uint64_t *)(X.data() + SX_NDRAW);
+  return t;
+}
+
+}  // namespace
+
+// options as tests/emu/tree_emu.cpp: turbulence, soft walls, noise, skin radiation, fossa,
+// inner length corrections, transvelar coupling, glottis loss, glottis model (ints) and the
+// flow-separation area ratio; iopt == NULL: TdsModel's defaults.
+extern "C" long emu_seg_utterance(const afs_frame *frames, int F, int hop, unsigned seed, double fs, const int *iopt,
+                                  double ratio, double *out, int64_t *draws) {
+  afs_options opt = afs::default_options();
+  if (iopt) {
+    opt.turbulence_losses = iopt[0];
+    opt.soft_walls = iopt[1];
+    opt.generate_noise_sources = iopt[2];
+    opt.radiation_from_skin = iopt[3];
+    opt.piriform_fossa = iopt[4];
+    opt.inner_length_corrections = iopt[5];
+    opt.transvelar_coupling = iopt[6];
+    opt.glottis_loss = iopt[7];
+    opt.glottis_model = iopt[8];
+    opt.flow_separation_area_ratio = ratio;
+  }
+  return run(frames, F, hop, seed, fs, opt, out, draws);
+}
+
+extern "C" int emu_seg_tables_ok(double fs) {
+  static Tables T;
+  static SegTables S;
+  build_tables(&T, fs, afs::default_options());
+  build_seg_tables(T, &S);
+  return S.ok;
+}
