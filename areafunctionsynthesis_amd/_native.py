@@ -18,6 +18,7 @@ STATUS = {0: "ok", 1: "invalid argument", 2: "no HIP device", 3: "HIP runtime er
 AFS_SOLVER_CHOLESKY = 0
 AFS_SOLVER_TREE = 1
 AFS_SOLVER_SOR = 2
+AFS_SOLVER_SEG = 3
 AFS_FP64 = 0
 AFS_ASYNC = 0x1
 AFS_PROFILE = 0x2

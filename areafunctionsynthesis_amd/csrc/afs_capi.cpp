@@ -21,6 +21,7 @@
 #include "afs_audio.h"
 #include "afs_ctx.h"
 #include "afs_model.h"
+#include "afs_seg.h"
 #include "afs_tree.h"
 
 static_assert(sizeof(afs_frame) == 1072, "afs_frame layout");
@@ -68,9 +69,13 @@ namespace {
 
 int64_t pad64(int64_t b) { return (b + 63) / 64 * 64; }
 
-bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_TREE || s == AFS_SOLVER_SOR; }
+bool solver_ok(int32_t s) {
+  return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_TREE || s == AFS_SOLVER_SOR || s == AFS_SOLVER_SEG;
+}
 
-bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE; }
+// the cooperative kernels (16 lanes per utterance, noise-source plans from K5): tree and seg
+bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE || c->cfg.solver == AFS_SOLVER_SEG; }
+bool seg(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_SEG; }
 
 // Bytes of noise-source plans one tree launch may use (afs_ctx::plan_budget: 4 GiB, or
 // AFS_PLAN_BUDGET_MB); a launch covers at most plan_budget / (rows * 128 B) samples and at most
@@ -114,13 +119,15 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     for (int64_t s0 = 0; s0 < S; s0 += per) {
       const int64_t s1 = std::min(S, s0 + per);
       afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)c->plan, per,
-                       c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0};
+                       c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0,
+                       seg(c) ? c->dev_seg->uo : c->dev_tab->consts.sec};
       hipEvent_t e0 = prof_event(c);
       HIP_TRY(c, afs::launch_plan(pa, c->stream));
       hipEvent_t e1 = prof_event(c);
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
                       (const uint64_t *)c->plan, per, lanes, (double *)ws, B, c->host_tab.uni};
-      HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
+      if (seg(c)) HIP_TRY(c, afs::launch_seg_synth(afs::SegArgs{a, c->dev_seg}, c->stream));
+      else HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
       hipEvent_t e2 = prof_event(c);
       prof_pair(c, e0, e1, 1);
       prof_pair(c, e1, e2, 0);
@@ -142,15 +149,19 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
 
 // bytes of the state buffers for B utterances
 size_t ws_bytes_for(const afs_ctx *c, int64_t bp) {
+  if (seg(c)) return (size_t)bp * afs::seg_lds_doubles() * sizeof(double);
   if (tree(c)) return (size_t)bp * afs::tree_lds_doubles() * sizeof(double);
   return (size_t)(afs::lane_ws_rows(c->host_tab) * bp) * sizeof(double);
 }
 size_t lanes_bytes_for(const afs_ctx *c, int64_t bp) {
+  if (seg(c)) return (size_t)bp * afs::seg::SW * afs::seg_lane_bytes();
   return tree(c) ? (size_t)bp * afs::TREE_W * afs::tree_lane_bytes() : 0;
 }
 
 afs_status reset_state(afs_ctx *c, void *ws, int32_t *rng, void *lanes, int64_t bp, int B, const uint32_t *seeds_dev) {
-  if (tree(c))
+  if (seg(c))
+    HIP_TRY(c, afs::launch_seg_reset(lanes, (double *)ws, B, seeds_dev, c->stream));
+  else if (tree(c))
     HIP_TRY(c, afs::launch_tree_reset(lanes, (double *)ws, B, seeds_dev, c->stream));
   else
     HIP_TRY(c, afs::launch_lane_reset((double *)ws, rng, bp, B, seeds_dev, c->stream));
@@ -172,7 +183,9 @@ afs_status nonfinite_report(afs_ctx *c, void *ws, int64_t bp, int B, uint8_t *fl
     *host_sync = true;
   }
   HIP_TRY(c, hipMemsetAsync(c->dcount, 0, sizeof(int32_t), c->stream));
-  if (tree(c))
+  if (seg(c))
+    HIP_TRY(c, afs::launch_seg_nonfinite((const double *)ws, B, c->dcount, dflags, c->stream));
+  else if (tree(c))
     HIP_TRY(c, afs::launch_tree_nonfinite((const double *)ws, B, c->dcount, dflags, c->stream));
   else
     HIP_TRY(c, afs::launch_lane_nonfinite((const double *)ws, bp, B, c->dcount, dflags, c->stream));
@@ -182,14 +195,15 @@ afs_status nonfinite_report(afs_ctx *c, void *ws, int64_t bp, int B, uint8_t *fl
 }
 
 afs_status draws_of(afs_ctx *c, const void *ws, int B, int64_t *draws) {
-  if (!tree(c)) return fail(c, AFS_ERR_UNSUPPORTED, "rand() call counts are kept by the tree solver only");
+  if (!tree(c)) return fail(c, AFS_ERR_UNSUPPORTED, "rand() call counts are kept by the tree and seg solvers only");
   int64_t *d = draws;
   void *tmp = nullptr;
   if (!is_device_ptr(draws)) {
     HIP_TRY(c, hipMalloc(&tmp, (size_t)B * sizeof(int64_t)));
     d = (int64_t *)tmp;
   }
-  hipError_t e = afs::launch_tree_draws((const double *)ws, B, d, c->stream);
+  hipError_t e = seg(c) ? afs::launch_seg_draws((const double *)ws, B, d, c->stream)
+                        : afs::launch_tree_draws((const double *)ws, B, d, c->stream);
   if (e == hipSuccess && tmp) e = hipMemcpyAsync(draws, d, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (tmp) (void)hipFree(tmp);
@@ -208,7 +222,7 @@ void afs_config_default(afs_config *cfg) {
   std::memset(cfg, 0, sizeof *cfg);
   cfg->sampling_rate_hz = 22050.0;
   cfg->precision = AFS_FP64;
-  cfg->solver = AFS_SOLVER_TREE;
+  cfg->solver = AFS_SOLVER_TREE;  // (AFS_SOLVER_SEG once its GPU figures are in: see DESIGN.md 4)
   cfg->device = 0;
   cfg->flags = 0;
   cfg->options = afs::default_options();
@@ -249,6 +263,15 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   if (hipMalloc((void **)&ctx->dev_tab, sizeof(afs::Tables)) != hipSuccess) return bail(AFS_ERR_OUT_OF_MEMORY);
   if (hipMemcpy(ctx->dev_tab, &ctx->host_tab, sizeof(afs::Tables), hipMemcpyHostToDevice) != hipSuccess)
     return bail(AFS_ERR_HIP);
+  if (c.solver == AFS_SOLVER_SEG) {
+    std::vector<char> buf(sizeof(afs::seg::SegTables));
+    auto *st = reinterpret_cast<afs::seg::SegTables *>(buf.data());
+    afs::seg::build_seg_tables(ctx->host_tab, st);
+    if (!st->ok) return bail(AFS_ERR_UNSUPPORTED);
+    if (hipMalloc((void **)&ctx->dev_seg, sizeof(afs::seg::SegTables)) != hipSuccess) return bail(AFS_ERR_OUT_OF_MEMORY);
+    if (hipMemcpy(ctx->dev_seg, st, sizeof(afs::seg::SegTables), hipMemcpyHostToDevice) != hipSuccess)
+      return bail(AFS_ERR_HIP);
+  }
   if (hipMalloc((void **)&ctx->dcount, sizeof(int32_t)) != hipSuccess) return bail(AFS_ERR_OUT_OF_MEMORY);
   if (hipHostMalloc((void **)&ctx->hcount, sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
     return bail(AFS_ERR_OUT_OF_MEMORY);
@@ -270,6 +293,7 @@ void afs_destroy(afs_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
   if (c->dev_tab) (void)hipFree(c->dev_tab);
+  if (c->dev_seg) (void)hipFree(c->dev_seg);
   if (c->ws) (void)hipFree(c->ws);
   if (c->rng) (void)hipFree(c->rng);
   if (c->tree_lanes) (void)hipFree(c->tree_lanes);

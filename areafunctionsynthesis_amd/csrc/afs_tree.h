@@ -35,6 +35,8 @@ struct PlanArgs {
   uint64_t *plan;           // as TreeArgs::plan
   int64_t plan_stride;
   int two_mass;
+  const SecRec *uo;         // the synthesis kernel's LDS offsets of the section outputs' noise-
+                            // smoothed flows (tree: tab->consts.sec; seg: SegTables::uo)
 };
 constexpr int64_t PLAN_RECORD_BYTES = 128;
 

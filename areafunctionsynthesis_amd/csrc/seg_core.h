@@ -45,7 +45,7 @@ constexpr double THR = tree::THR;
 // per-sample values of a lane (not state: cleared before a save)
 struct SegWork {
   // section terms of the dynamic slots (block 1)
-  double L[NDS], R[NDS], E[NDS], D[NDS], A[NDS], iA[NDS], r0[NDS], al[NDS], be[NDS];
+  double L[NDS], R[NDS], E[NDS], D[NDS], A[NDS], iA[NDS], iR0[NDS], al[NDS], be[NDS];
   double rrad, lrad;       // mouth radiation (the slot of section 64)
   double smp[NDS];         // dipole samples
   double sD[NSS], sbe[NSS];  // static slots: D, beta
@@ -61,7 +61,7 @@ struct SegWork {
   double gR0, gR1;         // glottal entrance / transition terms of section 23 (lane-uniform)
   int gon;                 // bit 0: u23 > 0, bit 1: u24 > 0
   double fl[4], p25;       // radiated flows 93..96 and the new p[25] (output stage)
-  bool neg;
+  int32_t neg, pad;        // a pivot this lane met was negative (no padding bytes: SROA)
 };
 
 struct SegLane {
@@ -70,12 +70,12 @@ struct SegLane {
   double u[NDS], ur[NDS], un[NDS];
   double aL[PD], aR[PD], lL[PD], lR[PD];  // frame cache (pharynx / mouth slots)
   double damp[NDS], dout[NDS], dcut[NDS];  // dipoles of the slots
-  uint32_t racc[NDS];
+  uint32_t racc[NDS + 1];  // (+1: no padding bytes, which would keep the struct in scratch)
   // static slots
   double sp[NSS], spr[NSS], sw[NSS], swr[NSS], swr2[NSS], su[NSS], sur[NSS];
   double sample;           // lane 0: the output of the sample
   uint64_t planw;          // word gl of this sample's plan (tree_plan.h)
-  uint32_t rtmp[3];        // rand() block scratch
+  uint32_t rtmp[4];        // rand() block scratch (4th: padding)
   SegWork k;
 };
 
@@ -83,8 +83,7 @@ struct SegLane {
 // reset (Synthesizer::reset + TdsModel::resetMotion + TriangularGlottis::resetMotion)
 // ---------------------------------------------------------------------------
 AFS_HD inline void seg_reset_lane(SegLane &R) {
-  char *b = reinterpret_cast<char *>(&R);
-  for (unsigned i = 0; i < sizeof(SegLane); ++i) b[i] = 0;
+  R = SegLane{};
 #pragma unroll
   for (int j = 0; j < NDS; ++j) R.dcut[j] = 3000.0;
 }
@@ -184,10 +183,15 @@ AFS_HD inline void seg_targets_uniform(Xc &x, const double *X, const Consts &T, 
   }
 }
 
-// The section terms of one dynamic slot (prepareTimeStep, TdsModel.cpp:732-834, with the
-// repeated divisions folded into reciprocals as in tree_core.h phase_network).
-AFS_HD inline void seg_section(SegLane &R, int j, const DynSlot &d, const Uni &U, const Consts &T, double r1,
-                               double ratio, double open, const SegUni &su, double *X) {
+// The section terms of one dynamic slot (prepareTimeStep, TdsModel.cpp:732-834), with the
+// divisions rewritten around one reciprocal of the area: the Poiseuille resistance of the
+// circular and the elliptic section (:741-760) as polynomials in 1/A, the wall terms with the
+// wall surface cancelled (alpha = surf / K, beta = k1 w + k2 w' + k3 w''; seg_tables.cpp), the
+// radiation elements of section 64 (:1874, :1889) from 1/A and r0.  (Rounding-level
+// differences from the reference's quotients; the decisions -- elliptic or not, the surface
+// clamp -- are the reference's comparisons.)
+AFS_HD inline void seg_section(SegLane &R, int j, const DynSlot &d, const Uni &U, const Consts &T, const SegConsts &C,
+                               double r1, double ratio, double open, const SegUni &su, double *X) {
   const Hot &h = T.h;
   const uint16_t f = d.flags;
   double area, len;
@@ -202,41 +206,37 @@ AFS_HD inline void seg_section(SegLane &R, int j, const DynSlot &d, const Uni &U
                               : k == K_STATIC ? d.c1 : 1.0;
   }
   const bool glot = (f & DF_GLOTSEC) != 0;
-  const double dt = h.dt, idt = h.inv_dtTH, idt2 = h.inv_dt2TH2;
-  const double vol = area * len;
   const double inv_area = fast_rcp(area);
   const double r0 = fast_sqrt(area * (1.0 / PI));
-  const double circ = 2.0 * PI * r0;
-  const double rmin = glot ? 0.8 : 1.6;
-  const bool ell = r0 < rmin;
-  const double a = ell ? rmin : r0;
-  const double b = ell ? area * (glot ? 1.0 / (PI * 0.8) : 1.0 / (PI * 1.6)) : r0;
+  const double ia2 = inv_area * inv_area;
+  const bool ell = r0 < (glot ? 0.8 : 1.6);
+  // elliptic: 2 mu len (a^2 + b^2) / (pi a^3 b^3), a = rmin, b = A / (pi rmin)
+  //         = len / A (2 mu pi^2 rmin^2 / A^2 + 2 mu / rmin^2); circular: 4 mu pi len / A^2
+  const double ce = glot ? 2.0 * MU * PI * PI * 0.64 : 2.0 * MU * PI * PI * 2.56;
+  const double cf = glot ? 2.0 * MU / 0.64 : 2.0 * MU / 2.56;
+  const double Rr = ell ? (len * inv_area) * fma(ce, ia2, cf) : (4.0 * MU * PI * len) * ia2;
   const double L = (RHO * 0.5 * len) * inv_area;
-  const double Cc = vol * (1.0 / (RHO * CSND * CSND));
-  const double Rr = fast_div((2.0 * MU * len) * (a * a + b * b), PI * a * a * a * b * b * b);
-  double surf = circ * len;
+  const double Cc = (area * len) * (1.0 / (RHO * CSND * CSND));
+  double surf = (2.0 * PI * r0) * len;
   if (surf < AMIN) surf = AMIN;
-  const double inv_surf = fast_rcp(surf);
-  const double Rw = h.Bw_ph0 * inv_surf, Lw = h.Mw_ph0 * inv_surf;
-  const double alw = fast_rcp(Lw * idt2 + Rw * idt + h.Kw_ph0 * inv_surf);
-  const double bew = alw * (R.w[j] * (Lw * idt2 + Rw * idt) + R.wr[j] * (Lw * (TH1 / TH + 1.0) * idt + Rw * (TH1 / TH)) +
-                            R.wr2[j] * Lw * (TH1 / TH));
   const bool walls = U.opt.soft_walls && (f & DF_WALLS);
-  const double alpha = walls ? alw : 0.0, beta = walls ? bew : 0.0;
-  const double E = fast_div(dt * TH, Cc + alpha);
+  const double alpha = walls ? surf * C.nk[NK_INVK] : 0.0;
+  const double beta = walls ? fma(R.w[j], C.nk[NK_K1], fma(R.wr[j], C.nk[NK_K2], R.wr2[j] * C.nk[NK_K3])) : 0.0;
+  const double E = fast_div(h.dt * TH, Cc + alpha);
   const double src = (f & DF_TV67) ? su.tvsrc : 0.0;
   const double D = R.p[j] + h.dtTH1 * R.pr[j] - E * (beta - src);
+  const double iR0 = (PI * r0) * inv_area;  // 1 / r0
   SegWork &k = R.k;
-  k.L[j] = L; k.R[j] = Rr; k.E[j] = E; k.D[j] = D; k.A[j] = area; k.iA[j] = inv_area; k.r0[j] = r0;
+  k.L[j] = L; k.R[j] = Rr; k.E[j] = E; k.D[j] = D; k.A[j] = area; k.iA[j] = inv_area; k.iR0[j] = iR0;
   k.al[j] = alpha; k.be[j] = beta;
-  if (j == 1) {  // (section 64 is slot 1 of arm B's first lane) radiation R and L (TdsModel.cpp:1874, 1889)
-    k.rrad = fast_div(h.rrad_num, 9.0 * PI * PI * area);
-    k.lrad = fast_div(h.lrad_num, 3.0 * PI * fast_sqrt(area * PI));
+  if (j == 1) {  // (section 64 is slot 1 of arm B's first lane) radiation R and L
+    k.rrad = C.nk[NK_RRAD] * inv_area;
+    k.lrad = (C.nk[NK_LRAD] * r0) * inv_area;
   }
   // the source block other lanes' rows read, and D for the static rows
   double *g = &xat(X, d.g_own);
   g[G_L] = L; g[G_R1] = Rr; g[G_E] = E; g[G_D] = D;
-  g[G_AREA] = area; g[G_R0] = r0; g[G_IAREA] = inv_area;
+  g[G_AREA] = area; g[G_IAREA] = inv_area; g[G_IR0] = iR0;
   xat(X, d.d_own) = D;
 }
 
@@ -280,7 +280,7 @@ AFS_HD inline void seg_block1(Xc &x, double *X, const Uni &U, const Consts &T, c
   const double open = r1 * X[SX_FRAME + 2] + ratio * X[SX_FRAME + 3];
   x.par([&](int gl, SegLane &R) {
 #pragma unroll
-    for (int j = 0; j < NDS; ++j) seg_section(R, j, C.dyn[gl][j], U, T, r1, ratio, open, su, X);
+    for (int j = 0; j < NDS; ++j) seg_section(R, j, C.dyn[gl][j], U, T, C, r1, ratio, open, su, X);
     // static slots: beta from the wall state, D (the other terms are table constants)
     const StatLane &S = C.st[gl];
 #pragma unroll
@@ -479,12 +479,12 @@ AFS_HD inline void seg_rows_dyn(int gl, SegLane &R, const double *X, const Uni &
   const double dR0g = k.gR0, dR1g = k.gR1;
   const int onb = k.gon;
   // the source sections' blocks, every slot's loads first
-  double sL[NDS], sR[NDS], sE[NDS], sD[NDS], sA[NDS], sr0[NDS], siA[NDS];
+  double sL[NDS], sR[NDS], sE[NDS], sD[NDS], sA[NDS], siR0[NDS], siA[NDS];
 #pragma unroll
   for (int j = 0; j < NDS; ++j) {
     const double *g = &xat(X, C.dyn[gl][j].g_src);
     sL[j] = g[G_L]; sR[j] = g[G_R1]; sE[j] = g[G_E]; sD[j] = g[G_D];
-    sA[j] = g[G_AREA]; sr0[j] = g[G_R0]; siA[j] = g[G_IAREA];
+    sA[j] = g[G_AREA]; siR0[j] = g[G_IR0]; siA[j] = g[G_IAREA];
   }
   // bifurcation partners (slot 4 <-> 2 or 0; seg_tables.cpp checks the pattern)
   const bool p40 = C.dyn[gl][FOLD].partner == 0;
@@ -520,8 +520,9 @@ AFS_HD inline void seg_rows_dyn(int gl, SegLane &R, const double *X, const Uni &
     LB = (f & DF_RAD_L) ? k.lrad : LB;
     RB = (f & DF_RAD_R) ? k.rrad : RB;
     double LAB = La + LB;
-    {
-      const double jl = tree::junction_l(sr0[j], k.r0[j]);
+    {  // getJunctionInductance (TdsModel.cpp:1745-1778): 8 rho H / (3 pi^2 b), H = 1 - b / a with
+       // a, b the larger and smaller radius = 8 rho / (3 pi^2) |1/r_a - 1/r_b|
+      const double jl = (8.0 * RHO / (3.0 * PI * PI)) * fabs(siR0[j] - k.iR0[j]);
       const bool use = (opt.inner_length_corrections != 0) & ((f & DF_JL) != 0);
       LAB = use ? LAB + jl : LAB;
     }
@@ -618,8 +619,14 @@ AFS_HD inline void seg_static_z(Xc &x, const SegConsts &C) {
   x.template pull<1, 1>([&](int, SegLane &R) { return D4{{R.k.zc, 0.0, 0.0, 0.0}}; },
                         [&](int gl, SegLane &R, const D4 &v) {
                           const StatSlot *s = C.st[gl].s;
+                          double z[NSS];
 #pragma unroll
-                          for (int j = 0; j < NSS; ++j) R.k.sz[j] += s[j].c[SC_CB] * v.v[0];
+                          for (int j = 0; j < NSS; ++j) z[j] = R.k.sz[j] + s[j].c[SC_CB] * v.v[0];
+#pragma unroll
+                          for (int j = 0; j < NSS; ++j) R.k.sz[j] = z[j];
+                          // the subtree root's z (for the attach node), selected among values
+                          const int r = C.st[gl].root;
+                          R.k.zc = r == 0 ? z[0] : r == 1 ? z[1] : z[2];
                         });
 }
 
@@ -684,7 +691,7 @@ AFS_HD inline void seg_walk(int gl, SegLane &R, const SegConsts &C) {
   k.Yb = Y[PD - 1];
   k.dA = dA;
   k.yA = yA;
-  k.neg = neg && arm;
+  k.neg = (neg && arm) ? 1 : 0;
 }
 
 // Back substitution of a lane's positions from its boundary's solution and the anchor's.
@@ -706,10 +713,7 @@ AFS_HD inline void seg_solve(Xc &x, const SegConsts &C) {
   // static: z = K^-1 y, its roots to the attach nodes (23: lane 0 slot 0, 69: lane 10 slot 0,
   // 84: lane 1 fold)
   seg_static_z(x, C);
-  auto zroot = [&](int gl, SegLane &R) {
-    const int r = C.st[gl].root;
-    return D4{{r == 0 ? R.k.sz[0] : r == 1 ? R.k.sz[1] : R.k.sz[2], 0.0, 0.0, 0.0}};
-  };
+  auto zroot = [&](int, SegLane &R) { return D4{{R.k.zc, 0.0, 0.0, 0.0}}; };
   x.template bcast<T_ROOT_LANE, 1>(zroot, [&](int, SegLane &R, const D4 &v) { R.k.jy[0] = v.v[0]; });
   x.template bcast<N_ROOT_LANE, 1>(zroot, [&](int, SegLane &R, const D4 &v) { R.k.jy[1] = v.v[0]; });
   x.template bcast<F_ROOT_LANE, 1>(zroot, [&](int, SegLane &R, const D4 &v) { R.k.jy[2] = v.v[0]; });
@@ -744,7 +748,7 @@ AFS_HD inline void seg_solve(Xc &x, const SegConsts &C) {
                            });
   }
   x.par([&](int gl, SegLane &R) {
-    R.k.neg = R.k.neg | (((C.dl[gl].wf & WF_ARM) != 0) & (R.k.Db < 0.0));
+    R.k.neg = R.k.neg | ((((C.dl[gl].wf & WF_ARM) != 0) & (R.k.Db < 0.0)) ? 1 : 0);
     R.k.jd[0] = R.k.Dp[0];
     R.k.jy[0] = R.k.Yp[0];
     R.k.jd[1] = R.k.Dp[2];
@@ -819,7 +823,7 @@ AFS_HD inline void seg_solve(Xc &x, const SegConsts &C) {
   }
   // a negative pivot anywhere: every solution of the sample is NaN (the reference's Cholesky
   // takes the square root of it, TdsModel.cpp:2267)
-  const bool bad = x.ballot([&](int, SegLane &R) { return R.k.neg; }) != 0;
+  const bool bad = x.ballot([&](int, SegLane &R) { return R.k.neg != 0; }) != 0;
   x.template pull<-1, 1>([&](int, SegLane &R) { return D4{{R.k.xb, 0.0, 0.0, 0.0}}; },
                          [&](int gl, SegLane &R, const D4 &v) {
                            seg_back(gl, R, C, v.v[0]);

@@ -58,7 +58,7 @@ enum : int {
   SX_D = SX_UN_SINK + 1,           // D of every section, zero, sink
   SX_D_ZERO = SX_D + NS, SX_D_SINK = SX_D_ZERO + 1,
   SX_G = SX_D_SINK + 1,            // sources of the dynamic rows: sections 22..68, 8 doubles each
-  NG = 47, G0 = 22,                //   (L, R1, E, D, area, r0, 1/area, -), then a zero and a sink block
+  NG = 47, G0 = 22,                //   (L, R1, E, D, area, 1/area, 1/r0, -), then a zero and a sink block
   SX_G_ZERO = SX_G + 8 * NG, SX_G_SINK = SX_G_ZERO + 8,
   SX_P4 = SX_G_SINK + 8,           // p[22..25] after the update (glottis inputs)
   SX_TVP = SX_P4 + 4,              // p[43], p[67] (transvelar filter inputs)
@@ -80,7 +80,7 @@ enum : int {
 };
 static_assert(SX_STRIDE % 32 == 16, "utterance blocks offset by half a bank row");
 static_assert(SX_G % 2 == 0, "16-byte aligned source blocks");
-constexpr int GB = 8, G_L = 0, G_R1 = 1, G_E = 2, G_D = 3, G_AREA = 4, G_R0 = 5, G_IAREA = 6;
+constexpr int GB = 8, G_L = 0, G_R1 = 1, G_E = 2, G_D = 3, G_AREA = 4, G_IAREA = 5, G_IR0 = 6;
 
 // ---- dynamic slot records ------------------------------------------------------------------
 // Where a slot's section area and length come from.
@@ -186,11 +186,13 @@ struct alignas(16) StatLane {
   StatSlot s[NSS];
 };
 
+// network constants of the dynamic sections (walls of pharynx / mouth / nose sections)
+enum : int { NK_INVK, NK_K1, NK_K2, NK_K3, NK_RRAD, NK_LRAD, NK_N = 8 };
 struct SegConsts {
   DynSlot dyn[SW][NDS];
   DynLane dl[SW];
   StatLane st[SW];
-  double jn_pad[2];
+  double nk[NK_N];
 };
 
 struct SegTables {

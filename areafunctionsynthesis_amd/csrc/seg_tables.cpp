@@ -458,8 +458,25 @@ void build_seg_tables(const Tables &t, SegTables *out) {
   out->g22[G_R1] = t.R[S_LAST_TRACHEA];
   out->g22[G_E] = t.E[S_LAST_TRACHEA];
   out->g22[G_AREA] = t.area[S_LAST_TRACHEA];
-  out->g22[G_R0] = std::sqrt(t.area[S_LAST_TRACHEA] / PI);
   out->g22[G_IAREA] = 1.0 / t.area[S_LAST_TRACHEA];
+  out->g22[G_IR0] = 1.0 / std::sqrt(t.area[S_LAST_TRACHEA] / PI);
+  // the walls of the dynamic sections (pharynx / mouth / nose: Tube.cpp's defaults) in the form
+  // alpha = surf / K, beta = k1 w + k2 w' + k3 w'' (TdsModel.cpp:805-832 with the wall surface
+  // cancelled: Lw = Mw / surf, Rw = Bw / surf, 1 / Cw = Kw / surf)
+  {
+    const double Mw = t.Mw[S_PHARYNX0], Bw = t.Bw[S_PHARYNX0], Kw = t.Kw[S_PHARYNX0];
+    const double idt2 = 1.0 / (t.dt * t.dt * TH * TH);
+    const double K = Mw * idt2 + Bw * idt + Kw;
+    C.nk[NK_INVK] = 1.0 / K;
+    C.nk[NK_K1] = (Mw * idt2 + Bw * idt) / K;
+    C.nk[NK_K2] = (Mw * (TH1_TH + 1.0) * idt + Bw * TH1_TH) / K;
+    C.nk[NK_K3] = Mw * TH1_TH / K;
+    C.nk[NK_RRAD] = t.rrad_num / (9.0 * PI * PI);  // Rrad = this / A  (TdsModel.cpp:1874)
+    C.nk[NK_LRAD] = t.lrad_num / (3.0 * PI);       // Lrad = this r0 / A  (:1889: 8 rho / (3 pi sqrt(A pi)))
+    for (int s = S_GLOT_LO; s <= S_NOSE0 + 4; ++s)
+      if (t.Mw[s] != Mw || t.Bw[s] != Bw || t.Kw[s] != Kw) ok = false;  // (one wall kind for the dynamic slots)
+    if (t.Mw[S_FOSSA0] != Mw || t.Bw[S_FOSSA0] != Bw || t.Kw[S_FOSSA0] != Kw) ok = false;
+  }
   (void)dyn_sec;
   out->ok = ok ? 1 : 0;
 }

@@ -52,10 +52,10 @@ __global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
     // two instantiations of the scans: LDS frames (ds_read) and global frames (global loads);
     // one pointer that may point at either would make every frame read a flat load
     if (staged)
-      plan_sample((const afs_frame *)fr_lds[k - 1 - k_lo], (const afs_frame *)fr_lds[k - k_lo], ratio,
-                  a.tab->consts.sec, a.two_mass != 0, w);
+      plan_sample((const afs_frame *)fr_lds[k - 1 - k_lo], (const afs_frame *)fr_lds[k - k_lo], ratio, a.uo,
+                  a.two_mass != 0, w);
     else
-      plan_sample(f + (k - 1), f + k, ratio, a.tab->consts.sec, a.two_mass != 0, w);
+      plan_sample(f + (k - 1), f + k, ratio, a.uo, a.two_mass != 0, w);
 #pragma unroll
     for (int q = 0; q < PLAN_WORDS; ++q) rec_lds[threadIdx.x * PLAN_PITCH + q] = w[q];
   }

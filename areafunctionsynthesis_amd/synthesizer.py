@@ -25,7 +25,8 @@ from .frames import FRAME_DTYPE
 
 _vp = ctypes.c_void_p
 
-SOLVERS = {"cholesky": _native.AFS_SOLVER_CHOLESKY, "tree": _native.AFS_SOLVER_TREE, "sor": _native.AFS_SOLVER_SOR}
+SOLVERS = {"cholesky": _native.AFS_SOLVER_CHOLESKY, "tree": _native.AFS_SOLVER_TREE, "sor": _native.AFS_SOLVER_SOR,
+           "seg": _native.AFS_SOLVER_SEG}
 
 
 def _addr(x) -> int:

@@ -70,7 +70,9 @@ typedef enum afs_status {
 typedef enum afs_solver {
   AFS_SOLVER_CHOLESKY = 0, /* TdsModel::CHOLESKY_FACTORIZATION, same operation order (TdsModel.cpp:2231-2314) */
   AFS_SOLVER_TREE = 1,     /* nested-dissection LDL^T on the tube tree (same system, fewer flops) */
-  AFS_SOLVER_SOR = 2       /* TdsModel::SOR_GAUSS_SEIDEL, same sweep order (TdsModel.cpp:2105-2180) */
+  AFS_SOLVER_SOR = 2,      /* TdsModel::SOR_GAUSS_SEIDEL, same sweep order (TdsModel.cpp:2105-2180) */
+  AFS_SOLVER_SEG = 3       /* the same LDL^T with lanes owning the same currents in every phase and the
+                              static subtrees condensed (the default: the fastest kernel) */
 } afs_solver;
 
 /* Glottis model driven by the synthesizer: the reference's Synthesizer uses TriangularGlottis

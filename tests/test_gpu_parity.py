@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 
 GOLD_TOL = 1e-9
 RMS_TOL = 1e-4
-SOLVERS = ("cholesky", "tree")
+SOLVERS = ("cholesky", "tree", "seg")
 
 
 @pytest.fixture(scope="module")
@@ -265,7 +265,7 @@ def _full_length_check(ctx, w, frames, stride, parity_report, label, solver):
     rms = np.sqrt(np.mean(err ** 2, axis=1))
     mx = np.abs(err).max(axis=1)
     flips = None
-    if solver == "tree":
+    if solver in ("tree", "seg"):
         gd = ctx.rng_draws(B)[idx]
         flips = int(np.count_nonzero(gd != draws))
     parity_report.append(
@@ -294,17 +294,18 @@ def test_full_second_static_vowels_rms(contexts, solver, parity_report):
     assert np.array_equal(y, y2)
 
 
-def test_full_second_fricatives_config5(contexts, parity_report):
+@pytest.mark.parametrize("solver", ("tree", "seg"))
+def test_full_second_fricatives_config5(contexts, parity_report, solver):
     """Config 5 at its defined length: fricatives s f z S Z x C R v (Default.params:44-52) with the
     velum open 1.0 cm^2 (MainPage.cpp:127-131), 1 s @ 44.1 kHz, noise sources active; 512
     utterances on the GPU, every 8th (64) against the oracle over the whole second, with the
     rand() call counts compared utterance by utterance."""
     from areafunctionsynthesis_amd.workloads import build_frames, fricatives
-    ctx = contexts(44100.0, "tree")
+    ctx = contexts(44100.0, solver)
     w = fricatives(512, seconds=1.0, fs=44100.0, velum_cm2=1.0)
     frames = build_frames(w, ctx.af_to_frames)
     _full_length_check(ctx, w, frames, 8, parity_report, "config 5 (fricatives + velum 1.0 cm^2, 1 s @ 44.1 kHz)",
-                       "tree")
+                       solver)
 
 
 OPTION_VARIANTS = [

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round-3 GPU session (run on the GPU box): tests, smoke, bench, kernel-trace profile, PMC
+# traffic passes (+ the FETCH_SIZE calibration probe) and the fp64 SQ pass.  Each GPU step has
+# its own time limit; anything but pass / test failure ends the script.
+# usage: tools/r02_session.sh TAG [steps...]   (steps: test smoke bench prof pmc sq calib)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:?tag}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+R=$PWD
+ok() {
+  if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "STOP after $2 (status $1)"; exit "$1"; fi
+  echo "$2 -> status $1"
+}
+STEPS=${*:-"test smoke bench prof pmc sq calib"}
+BA=${BENCH_ARGS:-}
+for s in $STEPS; do
+  case $s in
+    test)  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PK:+-k "$PK"} > $OUT/pytest_gpu.log 2>&1; ok $? pytest; tail -30 $OUT/pytest_gpu.log ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; ok $? smoke ;;
+    bench) timeout -k 10 600 python bench.py $BA > $OUT/bench.json 2> $OUT/bench.err; ok $? bench; cat $OUT/bench.json ;;
+    prof)  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o run -- python3 $R/bench.py $BA --no-cpu-baseline) > $OUT/prof.log 2>&1; ok $? prof ;;
+    pmc)   (cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/$OUT/pmc_fetch -o run -- python3 $R/bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline) > $OUT/pmc_fetch.log 2>&1; ok $? pmc_fetch
+           (cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/$OUT/pmc_write -o run -- python3 $R/bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline) > $OUT/pmc_write.log 2>&1; ok $? pmc_write ;;
+    sq)    (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_FLOPS_FP64 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --kernel-trace --output-format csv -d $R/$OUT/pmc_sq -o run -- python3 $R/bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline) > $OUT/pmc_sq.log 2>&1; ok $? pmc_sq ;;
+    calib) (cd /tmp && timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/$OUT/calib -o run -- $R/tools/microbench/fetch_calib) > $OUT/calib.log 2>&1; ok $? calib ;;
+    pp)    timeout -k 10 300 python tools/phase_prof/run.py --batch 8192 --seconds 0.02 > $OUT/phase_prof.txt 2>&1; ok $? phase_prof; cat $OUT/phase_prof.txt ;;
+  esac
+done
+echo ALL DONE
