@@ -44,13 +44,12 @@ constexpr double THR = tree::THR;
 
 // per-sample values of a lane (not state: cleared before a save)
 struct SegWork {
-  // section terms of the dynamic slots (block 1)
-  double L[NDS], R[NDS], E[NDS], D[NDS], A[NDS], iA[NDS], iR0[NDS], al[NDS], be[NDS];
+  // (the section terms of block 1 go to the LDS blocks SX_G / SX_D, not to registers)
   double rrad, lrad;       // mouth radiation (the slot of section 64)
-  double smp[NDS];         // dipole samples
-  double sD[NSS], sbe[NSS];  // static slots: D, beta
+  double smp[PD];          // dipole samples (slots 0..3)
+  double fD;               // D of the fold's section (84)
   // rows and the solve
-  double Dp[NDS], Yp[NDS], Ea[NDS], ebr[NDS];
+  double Dp[NDS], Yp[NDS], E[NDS], Ea[NDS], ebr[NDS];  // pivot, rhs, own and source section's E
   double iv[3], Fw[3], E3[3];
   double l0, l1, il, Yl;
   double dA, yA, Ff, Db, Yb, binv, xb, Fn, xJ, ej;
@@ -67,10 +66,9 @@ struct SegWork {
 struct SegLane {
   // dynamic slots: section and current state
   double p[NDS], pr[NDS], w[NDS], wr[NDS], wr2[NDS];
-  double u[NDS], ur[NDS], un[NDS];
-  double aL[PD], aR[PD], lL[PD], lR[PD];  // frame cache (pharynx / mouth slots)
-  double damp[NDS], dout[NDS], dcut[NDS];  // dipoles of the slots
-  uint32_t racc[NDS + 1];  // (+1: no padding bytes, which would keep the struct in scratch)
+  double u[NDS], ur[NDS];  // (the noise-smoothed flows live in SX_UN, the frame cache in SX_FC)
+  double damp[PD], dout[PD], dcut[PD];  // dipoles of the slots 0..3 (the fold has none)
+  uint32_t racc[PD];
   // static slots
   double sp[NSS], spr[NSS], sw[NSS], swr[NSS], swr2[NSS], su[NSS], sur[NSS];
   double sample;           // lane 0: the output of the sample
@@ -85,7 +83,7 @@ struct SegLane {
 AFS_HD inline void seg_reset_lane(SegLane &R) {
   R = SegLane{};
 #pragma unroll
-  for (int j = 0; j < NDS; ++j) R.dcut[j] = 3000.0;
+  for (int j = 0; j < PD; ++j) R.dcut[j] = 3000.0;
 }
 
 AFS_HD inline void seg_reset_lds(double *X, uint32_t seed) {
@@ -104,13 +102,14 @@ AFS_HD inline void seg_init_lds(double *X, const SegTables &S) {
 // ---------------------------------------------------------------------------
 AFS_HD inline void seg_frame_load(int gl, SegLane &R, double *X, const SegConsts &C, const afs_frame *fl,
                                   const afs_frame *fr) {
-#pragma unroll
-  for (int j = 0; j < PD; ++j) {
-    const int m = C.dyn[gl][j].m;  // (0 for the slots that do not interpolate: unused)
-    R.aL[j] = clampA(fl->area_cm2[m]);  // the caller's Tube stores clamped areas (Tube.cpp:337)
-    R.aR[j] = clampA(fr->area_cm2[m]);
-    R.lL[j] = fl->length_cm[m];
-    R.lR[j] = fr->length_cm[m];
+  (void)R;
+  (void)C;
+  for (int m = gl; m < NPM; m += SW) {  // (lanes share the 40 sections)
+    double *fc = X + SX_FC + 4 * m;
+    fc[0] = clampA(fl->area_cm2[m]);  // the caller's Tube stores clamped areas (Tube.cpp:337)
+    fc[1] = clampA(fr->area_cm2[m]);
+    fc[2] = fl->length_cm[m];
+    fc[3] = fr->length_cm[m];
   }
   if (gl == 0) {
     X[SX_FRAME + 0] = fl->teeth_position_cm;
@@ -147,7 +146,7 @@ struct SegUni {
 };
 
 template <class Xc>
-AFS_HD inline void seg_targets_uniform(Xc &x, const double *X, const Consts &T, double a_glot_up, tree::Target *t) {
+AFS_HD inline void seg_targets_uniform(Xc &x, const double *X, const SegHot &T, double a_glot_up, tree::Target *t) {
   using namespace tree;
   const uint64_t hdr = x.template rec<PW_HDR>(), uo = x.template rec<PW_UO>(), uol = x.template rec<PW_UOL>();
   const uint32_t fl = (uint32_t)hdr & 0xffu;
@@ -190,20 +189,31 @@ AFS_HD inline void seg_targets_uniform(Xc &x, const double *X, const Consts &T, 
 // radiation elements of section 64 (:1874, :1889) from 1/A and r0.  (Rounding-level
 // differences from the reference's quotients; the decisions -- elliptic or not, the surface
 // clamp -- are the reference's comparisons.)
-AFS_HD inline void seg_section(SegLane &R, int j, const DynSlot &d, const Uni &U, const Consts &T, const SegConsts &C,
+AFS_HD inline void seg_section(SegLane &R, int j, const DynSlot &d, const Uni &U, const SegHot &T, const SegConsts &C,
                                double r1, double ratio, double open, const SegUni &su, double *X) {
   const Hot &h = T.h;
+  // (the record's fields first, as values: a select whose operand is a load becomes a branch)
   const uint16_t f = d.flags;
+  const int kind = d.kind;
+  const double c0 = d.c0, c1 = d.c1;
+  const uint16_t g_own = d.g_own, d_own = d.d_own;
   double area, len;
   {
-    const double apm = interp_area(r1, R.aL[j < PD ? j : 0], ratio, R.aR[j < PD ? j : 0]);
-    const double lpm = interp_len(r1, R.lL[j < PD ? j : 0], ratio, R.lR[j < PD ? j : 0]);
-    const double anose = clampA(open + (d.c0 * (h.nose4_area - open)) * (1.0 / 16));
-    const int k = d.kind;
-    area = k == K_PM ? apm : k == K_GLOT0 ? su.g.go.a0 : k == K_GLOT1 ? su.g.go.a1 : k == K_NOSE ? anose
-                                 : k == K_STATIC ? d.c0 : 1.0;
-    len = k == K_PM ? lpm : k == K_GLOT0 ? su.g.go.l0 : k == K_GLOT1 ? su.g.go.l1 : k == K_NOSE ? h.len_nose0
-                              : k == K_STATIC ? d.c1 : 1.0;
+    const double *fc = X + SX_FC + 4 * d.m;  // (section 25's for the slots that do not interpolate)
+    const double apm = interp_area(r1, fc[0], ratio, fc[1]);
+    const double lpm = interp_len(r1, fc[2], ratio, fc[3]);
+    const double anose = clampA(open + (c0 * (h.nose4_area - open)) * (1.0 / 16));
+    const bool pm = kind == K_PM, g0 = kind == K_GLOT0, g1 = kind == K_GLOT1, no = kind == K_NOSE, st = kind == K_STATIC;
+    area = st ? c0 : 1.0;
+    area = no ? anose : area;
+    area = g1 ? su.g.go.a1 : area;
+    area = g0 ? su.g.go.a0 : area;
+    area = pm ? apm : area;
+    len = st ? c1 : 1.0;
+    len = no ? h.len_nose0 : len;
+    len = g1 ? su.g.go.l1 : len;
+    len = g0 ? su.g.go.l0 : len;
+    len = pm ? lpm : len;
   }
   const bool glot = (f & DF_GLOTSEC) != 0;
   const double inv_area = fast_rcp(area);
@@ -227,21 +237,19 @@ AFS_HD inline void seg_section(SegLane &R, int j, const DynSlot &d, const Uni &U
   const double D = R.p[j] + h.dtTH1 * R.pr[j] - E * (beta - src);
   const double iR0 = (PI * r0) * inv_area;  // 1 / r0
   SegWork &k = R.k;
-  k.L[j] = L; k.R[j] = Rr; k.E[j] = E; k.D[j] = D; k.A[j] = area; k.iA[j] = inv_area; k.iR0[j] = iR0;
-  k.al[j] = alpha; k.be[j] = beta;
   if (j == 1) {  // (section 64 is slot 1 of arm B's first lane) radiation R and L
     k.rrad = C.nk[NK_RRAD] * inv_area;
     k.lrad = (C.nk[NK_LRAD] * r0) * inv_area;
   }
   // the source block other lanes' rows read, and D for the static rows
-  double *g = &xat(X, d.g_own);
+  double *g = &xat(X, g_own);
   g[G_L] = L; g[G_R1] = Rr; g[G_E] = E; g[G_D] = D;
-  g[G_AREA] = area; g[G_IAREA] = inv_area; g[G_IR0] = iR0;
-  xat(X, d.d_own) = D;
+  g[G_AREA] = area; g[G_IAREA] = inv_area; g[G_IR0] = iR0; g[G_ALPHA] = alpha;
+  xat(X, d_own) = D;
 }
 
 template <int MODEL, bool VARLOSS, class Xc>
-AFS_HD inline void seg_block1(Xc &x, double *X, const Uni &U, const Consts &T, const SegConsts &C, double ratio) {
+AFS_HD inline void seg_block1(Xc &x, double *X, const Uni &U, const SegHot &T, const SegConsts &C, double ratio) {
   using namespace tree;
   const Hot &h = T.h;
   const afs_options &opt = U.opt;
@@ -280,7 +288,15 @@ AFS_HD inline void seg_block1(Xc &x, double *X, const Uni &U, const Consts &T, c
   const double open = r1 * X[SX_FRAME + 2] + ratio * X[SX_FRAME + 3];
   x.par([&](int gl, SegLane &R) {
 #pragma unroll
-    for (int j = 0; j < NDS; ++j) seg_section(R, j, C.dyn[gl][j], U, T, C, r1, ratio, open, su, X);
+    for (int j = 0; j < PD; ++j) seg_section(R, j, C.dyn[gl][j], U, T, C, r1, ratio, open, su, X);
+    {  // the fold's static section (84): beta from its wall state, D; the rest are table constants
+      const double *fk = C.dl[gl].fk;
+      const double v = fk[FK_ALPHA] * (R.w[FOLD] * fk[FK_K1] + R.wr[FOLD] * fk[FK_K2] + R.wr2[FOLD] * fk[FK_K3]);
+      const double beta = opt.soft_walls ? v : 0.0;
+      const double D = R.p[FOLD] + h.dtTH1 * R.pr[FOLD] - fk[FK_E] * (beta - 0.0);
+      R.k.fD = D;
+      xat(X, C.dyn[gl][FOLD].d_own) = D;
+    }
     // static slots: beta from the wall state, D (the other terms are table constants)
     const StatLane &S = C.st[gl];
 #pragma unroll
@@ -289,14 +305,12 @@ AFS_HD inline void seg_block1(Xc &x, double *X, const Uni &U, const Consts &T, c
       const double v = s.c[SC_ALPHA] * (R.sw[j] * s.c[SC_K1] + R.swr[j] * s.c[SC_K2] + R.swr2[j] * s.c[SC_K3]);
       const double beta = opt.soft_walls ? v : 0.0;
       const double D = R.sp[j] + h.dtTH1 * R.spr[j] - s.c[SC_E] * (beta - 0.0);
-      R.k.sbe[j] = beta;
-      R.k.sD[j] = D;
       xat(X, s.d_own) = D;
       xat(X, s.g_d) = D;  // (section 22's source block)
     }
     // the dipoles of the slots: targets in the reference's store order, the 40 Hz smoother
 #pragma unroll
-    for (int j = 0; j < NDS; ++j) {
+    for (int j = 0; j < PD; ++j) {
       const uint32_t d = C.dyn[gl][j].dip;  // 0xff: none (never targeted, never active)
       double tgt = 0.0, cut = 0.0;
 #pragma unroll
@@ -370,13 +384,13 @@ AFS_HD inline void seg_rng_block(Xc &x, uint32_t *g, uint32_t *sink, int head, b
 }
 
 template <class Xc>
-AFS_HD inline void seg_noise(Xc &x, double *X, const Consts &T, const SegConsts &C) {
+AFS_HD inline void seg_noise(Xc &x, double *X, const SegHot &T, const SegConsts &C) {
   using namespace tree;
   constexpr int RNG_BLOCK = 30;
   const uint64_t act = x.or64([&](int gl, SegLane &R) {
     uint64_t m = 0;
 #pragma unroll
-    for (int j = 0; j < NDS; ++j) {
+    for (int j = 0; j < PD; ++j) {
       const uint32_t d = C.dyn[gl][j].dip;
       m |= (d < (uint32_t)NDIP && !(R.damp[j] < THR)) ? (1ull << (d & 63u)) : 0ull;
     }
@@ -385,7 +399,7 @@ AFS_HD inline void seg_noise(Xc &x, double *X, const Consts &T, const SegConsts 
   if (act == 0) {
     x.par([&](int, SegLane &R) {
 #pragma unroll
-      for (int j = 0; j < NDS; ++j) R.k.smp[j] = 0.0;
+      for (int j = 0; j < PD; ++j) R.k.smp[j] = 0.0;
     });
     return;
   }
@@ -396,7 +410,7 @@ AFS_HD inline void seg_noise(Xc &x, double *X, const Consts &T, const SegConsts 
   auto consume = [&](int lo, int hi) {
     x.par([&](int gl, SegLane &R) {
 #pragma unroll
-      for (int j = 0; j < NDS; ++j) {
+      for (int j = 0; j < PD; ++j) {
         const uint32_t d = C.dyn[gl][j].dip;
         const uint32_t dd = d & 63u;
         const bool on = d < (uint32_t)NDIP && ((act >> dd) & 1);
@@ -429,7 +443,7 @@ AFS_HD inline void seg_noise(Xc &x, double *X, const Consts &T, const SegConsts 
                 });
   x.par([&](int gl, SegLane &R) {
 #pragma unroll
-    for (int j = 0; j < NDS; ++j) {
+    for (int j = 0; j < PD; ++j) {
       const uint32_t d = C.dyn[gl][j].dip;
       const bool on = d < (uint32_t)NDIP && ((act >> (d & 63u)) & 1);
       double xi = (double)(int32_t)R.racc[j];
@@ -469,8 +483,9 @@ AFS_HD inline void seg_rng_ahead(Xc &x, double *X) {
 // Rows (calcMatrix, TdsModel.cpp:1785-2039) as the SPD matrix A = -M, y = -rhs.
 // ---------------------------------------------------------------------------
 // The dynamic slots: pivot, rhs, the own and source sections' E, the edge to a bifurcation
-// partner (E_a + L_a / (dt theta) + R1_a).
-AFS_HD inline void seg_rows_dyn(int gl, SegLane &R, const double *X, const Uni &U, const Consts &T,
+// partner (E_a + L_a / (dt theta) + R1_a).  Slots 0..3 read their own section's terms back from
+// its SX_G block; the fold's section (84) is a static one (DynLane::fk, D from block 1).
+AFS_HD inline void seg_rows_dyn(int gl, SegLane &R, const double *X, const Uni &U, const SegHot &T,
                                 const SegConsts &C) {
   const Hot &h = T.h;
   const afs_options &opt = U.opt;
@@ -478,23 +493,34 @@ AFS_HD inline void seg_rows_dyn(int gl, SegLane &R, const double *X, const Uni &
   SegWork &k = R.k;
   const double dR0g = k.gR0, dR1g = k.gR1;
   const int onb = k.gon;
-  // the source sections' blocks, every slot's loads first
+  // the source and own sections' blocks, every slot's loads first
   double sL[NDS], sR[NDS], sE[NDS], sD[NDS], sA[NDS], siR0[NDS], siA[NDS];
+  double oL[NDS], oR[NDS], oE[NDS], oD[NDS], oA[NDS], oiR0[NDS], oiA[NDS];
 #pragma unroll
   for (int j = 0; j < NDS; ++j) {
     const double *g = &xat(X, C.dyn[gl][j].g_src);
     sL[j] = g[G_L]; sR[j] = g[G_R1]; sE[j] = g[G_E]; sD[j] = g[G_D];
     sA[j] = g[G_AREA]; siR0[j] = g[G_IR0]; siA[j] = g[G_IAREA];
+    if (j < PD) {
+      const double *o = &xat(X, C.dyn[gl][j].g_own);
+      oL[j] = o[G_L]; oR[j] = o[G_R1]; oE[j] = o[G_E]; oD[j] = o[G_D];
+      oA[j] = o[G_AREA]; oiR0[j] = o[G_IR0]; oiA[j] = o[G_IAREA];
+    }
   }
-  // bifurcation partners (slot 4 <-> 2 or 0; seg_tables.cpp checks the pattern)
-  const bool p40 = C.dyn[gl][FOLD].partner == 0;
+  {  // the fold's section: table constants (no Bernoulli pair, no junction term)
+    const double *fk = C.dl[gl].fk;
+    oL[FOLD] = fk[FK_L]; oR[FOLD] = fk[FK_R0]; oE[FOLD] = fk[FK_E]; oD[FOLD] = k.fD;
+    oA[FOLD] = 1.0; oiR0[FOLD] = 0.0; oiA[FOLD] = 0.0;
+  }
+  // bifurcation partners (seg_tables.cpp checks the pattern: slot 4 <-> 2 or 0, slot 2 <-> 4 or 3)
+  const bool p40 = C.dyn[gl][FOLD].partner == 0, p23 = C.dyn[gl][2].partner == 3;
   double uD[NDS], uDr[NDS];
   uD[0] = R.u[4]; uDr[0] = R.ur[4];
   uD[1] = 0.0; uDr[1] = 0.0;
-  uD[2] = R.u[4]; uDr[2] = R.ur[4];
-  uD[3] = 0.0; uDr[3] = 0.0;
+  uD[2] = p23 ? R.u[3] : R.u[4]; uDr[2] = p23 ? R.ur[3] : R.ur[4];
+  uD[3] = R.u[2]; uDr[3] = R.ur[2];
   uD[4] = p40 ? R.u[0] : R.u[2]; uDr[4] = p40 ? R.ur[0] : R.ur[2];
-  const double lips = k.smp[FOLD];
+  const double lips = k.smp[0];  // (the lips dipole rides on slot 0 of arm B's first lane)
 #pragma unroll
   for (int j = 0; j < NDS; ++j) {
     const DynSlot &d = C.dyn[gl][j];
@@ -503,40 +529,41 @@ AFS_HD inline void seg_rows_dyn(int gl, SegLane &R, const double *X, const Uni &
     const double La = sL[j], Ea = sE[j], Da = sD[j];
     const double u = R.u[j], ur = R.ur[j];
     double RA = sR[j];
-    double RB = sec ? k.R[j] : 0.0;
+    double RB = sec ? oR[j] : 0.0;
     // Bernoulli pair (source, own section) (TdsModel.cpp:850-877): R1 of the source, R0 of the own
     {
-      const double Aa = sA[j], Ab = k.A[j];
+      const double Aa = sA[j], Ab = oA[j];
       const bool c = ((Ab < Aa) & (u > 0)) | ((Ab > Aa) & (u < 0));
       const bool on = (opt.turbulence_losses != 0) & ((f & DF_BERN) != 0) & c;
-      const double ta = u * (0.5 * RHO) * (siA[j] * siA[j]), tb = u * (0.5 * RHO) * (k.iA[j] * k.iA[j]);
+      const double ta = u * (0.5 * RHO) * (siA[j] * siA[j]), tb = u * (0.5 * RHO) * (oiA[j] * oiA[j]);
       RA = on ? RA - ta : RA;
       RB = on ? RB + tb : RB;
     }
     RB = ((f & DF_GLOT_R0) && (onb & 1)) ? RB + dR0g : RB;
     RA = ((f & DF_GLOT_R1) && (onb & 2)) ? RA + dR1g : RA;
     RB = ((f & DF_FOSSA) && !opt.piriform_fossa) ? h.fossa_R0 : RB;
-    double LB = sec ? k.L[j] : 0.0;
+    double LB = sec ? oL[j] : 0.0;
     LB = (f & DF_RAD_L) ? k.lrad : LB;
     RB = (f & DF_RAD_R) ? k.rrad : RB;
     double LAB = La + LB;
-    {  // getJunctionInductance (TdsModel.cpp:1745-1778): 8 rho H / (3 pi^2 b), H = 1 - b / a with
-       // a, b the larger and smaller radius = 8 rho / (3 pi^2) |1/r_a - 1/r_b|
-      const double jl = (8.0 * RHO / (3.0 * PI * PI)) * fabs(siR0[j] - k.iR0[j]);
+    if (j < PD) {  // getJunctionInductance (TdsModel.cpp:1745-1778): 8 rho H / (3 pi^2 b), H = 1 - b / a
+                   // with a, b the larger and smaller radius = 8 rho / (3 pi^2) |1/r_a - 1/r_b|
+      const double jl = (8.0 * RHO / (3.0 * PI * PI)) * fabs(siR0[j] - oiR0[j]);
       const bool use = (opt.inner_length_corrections != 0) & ((f & DF_JL) != 0);
       LAB = use ? LAB + jl : LAB;
     }
     const double RAB = RA + RB;
-    const double EB = sec ? k.E[j] : 0.0, DB = sec ? k.D[j] : 0.0;
+    const double EB = sec ? oE[j] : 0.0, DB = sec ? oD[j] : 0.0;
     const bool par = (f & (DF_BIF | DF_RAD_R | DF_RAD_L)) != 0;
     const double pu = par ? uD[j] : 0.0, pur = par ? uDr[j] : 0.0;
-    const double S = -(((f & (DF_RAD_R | DF_RAD_L)) != 0) ? lips : k.smp[j]);
+    const double S = -(((f & (DF_RAD_R | DF_RAD_L)) != 0) ? lips : (j < PD ? k.smp[j < PD ? j : 0] : 0.0));
     const double H = -idt * (LAB * u + La * pu) - (TH1 / TH) * (LAB * ur + La * pur) + S;
     const double diag = EB + Ea + (LAB * idt + RAB);
     const double rhs = H + DB - Da;
     const bool cur = (f & DF_CUR) != 0;
     k.Dp[j] = cur ? diag : 1.0;
     k.Yp[j] = cur ? -rhs : 0.0;
+    k.E[j] = EB;
     k.Ea[j] = Ea;
     k.ebr[j] = Ea + (La * idt + RA);
   }
@@ -546,9 +573,12 @@ AFS_HD inline void seg_rows_dyn(int gl, SegLane &R, const double *X, const Uni &
 AFS_HD inline void seg_rows_static(int gl, SegLane &R, const double *X, const SegConsts &C, double lung,
                                    double lips) {
   const StatLane &S = C.st[gl];
-  double Da[NSS];
+  double Da[NSS], Db[NSS];
 #pragma unroll
-  for (int j = 0; j < NSS; ++j) Da[j] = xat(X, S.s[j].d_src);
+  for (int j = 0; j < NSS; ++j) {
+    Da[j] = xat(X, S.s[j].d_src);
+    Db[j] = xat(X, S.s[j].d_own);
+  }
   // partners: slots 0 <-> 3, 1 <-> 4 (seg_tables.cpp checks the pattern)
   const double uD[NSS] = {R.su[3], R.su[4], 0.0, R.su[0], R.su[1]};
   const double uDr[NSS] = {R.sur[3], R.sur[4], 0.0, R.sur[0], R.sur[1]};
@@ -558,7 +588,7 @@ AFS_HD inline void seg_rows_static(int gl, SegLane &R, const double *X, const Se
     const uint16_t f = s.flags;
     const double S0 = (f & SF_LUNG) ? -lung : (f & SF_LIPS) ? -lips : 0.0;
     const double H = -(s.c[SC_CU] * R.su[j] + s.c[SC_CUD] * uD[j]) - (s.c[SC_CUR] * R.sur[j] + s.c[SC_CUDR] * uDr[j]) + S0;
-    const double DB = (f & SF_SEC) ? R.k.sD[j] : 0.0;
+    const double DB = (f & SF_SEC) ? Db[j] : 0.0;
     const double rhs = H + DB - Da[j];
     R.k.sy[j] = (f & SF_CUR) ? -rhs : 0.0;
   }
@@ -753,11 +783,11 @@ AFS_HD inline void seg_solve(Xc &x, const SegConsts &C) {
     R.k.jy[0] = R.k.Yp[0];
     R.k.jd[1] = R.k.Dp[2];
     R.k.jy[1] = R.k.Yp[2];
-    R.k.jd[2] = R.k.Dp[FOLD];
-    R.k.jy[2] = R.k.Yp[FOLD];
+    R.k.jd[2] = R.k.Dp[3];
+    R.k.jy[2] = R.k.Yp[3];
   });
   // the junction lane takes the arms' last boundaries: 38 -> 39 (slot 0), 42 -> 41 (slot 2),
-  // 66 -> 65 (the fold slot)
+  // 66 -> 65 (slot 3)
   auto give = [&](int, SegLane &R) { return D4{{R.k.binv, R.k.Yb, R.k.ej, 0.0}}; };
   auto take = [&](int q) {
     return [&, q](int, SegLane &R, const D4 &v) {
@@ -831,7 +861,7 @@ AFS_HD inline void seg_solve(Xc &x, const SegConsts &C) {
                              R.k.xs[0] = R.k.jd[0];
                              R.k.xs[1] = R.k.jd[1];
                              R.k.xs[2] = R.k.jd[2];
-                             R.k.xs[FOLD] = R.k.jy[0];
+                             R.k.xs[3] = R.k.jy[0];
                            }
 #pragma unroll
                            for (int j = 0; j < NDS; ++j) R.k.xs[j] = bad ? NAN : R.k.xs[j];
@@ -861,27 +891,46 @@ AFS_HD inline void seg_publish_x(int gl, SegLane &R, double *X, const SegConsts 
 }
 
 AFS_HD inline void seg_update(int gl, SegLane &R, const double *__restrict__ X, double *__restrict__ Xw, const Uni &U,
-                              const Consts &T, const SegConsts &C) {
+                              const SegHot &T, const SegConsts &C) {
   const double c = T.h.noise_lp_c, idt = T.h.inv_dtTH;
-  double o0[NDS], o1[NDS], so0[NSS], so1[NSS];
+  // every slot's loads first: the output flows, the section's D, E, alpha (block 1, LDS)
+  double o0[NDS], o1[NDS], dD[NDS], dE[NDS], dal[NDS], so0[NSS], so1[NSS], sD[NSS];
+  double unold[NDS], unew[NDS];
 #pragma unroll
   for (int j = 0; j < NDS; ++j) {
-    o0[j] = xat(X, C.dyn[gl][j].out0);
-    o1[j] = xat(X, C.dyn[gl][j].out1);
+    const DynSlot &d = C.dyn[gl][j];
+    o0[j] = xat(X, d.out0);
+    o1[j] = xat(X, d.out1);
+    unold[j] = xat(X, d.un_pub);
+    if (j < PD) {
+      const double *g = &xat(X, d.g_own);
+      dD[j] = g[G_D];
+      dE[j] = g[G_E];
+      dal[j] = g[G_ALPHA];
+    }
   }
+  const double *fk = C.dl[gl].fk;
+  dD[FOLD] = R.k.fD;
+  dE[FOLD] = fk[FK_E];
+  dal[FOLD] = U.opt.soft_walls ? fk[FK_ALPHA] : 0.0;
 #pragma unroll
   for (int j = 0; j < NSS; ++j) {
     so0[j] = xat(X, C.st[gl].s[j].out0);
     so1[j] = xat(X, C.st[gl].s[j].out1);
+    sD[j] = xat(X, C.st[gl].s[j].d_own);
   }
-  (void)U;
 #pragma unroll
   for (int j = 0; j < NDS; ++j) {
+    // beta of block 1 again, from the wall state before this update
+    const bool walls = U.opt.soft_walls && (C.dyn[gl][j].flags & DF_WALLS);
+    const double bd = fma(R.w[j], C.nk[NK_K1], fma(R.wr[j], C.nk[NK_K2], R.wr2[j] * C.nk[NK_K3]));
+    const double bf = fk[FK_ALPHA] * (R.w[j] * fk[FK_K1] + R.wr[j] * fk[FK_K2] + R.wr2[j] * fk[FK_K3]);
+    const double beta = walls ? (j < PD ? bd : bf) : 0.0;
     const double un = R.k.xs[j];
     const double uold = R.u[j];
     R.u[j] = un;
     R.ur[j] = (un - uold) * idt - (TH1 / TH) * R.ur[j];
-    R.un[j] = (1.0 - c) * un + c * R.un[j];
+    unew[j] = (1.0 - c) * un + c * unold[j];
     double cout = 0.0;
     cout += o0[j];
     cout += o1[j];
@@ -889,12 +938,12 @@ AFS_HD inline void seg_update(int gl, SegLane &R, const double *__restrict__ X, 
     cin += un;
     const double net = cin - cout;
     const double old = R.p[j];
-    const double p = R.k.D[j] + R.k.E[j] * net;
+    const double p = dD[j] + dE[j] * net;
     R.p[j] = p;
     const double prr = (p - old) * idt - R.pr[j] * (TH1 / TH);
     R.pr[j] = prr;
     const double ow = R.w[j], owr = R.wr[j];
-    const double w = prr * R.k.al[j] + R.k.be[j];
+    const double w = prr * dal[j] + beta;
     R.w[j] = w;
     const double wr = (w - ow) * idt - owr * (TH1 / TH);
     R.wr[j] = wr;
@@ -903,6 +952,8 @@ AFS_HD inline void seg_update(int gl, SegLane &R, const double *__restrict__ X, 
 #pragma unroll
   for (int j = 0; j < NSS; ++j) {
     const StatSlot &s = C.st[gl].s[j];
+    const double v = s.c[SC_ALPHA] * (R.sw[j] * s.c[SC_K1] + R.swr[j] * s.c[SC_K2] + R.swr2[j] * s.c[SC_K3]);
+    const double beta = U.opt.soft_walls ? v : 0.0;  // (block 1's)
     const double un = R.k.sx[j];
     const double uold = R.su[j];
     R.su[j] = un;
@@ -914,12 +965,12 @@ AFS_HD inline void seg_update(int gl, SegLane &R, const double *__restrict__ X, 
     cin += un;
     const double net = cin - cout;
     const double old = R.sp[j];
-    const double p = R.k.sD[j] + s.c[SC_E] * net;
+    const double p = sD[j] + s.c[SC_E] * net;
     R.sp[j] = p;
     const double prr = (p - old) * idt - R.spr[j] * (TH1 / TH);
     R.spr[j] = prr;
     const double ow = R.sw[j], owr = R.swr[j];
-    const double w = prr * s.c[SC_ALPHA] + R.k.sbe[j];
+    const double w = prr * s.c[SC_ALPHA] + beta;
     R.sw[j] = w;
     const double wr = (w - ow) * idt - owr * (TH1 / TH);
     R.swr[j] = wr;
@@ -928,7 +979,7 @@ AFS_HD inline void seg_update(int gl, SegLane &R, const double *__restrict__ X, 
   // publish: noise-smoothed flows (the constriction phase), p[22..25], p[43], p[67]
 #pragma unroll
   for (int j = 0; j < NDS; ++j) {
-    xat(Xw, C.dyn[gl][j].un_pub) = R.un[j];
+    xat(Xw, C.dyn[gl][j].un_pub) = unew[j];
     xat(Xw, C.dyn[gl][j].p_pub) = R.p[j];
   }
 #pragma unroll
@@ -936,7 +987,7 @@ AFS_HD inline void seg_update(int gl, SegLane &R, const double *__restrict__ X, 
 }
 
 // The output stage (Synthesizer.cpp:614-627) as tree_core.h's, on this layout.
-AFS_HD inline double seg_output_filter_one(double *X, const Consts &T, double flow) {
+AFS_HD inline double seg_output_filter_one(double *X, const SegHot &T, double flow) {
   double op = (flow - X[SX_PREVFLOW]) * T.h.inv_dt;
   X[SX_PREVFLOW] = flow;
   double y = tree::iir_run<8>(X + SX_OUTF, T.h.out_a, T.h.out_b, op);
@@ -946,7 +997,7 @@ AFS_HD inline double seg_output_filter_one(double *X, const Consts &T, double fl
   return smp;
 }
 
-AFS_HD inline void seg_output_filter_run(double *X, const Consts &T, double *o, int n) {
+AFS_HD inline void seg_output_filter_run(double *X, const SegHot &T, double *o, int n) {
   double sx[8], sy[8], ca[9], cb[9];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { sx[k] = X[SX_OUTF + k]; sy[k] = X[SX_OUTF + 8 + k]; }
@@ -995,7 +1046,7 @@ AFS_HD inline void seg_output_filter_run(double *X, const Consts &T, double *o, 
 // One audio sample.
 // ---------------------------------------------------------------------------
 template <int MODEL, class Xc>
-AFS_HD inline void seg_sample_step(Xc &x, double *X, const Uni &U, const Consts &T, const SegConsts &C, double ratio,
+AFS_HD inline void seg_sample_step(Xc &x, double *X, const Uni &U, const SegHot &T, const SegConsts &C, double ratio,
                                    bool defer_out) {
   if (U.opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE) seg_block1<MODEL, true>(x, X, U, T, C, ratio);
   else seg_block1<MODEL, false>(x, X, U, T, C, ratio);
@@ -1006,13 +1057,13 @@ AFS_HD inline void seg_sample_step(Xc &x, double *X, const Uni &U, const Consts 
   } else {
     x.par([&](int, SegLane &R) {
 #pragma unroll
-      for (int j = 0; j < NDS; ++j) R.k.smp[j] = 0.0;
+      for (int j = 0; j < PD; ++j) R.k.smp[j] = 0.0;
     });
   }
   x.mark(1);
   const double lung = X[SX_GP + 1];
-  // the lips sample for the nostril radiation rows: slot FOLD of arm B's first lane
-  x.template bcast<4, 1>([&](int, SegLane &R) { return D4{{R.k.smp[FOLD], 0.0, 0.0, 0.0}}; },
+  // the lips sample for the nostril radiation rows: slot 0 of arm B's first lane
+  x.template bcast<4, 1>([&](int, SegLane &R) { return D4{{R.k.smp[0], 0.0, 0.0, 0.0}}; },
                          [&](int gl, SegLane &R, const D4 &v) {
                            seg_rows_dyn(gl, R, X, U, T, C);
                            seg_rows_static(gl, R, X, C, lung, v.v[0]);

@@ -107,6 +107,7 @@ struct SegGpuExec {
 };
 
 struct SegWaveLds {
+  SegHot H;
   SegConsts C;
   double X[UPB][SX_STRIDE];
 };
@@ -121,10 +122,14 @@ __device__ __forceinline__ void seg_synth_body(const SegArgs &sa, SegWaveLds &ld
   const int ue = valid ? u : 0;
   double *X = lds.X[g];
   const Tables &T = *a.tab;
-  {  // stage the lane records (8-byte words)
+  {  // stage the lane records and the scalars (8-byte words)
     const uint64_t *src = (const uint64_t *)&sa.seg->c;
     uint64_t *dst = (uint64_t *)&lds.C;
     for (int k = lane; k < (int)(sizeof(SegConsts) / 8); k += 64 * WPB) dst[k] = src[k];
+    const uint64_t *hs = (const uint64_t *)&T.consts.h;
+    uint64_t *hd = (uint64_t *)&lds.H.h;
+    static_assert(sizeof(Hot) % 8 == 0, "Hot: 8-byte words");
+    for (int k = lane; k < (int)(sizeof(Hot) / 8); k += 64 * WPB) hd[k] = hs[k];
   }
   SegLane R = ((const SegLane *)a.lane_state)[(int64_t)ue * SW + gl];
   const double *ls = a.lds_state + (int64_t)ue * SX_TOTAL;
@@ -150,10 +155,18 @@ __device__ __forceinline__ void seg_synth_body(const SegArgs &sa, SegWaveLds &ld
     R.planw = next;
     next = pl[(t + 1 < n ? t + 1 : t) * tree::PLAN_WORDS];  // the next sample's word, a sample ahead
     const double ratio = (double)i / (double)hop;
-    seg_sample_step<MODEL>(ex, X, a.uni, T.consts, C, ratio, defer);
+#if defined(AFS_SEG_OPAQUE)
+    // (the tables' addresses opaque per sample: their loads stay in the loop instead of holding
+    // registers for the whole launch)
+    const SegConsts *cp = &C;
+    __asm__ volatile("" : "+s"(cp));
+    seg_sample_step<MODEL>(ex, X, a.uni, lds.H, *cp, ratio, defer);
+#else
+    seg_sample_step<MODEL>(ex, X, a.uni, lds.H, C, ratio, defer);
+#endif
     if (valid && gl == 0) o[t] = R.sample;
     if (++i == hop) {
-      if (defer && valid && gl == 0) seg_output_filter_run(X, T.consts, o + t0, (int)(t + 1 - t0));
+      if (defer && valid && gl == 0) seg_output_filter_run(X, lds.H, o + t0, (int)(t + 1 - t0));
       t0 = t + 1;
       i = 0;
       ++k;
@@ -161,7 +174,7 @@ __device__ __forceinline__ void seg_synth_body(const SegArgs &sa, SegWaveLds &ld
       ex.sync();
     }
   }
-  if (defer && valid && gl == 0 && t0 < n) seg_output_filter_run(X, T.consts, o + t0, (int)(n - t0));
+  if (defer && valid && gl == 0 && t0 < n) seg_output_filter_run(X, lds.H, o + t0, (int)(n - t0));
   ex.sync();
   if (valid) {
     R.k = SegWork{};  // (per-sample values carry nothing to the next launch)

@@ -12,7 +12,8 @@
 //      arm B  [93 64 63 62]+94 [61 60 59 58] [57 56 55 54] [53 52 51 50] [49 48 47 46] [45 44 43 42]
 //      arm C  [69 68 67 66]                                                       (descending)
 //      junction lane [39 40 41 65]
-//    (84 is folded on 28/29, 94 on 93/64); a lane walks its four positions in registers, the
+//    (84 is folded on 28/29, 94 on 93/64: the fold slot has no interpolated geometry -- 84 is a
+//    static section, 94 a radiation current); a lane walks its four positions in registers, the
 //    boundaries are reduced lane to lane toward the junction by DPP, the junction lane solves
 //    its four nodes, the solutions flow back;
 //  * static part (the 47 currents whose two sections are static: trachea 0..22, nose 70..83
@@ -57,8 +58,9 @@ enum : int {
   SX_UN_SINK = SX_UN + NC,
   SX_D = SX_UN_SINK + 1,           // D of every section, zero, sink
   SX_D_ZERO = SX_D + NS, SX_D_SINK = SX_D_ZERO + 1,
-  SX_G = SX_D_SINK + 1,            // sources of the dynamic rows: sections 22..68, 8 doubles each
-  NG = 47, G0 = 22,                //   (L, R1, E, D, area, 1/area, 1/r0, -), then a zero and a sink block
+  SX_G = SX_D_SINK + 1,            // the section terms of the dynamic rows' sections: 22..69 and 84,
+  NG = 49, G0 = 22,                //   8 doubles each (L, R1, E, D, area, 1/area, 1/r0, alpha), then a
+                                   //   zero and a sink block
   SX_G_ZERO = SX_G + 8 * NG, SX_G_SINK = SX_G_ZERO + 8,
   SX_P4 = SX_G_SINK + 8,           // p[22..25] after the update (glottis inputs)
   SX_TVP = SX_P4 + 4,              // p[43], p[67] (transvelar filter inputs)
@@ -75,12 +77,17 @@ enum : int {
   SX_TGLOT = SX_GP + 8,            // transglottal-pressure filter (variable entrance loss)
   SX_TVEL = SX_TGLOT + 8,          // transvelar coupling filters
   SX_ACT = SX_TVEL + 16,           // scratch / sinks of the noise phases (16)
-  SX_TOTAL = SX_ACT + 16,
+  SX_FC = SX_ACT + 16,             // frame cache of the pharynx/mouth sections: aL, aR, lL, lR (40 x 4)
+  SX_TOTAL = SX_FC + 4 * NPM,
   SX_STRIDE = SX_TOTAL + ((16 - SX_TOTAL % 32) + 32) % 32
 };
 static_assert(SX_STRIDE % 32 == 16, "utterance blocks offset by half a bank row");
 static_assert(SX_G % 2 == 0, "16-byte aligned source blocks");
-constexpr int GB = 8, G_L = 0, G_R1 = 1, G_E = 2, G_D = 3, G_AREA = 4, G_IAREA = 5, G_IR0 = 6;
+constexpr int GB = 8, G_L = 0, G_R1 = 1, G_E = 2, G_D = 3, G_AREA = 4, G_IAREA = 5, G_IR0 = 6, G_ALPHA = 7;
+// the SX_G block of section s (-1: none)
+AFS_HD constexpr int g_block(int s) {
+  return (s >= G0 && s <= G0 + 47) ? SX_G + GB * (s - G0) : s == S_FOSSA0 ? SX_G + GB * 48 : -1;
+}
 
 // ---- dynamic slot records ------------------------------------------------------------------
 // Where a slot's section area and length come from.
@@ -130,6 +137,8 @@ enum : uint8_t {
   WF_ARM = 16,       // an arm lane (walk, reduction)
   WF_FOLD_P0 = 32    // the fold's bifurcation partner is position q (else q + 1)
 };
+// the fold slot's section constants (a static section: 84; zeros for 94)
+enum : int { FK_L, FK_R0, FK_R1, FK_E, FK_ALPHA, FK_K1, FK_K2, FK_K3, FK_N };
 struct alignas(16) DynLane {
   uint8_t wf;        // WF_*
   uint8_t idx;       // position of the lane in its arm (0 = far end)
@@ -138,8 +147,9 @@ struct alignas(16) DynLane {
   uint8_t pad[3];
   double delta0, e0;   // position 0's attach: constant pivot term, edge to the subtree root
   double deltaf, ef;   // the fold's
+  double fk[FK_N];     // the fold's section (L, R0, R1, E, alpha, wall coefficients)
 };
-static_assert(sizeof(DynLane) == 48, "DynLane: 48 bytes");
+static_assert(sizeof(DynLane) == 112, "DynLane: 112 bytes");
 
 // ---- static lanes -----------------------------------------------------------------------------
 enum : uint16_t {
@@ -193,6 +203,11 @@ struct SegConsts {
   DynLane dl[SW];
   StatLane st[SW];
   double nk[NK_N];
+};
+
+// The time loop's scalars (a copy of Tables::consts.h), staged in LDS next to the lane records.
+struct SegHot {
+  Hot h;
 };
 
 struct SegTables {

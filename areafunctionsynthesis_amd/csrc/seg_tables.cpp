@@ -25,7 +25,7 @@ const int DYN[SW][NDS] = {
     {93, 64, 63, 62, 94}, {61, 60, 59, 58, -1}, {57, 56, 55, 54, -1}, {53, 52, 51, 50, -1},
     {49, 48, 47, 46, -1}, {45, 44, 43, 42, -1},
     {69, 68, 67, 66, -1},
-    {39, 40, 41, -1, 65},  // junction lane (no walk): 65 in the fold slot, partner of 41
+    {39, 40, 41, 65, -1},  // junction lane (no walk)
     {-1, -1, -1, -1, -1}, {-1, -1, -1, -1, -1}, {-1, -1, -1, -1, -1}, {-1, -1, -1, -1, -1}};
 const int ARM[SW] = {0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 2, -1, -1, -1, -1, -1};
 const int FOLD_Q[SW] = {0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -51,7 +51,6 @@ void build_seg_tables(const Tables &t, SegTables *out) {
   const double idt = 1.0 / (t.dt * TH);
   auto dyn_sec = [](int s) { return s >= 23 && s <= 68; };
   auto pm = [](int s) { return s >= S_PHARYNX0 && s <= S_LAST_MOUTH; };
-  auto g_block = [](int s) { return (s >= G0 && s < G0 + NG) ? SX_G + GB * (s - G0) : -1; };
   const uint16_t U_ZERO = off(SX_U_ZERO), U_SINK = off(SX_U_SINK), D_ZERO = off(SX_D_ZERO),
                  D_SINK = off(SX_D_SINK), G_ZERO = off(SX_G_ZERO), G_SINK = off(SX_G_SINK), UN_SINK = off(SX_UN_SINK);
   auto p_slot = [&](int s) -> uint16_t {
@@ -82,7 +81,7 @@ void build_seg_tables(const Tables &t, SegTables *out) {
       d.u_pub = off(SX_U + c);
       d.un_pub = off(SX_UN + c);
       const int a = t.src[c];
-      if (a < 0 || g_block(a) < 0) { ok = false; continue; }  // every dynamic row has a source in 22..68
+      if (a < 0 || g_block(a) < 0) { ok = false; continue; }  // every dynamic row's source has a block
       d.g_src = off(g_block(a));
       const bool two = t.cout0[a] >= 0 && t.cout1[a] >= 0;
       if (c >= NS) {  // radiation current of section 64
@@ -91,7 +90,9 @@ void build_seg_tables(const Tables &t, SegTables *out) {
         const int s = c;
         d.flags |= DF_SEC;
         d.d_own = off(SX_D + s);
-        if (g_block(s) >= 0) d.g_own = off(g_block(s));
+        if (g_block(s) < 0) ok = false;  // every dynamic slot's section has a block
+        else d.g_own = off(g_block(s));
+        if (j == FOLD && s != S_FOSSA0) ok = false;  // (the fold's static-section path: 84 only)
         d.out0 = t.cout0[s] >= 0 ? off(SX_U + t.cout0[s]) : U_ZERO;
         d.out1 = t.cout1[s] >= 0 ? off(SX_U + t.cout1[s]) : U_ZERO;
         d.p_pub = p_slot(s);
@@ -135,13 +136,33 @@ void build_seg_tables(const Tables &t, SegTables *out) {
       for (int q = 0; q < NDS; ++q)
         if (DYN[k][q] == br) d.partner = (uint8_t)q;
       if (d.partner == 0xff) ok = false;
-      // the kernel's partner pattern: slot 4 <-> 2 or 0, slot 0 <-> 4, slot 2 <-> 4
-      if (!((j == 4 && (d.partner == 2 || d.partner == 0)) || (j == 0 && d.partner == 4) || (j == 2 && d.partner == 4)))
+      // the kernel's partner pattern: slot 4 <-> 2 or 0, slot 2 <-> 4 or 3
+      if (!((j == 4 && (d.partner == 2 || d.partner == 0)) || (j == 0 && d.partner == 4) ||
+            (j == 2 && (d.partner == 4 || d.partner == 3)) || (j == 3 && d.partner == 2)))
         ok = false;
     }
-    if (DYN[k][FOLD] == 94) {
-      C.dyn[k][FOLD].flags |= DF_LIPS;
-      C.dyn[k][FOLD].dip = (uint8_t)DIP_LIPS;
+    if (DYN[k][0] == 93) {  // the lips dipole rides on slot 0 (93 has no section, no dipole of its own)
+      C.dyn[k][0].flags |= DF_LIPS;
+      C.dyn[k][0].dip = (uint8_t)DIP_LIPS;
+    }
+    // the fold slot carries no interpolated section: a static section (84) from the tables, or none
+    {
+      const int f = DYN[k][FOLD];
+      DynLane &Lf = C.dl[k];
+      for (int q = 0; q < FK_N; ++q) Lf.fk[q] = 0.0;
+      if (f >= 0 && f < NS) {
+        if (!is_static_section(f)) ok = false;
+        Lf.fk[FK_L] = t.L[f];
+        Lf.fk[FK_R0] = t.R[f];
+        Lf.fk[FK_R1] = t.R[f];
+        Lf.fk[FK_E] = t.E[f];
+        Lf.fk[FK_ALPHA] = t.alpha[f];
+        Lf.fk[FK_K1] = t.wc1[f];
+        Lf.fk[FK_K2] = t.wc2[f];
+        Lf.fk[FK_K3] = t.Lw[f] * TH1_TH;
+        C.dyn[k][FOLD].g_own = G_SINK;  // (nothing reads its block)
+      }
+      if (f >= 0 && C.dyn[k][FOLD].dip != 0xff) ok = false;
     }
     // lane record
     DynLane &L = C.dl[k];
@@ -174,7 +195,7 @@ void build_seg_tables(const Tables &t, SegTables *out) {
   // roles fixed in the kernel
   if (!(C.dl[ARM_A_END].wf & WF_END) || !(C.dl[ARM_B_END].wf & WF_END) || !(C.dl[ARM_C_END].wf & WF_END)) ok = false;
   if (DYN[JUNCTION_LANE][0] != 39 || DYN[JUNCTION_LANE][1] != 40 || DYN[JUNCTION_LANE][2] != 41 ||
-      DYN[JUNCTION_LANE][FOLD] != 65 || DYN[ARM_A_END][3] != 38 || DYN[ARM_B_END][3] != 42 || DYN[ARM_C_END][3] != 66)
+      DYN[JUNCTION_LANE][3] != 65 || DYN[ARM_A_END][3] != 38 || DYN[ARM_B_END][3] != 42 || DYN[ARM_C_END][3] != 66)
     ok = false;
 
   // ---- static slots ----

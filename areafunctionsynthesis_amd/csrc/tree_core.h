@@ -296,7 +296,8 @@ struct GlotOut { double a0, a1, l0, l1; };
 // from the interpolated controls gp, the pressures p4 = p[22..25] of the previous sample and the
 // relative displacements rel (current 0/1, previous 2/3, as for the triangular glottis); the new
 // displacements go to rel_out.
-AFS_HD inline GlotOut two_mass_glottis(const Consts &C, const double *gp, const double *p4, const double *rel,
+template <class CT>
+AFS_HD inline GlotOut two_mass_glottis(const CT &C, const double *gp, const double *p4, const double *rel,
                                        double *rel_out) {
   double Q = 1.0 + (gp[0] - TM_NAT_F0) * (1.0 / TM_F0_DIV_Q);  // getTensionParameter (:467-485)
   if (Q < 0.05) Q = 0.05;
@@ -563,8 +564,8 @@ AFS_HD inline GlotIn glottis_inputs(const double *X) {
   return in;
 }
 
-template <int MODEL>
-AFS_HD inline GlotRes glottis_eval(const GlotIn &in, const Consts &C, double ratio, const double *p4) {
+template <int MODEL, class CT>
+AFS_HD inline GlotRes glottis_eval(const GlotIn &in, const CT &C, double ratio, const double *p4) {
   const double r1 = 1.0 - ratio;
   GlotRes res;
   double *gp = res.gp;

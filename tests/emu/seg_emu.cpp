@@ -76,6 +76,7 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
   seg_reset_lds(X.data(), seed);
   seg_init_lds(X.data(), S);
   SegCpuExec ex{R.data()};
+  SegHot H{T.consts.h};
   const bool defer = hop >= tree::OUT_DEFER_MIN_HOP;
   const bool two = opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
   long t = 0;
@@ -87,12 +88,12 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
       uint64_t w[tree::PLAN_WORDS];
       tree::plan_sample(frames + k - 1, frames + k, ratio, S.uo, two, w);
       for (int gl = 0; gl < SW; ++gl) R[gl].planw = w[gl % tree::PLAN_WORDS];
-      if (two) seg_sample_step<AFS_GLOTTIS_TWO_MASS>(ex, X.data(), T.uni, T.consts, S.c, ratio, defer);
-      else seg_sample_step<AFS_GLOTTIS_TRIANGULAR>(ex, X.data(), T.uni, T.consts, S.c, ratio, defer);
+      if (two) seg_sample_step<AFS_GLOTTIS_TWO_MASS>(ex, X.data(), T.uni, H, S.c, ratio, defer);
+      else seg_sample_step<AFS_GLOTTIS_TRIANGULAR>(ex, X.data(), T.uni, H, S.c, ratio, defer);
       out[t] = R[0].sample;
       ++t;
     }
-    if (defer) seg_output_filter_run(X.data(), T.consts, out + t0, hop);
+    if (defer) seg_output_filter_run(X.data(), H, out + t0, hop);
   }
   if (draws) *draws = (int64_t) * (const uint64_t *)(X.data() + SX_NDRAW);
   return t;

@@ -28,6 +28,7 @@ for s in $STEPS; do
     sq)    (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_FLOPS_FP64 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --kernel-trace --output-format csv -d $R/$OUT/pmc_sq -o run -- python3 $R/bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline) > $OUT/pmc_sq.log 2>&1; ok $? pmc_sq ;;
     calib) (cd /tmp && timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/$OUT/calib -o run -- $R/tools/microbench/fetch_calib) > $OUT/calib.log 2>&1; ok $? calib ;;
     pp)    timeout -k 10 300 python tools/phase_prof/run.py --batch 8192 --seconds 0.02 > $OUT/phase_prof.txt 2>&1; ok $? phase_prof; cat $OUT/phase_prof.txt ;;
+    spp)   timeout -k 10 300 python tools/phase_prof/seg_run.py --batch 8192 --seconds 0.02 > $OUT/seg_phase_prof.txt 2>&1; ok $? seg_phase_prof; cat $OUT/seg_phase_prof.txt ;;
   esac
 done
 echo ALL DONE
