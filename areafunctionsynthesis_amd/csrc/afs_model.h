@@ -165,6 +165,10 @@ struct Hot {
   double g_smk0, g_smk1;        // sqrt(mass * stiffness) of the two glottis masses (q-free)
   double tglot_a[5], tglot_b[5];  // transglottal-pressure Chebyshev, 50 Hz (TdsModel.cpp:474)
   double tvel2_a[5];              // transvelar coupling H2 numerator (H1 = tone_a; b = tone_b)
+  // the walls of the dynamic sections with the wall surface cancelled: alpha = surf * wall_invK,
+  // beta = wall_k1 w + wall_k2 w' + wall_k3 w'' (TdsModel.cpp:805-832); the mouth's radiation
+  // elements Rrad = rrad_c / A, Lrad = lrad_c r0 / A (:1874, :1889)
+  double wall_invK, wall_k1, wall_k2, wall_k3, rrad_c, lrad_c;
 };
 // Values that steer branches in the time loop: kernel arguments on the device, so the
 // compiler keeps them in scalar registers and branches on them uniformly.

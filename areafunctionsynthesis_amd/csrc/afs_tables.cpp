@@ -374,6 +374,17 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   h.inv_dt = 1.0 / t->dt;
   h.g_smk0 = std::sqrt(G_MASS0 * G_K0);
   h.g_smk1 = std::sqrt(G_MASS1 * G_K1);
+  {
+    const double Mw = h.Mw_ph0, Bw = h.Bw_ph0, Kw = h.Kw_ph0;
+    const double idt = 1.0 / (t->dt * TH), idt2 = 1.0 / (t->dt * t->dt * TH * TH), th = TH1 / TH;
+    const double K = Mw * idt2 + Bw * idt + Kw;
+    h.wall_invK = 1.0 / K;
+    h.wall_k1 = (Mw * idt2 + Bw * idt) / K;
+    h.wall_k2 = (Mw * (th + 1.0) * idt + Bw * th) / K;
+    h.wall_k3 = Mw * th / K;
+    h.rrad_c = t->rrad_num / (9.0 * PI * PI);
+    h.lrad_c = t->lrad_num / (3.0 * PI);
+  }
   // step records: LDS byte offsets of the tree kernel's utterance block (tree_core.h)
   using namespace tree;
   // X_UR slots: both outputs of every bifurcation (their partner reads d/dt of the flow)

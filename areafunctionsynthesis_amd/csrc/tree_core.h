@@ -69,7 +69,7 @@ enum : int {
   // X_D has a sink at NS)
   X_E = X_P4 + 4, X_D = X_E + NDYP,                      // E: dynamic sections (s-23), D: all
   X_L = X_D + NS + 1, X_R1 = X_L + NDYP, X_R0 = X_R1 + NDYP,  // dynamic, s-23
-  X_RAD = X_R0 + NDYP,                                   // radius sqrt(A / pi) of the dynamic sections
+  X_RAD = X_R0 + NDYP,                                   // 1 / radius sqrt(pi / A) of the dynamic sections
   X_SMP = X_RAD + NDYP,                                  // dipole samples (41)
   X_UNION = X_SMP + NDIP,
   //   sink slots of the phases before the rows (n): stores of lanes / slots with nothing to store
@@ -369,15 +369,12 @@ AFS_HD inline double fulcher_kent(double pressure_dPa, double d_cm) {
   return k;
 }
 
-// getJunctionInductance (TdsModel.cpp:1745-1778) from the radii sqrt(A / pi) of the two
-// sections, which the network phase computed already (X_RAD).  The areas are >= MIN_AREA (the
-// reference's clamps are no-ops) and sqrt is monotone, so max/min of the radii are the radii of
-// max/min of the areas.  (One reciprocal for b / a and H / b.)
-AFS_HD inline double junction_l(double r1, double r2) {
-  const double a = r1 > r2 ? r1 : r2, b = r1 > r2 ? r2 : r1;
-  const double r = fast_rcp(a * b);
-  const double H = 1.0 - (b * b) * r;
-  return (8.0 * RHO / (3.0 * PI * PI)) * H * (a * r);
+// getJunctionInductance (TdsModel.cpp:1745-1778) from the inverse radii sqrt(pi / A) of the two
+// sections, which the network phase computed already (X_RAD): with a, b the larger and the
+// smaller radius, 8 rho H / (3 pi^2 b) and H = 1 - b / a give 8 rho / (3 pi^2) (1/b - 1/a).  The
+// areas are >= MIN_AREA (the reference's clamps are no-ops).
+AFS_HD inline double junction_l(double ir1, double ir2) {
+  return (8.0 * RHO / (3.0 * PI * PI)) * fabs(ir1 - ir2);
 }
 
 // IirFilter::getOutputSample on a shift-register state x[0..n-1], y[0..n-1] (newest first).
@@ -522,7 +519,10 @@ AFS_HD inline void phase_interpolate(int gl, Lane<W> &R, double *X, const Consts
   // laterality, the nose sections 65..68 take the velum taper (Tube.cpp:402-416); other slots
   // (glottis, absent) compute on stand-ins.  The area and length stay in the lane (acur,
   // lcur) for the network phase of the same block.  (The constriction scans that read the
-  // interpolated geometry of all sections run ahead of the time loop: tree_plan.h.)
+  // interpolated geometry of all sections run ahead of the time loop: tree_plan.h.)  Not
+  // contracted into fmas: K5 (tree_plan.h PlanGeom) evaluates the same products and sums, and
+  // the reference's own a * (1 - r) + b * r rounds each product.
+#pragma clang fp contract(off)
   using S = Shape<W>;
   (void)gl;
   (void)X;
@@ -569,7 +569,10 @@ AFS_HD inline GlotRes glottis_eval(const GlotIn &in, const CT &C, double ratio, 
   const double r1 = 1.0 - ratio;
   GlotRes res;
   double *gp = res.gp;
-  for (int k = 0; k < 6; ++k) gp[k] = r1 * in.fl[k] + ratio * in.fr[k];
+  {  // (uncontracted as Tube::interpolate and K5's aspiration strength, tree_plan.h)
+#pragma clang fp contract(off)
+    for (int k = 0; k < 6; ++k) gp[k] = r1 * in.fl[k] + ratio * in.fr[k];
+  }
   if constexpr (MODEL == AFS_GLOTTIS_TWO_MASS) {
     res.go = two_mass_glottis(C, gp, p4, in.rel, res.rel);
     gp[5] = GLOTTIS_DEFAULT_ASPIRATION_DB;  // X_GP + 5 is read as the aspiration strength
@@ -705,33 +708,32 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     // divisions folded into one reciprocal of the area and one of the wall surface.
 #if defined(AFS_EXP_NO_NETGEO)  // timing experiment only (tools/phase_prof): no geometric chains
     const double inv_area = area, r0 = area * 0.5641895835, Rr = len * 1e-3, L = len * area, alw = 1e-3 * area,
-                 E = 1e-3 * len, c1 = 1e-3, c2 = 2e-3, c3 = 3e-3;
+                 E = 1e-3 * len, c1 = 1e-3, c2 = 2e-3, c3 = 3e-3, ia2 = inv_area * inv_area;
     const double bew = alw * (R.w[j] * c1 + R.wr[j] * c2 + R.wr2[j] * c3);
     (void)idt; (void)idt2;
 #else
-    const double vol = area * len;
+    // (the divisions rewritten around one reciprocal of the area: the Poiseuille resistance of
+    // the circular and the elliptic section (:741-760) as polynomials in 1/A, the wall terms with
+    // the wall surface cancelled (alpha = surf / K, beta = k1 w + k2 w' + k3 w''); the decisions
+    // -- elliptic or not, the surface clamp -- are the reference's comparisons)
     const double inv_area = fast_rcp(area);
     const double r0 = fast_sqrt(area * (1.0 / PI));
-    const double circ = 2.0 * PI * r0;
-    const double rmin = glot ? 0.8 : 1.6;
-    const bool ell = r0 < rmin;
-    const double a = ell ? rmin : r0;
-    const double b = ell ? area * (glot ? 1.0 / (PI * 0.8) : 1.0 / (PI * 1.6)) : r0;
+    const double ia2 = inv_area * inv_area;
+    const bool ell = r0 < (glot ? 0.8 : 1.6);
+    // elliptic: 2 mu len (a^2 + b^2) / (pi a^3 b^3), a = rmin, b = A / (pi rmin)
+    //         = len / A (2 mu pi^2 rmin^2 / A^2 + 2 mu / rmin^2); circular: 4 mu pi len / A^2
+    const double ce = glot ? 2.0 * MU * PI * PI * 0.64 : 2.0 * MU * PI * PI * 2.56;
+    const double cf = glot ? 2.0 * MU / 0.64 : 2.0 * MU / 2.56;
+    const double Rr = ell ? (len * inv_area) * fma(ce, ia2, cf) : (4.0 * MU * PI * len) * ia2;
     const double L = (RHO * 0.5 * len) * inv_area;
-    const double Cc = vol * (1.0 / (RHO * CSND * CSND));
-    const double Rr = fast_div((2.0 * MU * len) * (a * a + b * b), PI * a * a * a * b * b * b);
-    // soft walls (not for the glottis); evaluated for every slot, selected
-    double surf = circ * len;
+    const double Cc = (area * len) * (1.0 / (RHO * CSND * CSND));
+    double surf = (2.0 * PI * r0) * len;
     if (surf < AMIN) surf = AMIN;
-    const double inv_surf = fast_rcp(surf);
-    const double Rw = C.h.Bw_ph0 * inv_surf, Lw = C.h.Mw_ph0 * inv_surf;
-    const double alw = fast_rcp(Lw * idt2 + Rw * idt + C.h.Kw_ph0 * inv_surf);
-    const double bew = alw * (R.w[j] * (Lw * idt2 + Rw * idt) +
-                              R.wr[j] * (Lw * (TH1 / TH + 1.0) * idt + Rw * (TH1 / TH)) +
-                              R.wr2[j] * Lw * (TH1 / TH));
     const bool walls = opt.soft_walls && !glot;
-    const double alpha = walls ? alw : 0.0, beta = walls ? bew : 0.0;
+    const double alpha = walls ? surf * C.h.wall_invK : 0.0;
+    const double beta = walls ? fma(R.w[j], C.h.wall_k1, fma(R.wr[j], C.h.wall_k2, R.wr2[j] * C.h.wall_k3)) : 0.0;
     const double E = fast_div(dt * TH, Cc + alpha);
+    (void)idt; (void)idt2;
 #endif
 #if defined(AFS_EXP_NO_NETGEO)
     const bool walls = opt.soft_walls && !glot;
@@ -741,7 +743,6 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     double R0 = Rr, R1 = Rr;
     // Bernoulli losses between pharynx/mouth sections (TdsModel.cpp:850-877)
     const bool turb = opt.turbulence_losses && pm;
-    const double ia2 = inv_area * inv_area;
     {  // pair (s, s+1)
       double u = 0.0;
       u += X[X_U + s + 1];
@@ -763,9 +764,10 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
       R0 = (on & c) ? Rb : R0;
     }
     if (j == (S_LAST_MOUTH - DYN0) / W) {  // the slot that holds section 64 on one lane
-      // radiation resistance and inductance of the mouth (TdsModel.cpp:1874, 1889)
-      const double Rrad = fast_div(C.h.rrad_num, 9.0 * PI * PI * area);
-      const double Lrad = fast_div(C.h.lrad_num, 3.0 * PI * fast_sqrt(area * PI));
+      // radiation resistance and inductance of the mouth (TdsModel.cpp:1874, 1889): 128 rho c /
+      // (9 pi^2 A) and 8 rho / (3 pi sqrt(A pi)) = (8 rho / (3 pi)) r0 / A
+      const double Rrad = C.h.rrad_c * inv_area;
+      const double Lrad = (C.h.lrad_c * r0) * inv_area;
       const bool own = s == S_LAST_MOUTH;
       X[own ? X_RRAD : X_ACT] = Rrad;
       X[own ? X_RRAD + 1 : X_ACT + 1] = Lrad;
@@ -786,7 +788,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     X[X_E + ks] = E;
     X[X_D + (present ? s : NS)] = R.p[j] + C.h.dtTH1 * R.pr[j] - E * (beta - 0.0);
     X[X_L + ks] = L;
-    X[X_RAD + ks] = r0;  // (the row phase's junction inductance)
+    X[X_RAD + ks] = (PI * r0) * inv_area;  // 1 / r0 (the row phase's junction inductance)
     X[X_R0 + ks] = R0;
     X[X_R1 + ks] = R1;
   }

@@ -69,16 +69,24 @@ AFS_HD inline double plan_clampA(double a) { return a < AMIN ? AMIN : a; }
 
 // The interpolated pharynx/mouth geometry of one sample, evaluated on demand (no per-thread
 // arrays: K5 keeps its registers for occupancy).  Every value is computed with the operations
-// of tree_core.h phase_interpolate and Tube::calcPositions, so it is bit-identical however
-// often it is re-evaluated.
+// of tree_core.h phase_interpolate and Tube::calcPositions, with contraction into fmas off in
+// both (the pragmas below and in phase_interpolate), so K5 and the synthesis kernel see the same
+// bits whatever the compiler's -ffp-contract default, and re-evaluation gives the same value.
 struct PlanGeom {
   const afs_frame *fl, *fr;
   double r1, ratio;
   AFS_HD double area(int m) const {
+#pragma clang fp contract(off)
     return plan_clampA(r1 * plan_clampA(fl->area_cm2[m]) + ratio * plan_clampA(fr->area_cm2[m]));
   }
-  AFS_HD double len(int m) const { return r1 * fl->length_cm[m] + ratio * fr->length_cm[m]; }
-  AFS_HD double lat(int m) const { return r1 * fl->laterality[m] + ratio * fr->laterality[m]; }
+  AFS_HD double len(int m) const {
+#pragma clang fp contract(off)
+    return r1 * fl->length_cm[m] + ratio * fr->length_cm[m];
+  }
+  AFS_HD double lat(int m) const {
+#pragma clang fp contract(off)
+    return r1 * fl->laterality[m] + ratio * fr->laterality[m];
+  }
   AFS_HD int art(int m) const { return fl->articulator[m]; }  // the left tube's (Tube.cpp:452)
   // first section with the articulator and the smallest area (strict "<", from 1e6), -1: none
   AFS_HD int argmin(int a, double &amin, int skip_lo = 1, int skip_hi = 0) const {
@@ -119,6 +127,7 @@ struct PlanGeom {
 // (the same comparisons and the same sequential sums).
 AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double ratio, const SecRec *sec,
                                bool two_mass, uint64_t *w) {
+#pragma clang fp contract(off)
   const PlanGeom g{fl, fr, 1.0 - ratio, ratio};
   const double teeth = g.r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm;
   const double asp_db = two_mass ? GLOTTIS_DEFAULT_ASPIRATION_DB : g.r1 * fl->glottis[5] + ratio * fr->glottis[5];
