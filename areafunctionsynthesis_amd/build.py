@@ -84,5 +84,19 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return LIB
 
 
+def kernel_digest() -> str:
+    """Digest of what libafs.so is built from (every source and header, the compiler flags):
+    the committed PMC summaries (profiles/pmc_*.json) are keyed by it, so bench.py quotes a
+    counter figure only for the kernel it is timing."""
+    import hashlib
+    h = hashlib.sha1()
+    for f in SOURCES + HEADERS:
+        h.update(f.encode())
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    h.update(repr((COMMON, sorted(PER_SOURCE.items()))).encode())
+    return h.hexdigest()[:12]
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)

@@ -433,6 +433,40 @@ afs_status afs_rng_draws(afs_ctx *c, int32_t B, int64_t *draws) {
   return draws_of(c, c->ws, B, draws);
 }
 
+afs_status afs_noise_plans(afs_ctx *c, const afs_frame *frames, int32_t rows, int32_t F, int32_t hop, int64_t s0,
+                           int64_t s1, uint64_t *plans) {
+  static_assert(AFS_PLAN_WORDS * 8 == afs::PLAN_RECORD_BYTES, "afs.h / tree_plan.h record size");
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (!tree(c)) return fail(c, AFS_ERR_UNSUPPORTED, "afs_noise_plans: tree / seg solvers only");
+  if (!frames || !plans || rows <= 0 || F < 2 || hop < 1 || s0 < 0 || s1 <= s0 || s1 > (int64_t)(F - 1) * hop)
+    return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_noise_plans: need frames, plans, rows>0, num_frames>=2, hop>=1, "
+                                             "0 <= s_begin < s_end <= (num_frames-1)*hop");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  afs_status s;
+  const afs_frame *dframes = frames;
+  if (!is_device_ptr(frames)) {
+    const size_t bytes = (size_t)rows * F * sizeof(afs_frame);
+    if ((s = ensure(c, &c->stage_in, &c->stage_in_bytes, bytes)) != AFS_OK) return s;
+    HIP_TRY(c, hipMemcpyAsync(c->stage_in, frames, bytes, hipMemcpyHostToDevice, c->stream));
+    dframes = (const afs_frame *)c->stage_in;
+  }
+  const int64_t n = s1 - s0;
+  const size_t bytes = (size_t)rows * (size_t)n * afs::PLAN_RECORD_BYTES;
+  uint64_t *dplans = plans;
+  const bool host_out = !is_device_ptr(plans);
+  if (host_out) {
+    if ((s = ensure(c, &c->plan, &c->plan_bytes, bytes)) != AFS_OK) return s;
+    dplans = (uint64_t *)c->plan;
+  }
+  afs::PlanArgs pa{c->dev_tab, dframes, F, rows, hop, s0, s1, dplans, n,
+                   c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0,
+                   seg(c) ? c->dev_seg->uo : c->dev_tab->consts.sec};
+  HIP_TRY(c, afs::launch_plan(pa, c->stream));
+  if (host_out) HIP_TRY(c, hipMemcpyAsync(plans, dplans, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return AFS_OK;
+}
+
 afs_status afs_session_create(afs_ctx *c, int32_t B, const uint32_t *seeds, afs_session **out) {
   if (!c || !out || B <= 0) return c ? fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_session_create: bad args") : AFS_ERR_INVALID_ARGUMENT;
   HIP_TRY(c, hipSetDevice(c->cfg.device));

@@ -135,6 +135,20 @@ class Context:
                          "nonfinite": nonfinite}
         return out
 
+    def noise_plans(self, frames: np.ndarray, hop: int, s_begin: int = 0, s_end: Optional[int] = None) -> np.ndarray:
+        """Diagnostics (tree / seg solvers): the noise-source plan records K5 computes for samples
+        [s_begin, s_end) of frames[rows, F] -> uint64[rows, s_end - s_begin, AFS_PLAN_WORDS]."""
+        if frames.dtype != FRAME_DTYPE or frames.ndim != 2:
+            raise ValueError("frames must be a 2-D FRAME_DTYPE array [rows, F]")
+        rows, F = frames.shape
+        if s_end is None:
+            s_end = (F - 1) * hop
+        frames = np.ascontiguousarray(frames)
+        out = np.zeros((rows, s_end - s_begin, _native.AFS_PLAN_WORDS), dtype=np.uint64)
+        st = self._lib.afs_noise_plans(self._h, _vp(_addr(frames)), rows, F, hop, s_begin, s_end, _vp(_addr(out)))
+        _native.check(st, self._h, "afs_noise_plans")
+        return out
+
     def kernel_times(self) -> dict:
         """(profile=True contexts) summed device time and count of the synthesis-kernel and
         noise-source-plan launches since the previous call (waits for the stream)."""

@@ -17,7 +17,12 @@ object of the dominant kernel (HBM, as the north star asks, with the kernel's ow
 from HIP events around every launch: afs_kernel_times), the fp64 object (the path's binding
 resource: algorithmic flops counted from the restatement, profiles/flops_per_sample.json) and
 the CPU baseline (the reference's own sources, oracle/_ref, timed on this host's cores over a
-bounded sample, plus the single-core config-1 figure).
+bounded sample, plus the single-core config-1 figure).  On one GPU the line also carries
+"configs": config 5 (8192 fricatives, velum 1.0 cm^2) and config 3 (8192 VCV utterances through
+playTargetSequence), each timed over a few steps with its own launch times, roofline, fp64
+object, reference CPU rate and error against the reference build (--no-sub-configs skips them).
+PMC-derived figures are quoted only when profiles/pmc_*.json hold a pass of this build's kernel
+sources (areafunctionsynthesis_amd.build.kernel_digest).
 """
 from __future__ import annotations
 
@@ -38,25 +43,32 @@ CPU_PROC_CAP = 16              # the box's CPU share per GPU (gpurun: 16 for one
 
 
 def flops_per_sample(workload: str):
-    """Reference-algorithm fp64 flops per sample (tools/flopcount: the restatement in the
-    reference's operation order, instrumented), for the workload's family."""
+    """fp64 flops per sample (tools/flopcount: the restatement in the reference's operation
+    order, instrumented; with the own-algorithm figure beside it), for the workload's family."""
     path = os.path.join(ROOT, "profiles", "flops_per_sample.json")
     if not os.path.exists(path):
         return None, None
     db = json.load(open(path))["workloads"]
-    fam = {"static": "config2", "fricatives": "config5", "vcv": "config2"}[workload]
+    fam = {"static": "config2", "fricatives": "config5", "vcv": "config3"}[workload]
     for name, e in db.items():
         if name.startswith(fam):
             return e["per_sample"], name
     return None, None
 
 
-def pmc_entry(name: str, key: str):
-    """An entry of a committed PMC summary under profiles/ (None when absent)."""
+def pmc_entry(name: str, key: str, digest: str):
+    """(entry, stale) of a committed PMC summary under profiles/: the entry measured on this
+    build's kernel sources (build.kernel_digest), else (None, the newest other entry's tag)."""
     path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
-        return None
-    return json.load(open(path)).get(key)
+        return None, None
+    by = json.load(open(path)).get(key) or {}
+    if "tag" in by:  # (a summary written before the entries were keyed by the sources' digest)
+        by = {"?": by}
+    if digest in by:
+        return by[digest], None
+    others = sorted(by.values(), key=lambda e: e.get("tag", ""))
+    return None, (others[-1].get("tag") if others else None)
 
 
 def frame_bytes_per_sample(hop: int) -> float:
@@ -141,6 +153,169 @@ def config1_frames(fs: float):
     return np.repeat(f[None], int(round(fs / 441)) + 1)
 
 
+WORKLOAD_TEXT = {
+    "static": "BASELINE config 4 shard: {B} static-vowel utterances/GPU x {sec:g} s @ {fs:g} Hz ({B8} at 8 GPUs), "
+              "frames resident in HBM",
+    "fricatives": "BASELINE config 5: {B} fricative utterances (s f z S Z x C R v) + velum 1.0 cm^2/GPU x {sec:g} s "
+                  "@ {fs:g} Hz, frames resident in HBM",
+    "vcv": "BASELINE config 3 (fp64 state): {B} VCV utterances/GPU through playTargetSequence ({T} samples @ "
+           "{fs:g} Hz, per-sample area-function tubes built on the GPU)",
+}
+
+
+class Measured:
+    """One workload's timed run: K steps bracketed by synchronisations (and barriers)."""
+
+
+def measure(args, ctx, dev, stream, workload: str, B: int, first: int, world: int, rank: int, comm,
+            steps: int, warmup: int) -> Measured:
+    import torch
+    import torch.distributed as dist
+
+    from areafunctionsynthesis_amd import sharding
+    from areafunctionsynthesis_amd.frames import FRAME_DTYPE
+    from areafunctionsynthesis_amd.workloads import build_frames, fricatives, static_vowels, vcv_targets
+
+    m = Measured()
+    m.workload, m.B, m.steps, m.warmup = workload, B, steps, warmup
+    if workload in ("static", "fricatives"):
+        gen = static_vowels if workload == "static" else fricatives
+        w = gen(B, seconds=args.seconds, fs=args.fs, first_utterance=first)
+        m.frames = build_frames(w, ctx.af_to_frames)
+        m.F, m.hop, m.T = w.num_frames, w.hop, w.samples_per_utterance
+        m.seeds = w.seeds
+        frames_dev = torch.from_numpy(m.frames.view(np.uint8).reshape(B, m.F, FRAME_DTYPE.itemsize)).to(dev)
+
+        def synth():
+            ctx.synthesize(frames_dev, m.hop, seeds=seeds_dev, out=out_dev)
+    else:
+        m.shapes, m.targets, m.seeds = vcv_targets(B, first_utterance=first)
+        m.hop, m.T = 1, ctx.target_sequence_samples()
+
+        def synth():
+            ctx.play_target_sequences(m.shapes, m.targets, seeds=seeds_dev, out=out_dev)
+    seeds_dev = torch.from_numpy(m.seeds.astype(np.int32)).to(dev)
+    out_dev = torch.empty((B, m.T), dtype=torch.float64, device=dev)
+    m.out_dev = out_dev
+
+    # the reference's output format (int16, Synthesizer.cpp:955-973) is produced on the GPU and
+    # gathered to rank 0 by the library's RCCL gather while the next step synthesizes
+    transport = sharding.CommTransport(comm) if comm is not None else _NoGather()
+    pcm = sharding.PcmGather(lambda x, o: ctx.to_int16(x, out=o), (B, m.T), world, rank, transport, device=dev)
+
+    for _ in range(warmup):
+        synth()
+        pcm.submit(out_dev)
+    pcm.drain()
+    torch.cuda.synchronize(dev)
+    ctx.kernel_times()  # drop the warm-up launches
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        synth()
+        ev[k][1].record(stream)
+        pcm.submit(out_dev)
+    pcm.drain()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    m.synth_ms = [a.elapsed_time(b) for a, b in ev]
+    m.kt = ctx.kernel_times()
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    m.elapsed = float(t.item())
+    return m
+
+
+def describe(args, m: Measured, world: int, digest: str) -> dict:
+    """value, roofline and fp64 objects of a measured workload."""
+    B, T, hop = m.B, m.T, m.hop
+    total_samples = float(world) * B * T * m.steps
+    value = total_samples / m.elapsed
+    kname = {"cholesky": "lane_synth_kernel", "sor": "lane_synth_kernel", "seg": "seg_synth_kernel"}.get(
+        args.solver, "tree_synth_kernel")
+    launches = max(1, m.kt["synth_launches"])
+    avg_launch_s = m.kt["synth_ms"] / launches / 1e3
+    samples_per_launch = B * T * m.steps / launches
+    bps = frame_bytes_per_sample(hop)
+    alg_bytes = samples_per_launch * bps
+    achieved_gbs = alg_bytes / avg_launch_s / 1e9
+    tkey = f"{kname}|{m.workload}|B={B}|T={T}|hop={hop}"
+    tr, tr_stale = pmc_entry("pmc_traffic.json", tkey, digest)
+    sq, sq_stale = pmc_entry("pmc_sq_fp64.json", tkey, digest)
+    per, per_src = flops_per_sample(m.workload)
+    fp64 = None
+    if per is not None:
+        alg_tf = per["flops"] * samples_per_launch / avg_launch_s / 1e12
+        own = per.get("own_algorithm_flops")
+        own_tf = own * samples_per_launch / avg_launch_s / 1e12 if own else None
+        fp64 = {
+            "algorithmic_flops_per_sample": per["flops"],
+            "algorithmic_transcendentals_per_sample": per["transc"],
+            "algorithmic_source": f"profiles/flops_per_sample.json [{per_src}]: the restatement in the "
+                                  "reference's operation order (envelope Cholesky), instrumented per IR block",
+            "achieved_tflops": alg_tf,
+            "peak_tflops": FP64_PEAK_TFLOPS,
+            "frac": alg_tf / FP64_PEAK_TFLOPS,
+            "own_algorithm_flops_per_sample": own,
+            "own_algorithm": "the same count with the envelope Cholesky (counted per function: "
+                             f"{per.get('cholesky_flops', 0):.0f} flops) replaced by the arm LDL^T "
+                             f"({per.get('arm_ldlt_flops', 0):.0f} flops: 2 per current, 7 per edge)",
+            "own_algorithm_achieved_tflops": own_tf,
+            "own_algorithm_frac": own_tf / FP64_PEAK_TFLOPS if own_tf else None,
+            "executed_lane_flops_per_sample": sq["lane_flops_per_sample"] if sq else None,
+            "executed_source": (f"profiles/pmc_sq_fp64.json [{sq['tag']}, commit {sq.get('commit')}, sources "
+                                f"{digest} = this build] (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes / 4 utterances per wave)"
+                                if sq else (f"no SQ pass of this build's kernel (sources {digest}); newest is "
+                                            f"{sq_stale}" if sq_stale else None)),
+        }
+    roof = {
+        "bound": "hbm",
+        "achieved": achieved_gbs,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved_gbs / HBM_PEAK_GBS,
+        "traffic": tr["traffic_bytes_per_launch"] if tr else None,
+        "traffic_unit": "bytes per launch (rocprofv3 PMC)",
+        "traffic_correction": tr["correction"] if tr else None,
+        "traffic_source": (f"profiles/pmc_traffic.json [{tr['tag']}, commit {tr.get('commit')}, sources {digest} = "
+                           "this build]" if tr else (f"no PMC pass of this build's kernel (sources {digest}); "
+                                                     f"newest is {tr_stale}" if tr_stale else None)),
+        "algorithmic_bytes_per_launch": alg_bytes,
+        "bytes_per_sample": bps,
+        "kernel": kname,
+        "avg_launch_ms": avg_launch_s * 1e3,
+        "launches_per_step": m.kt["synth_launches"] / m.steps,
+        "launch_timing": "HIP events around every launch on the library's stream (afs_kernel_times)",
+        "plan_kernel_ms_per_step": m.kt["plan_ms"] / m.steps,
+        "binding_resource": "neither HBM nor MFMA: the latency of the per-sample fp64 recurrence "
+                            "(SURVEY.md 8(d)); see fp64",
+    }
+    if tr and tr.get("plan_kernel_traffic_bytes_per_launch") is not None:
+        roof["plan_kernel_traffic_bytes_per_launch"] = tr["plan_kernel_traffic_bytes_per_launch"]
+    return {"value": value, "ms_per_step": m.elapsed / m.steps * 1e3, "roofline": roof, "fp64": fp64,
+            "step_device_ms": float(np.mean(m.synth_ms))}
+
+
+def cpu_leg(args, m: Measured, n: int):
+    """The reference build on the first n utterances of the measured batch (bounded sample)."""
+    gpu_out = m.out_dev[:n].cpu().numpy()
+    if m.workload != "vcv":
+        jobs = [("frames", m.frames[u], int(m.seeds[u]), m.hop) for u in range(n)]
+        what = f"{m.F - 1} frames x {m.hop} samples"
+    else:
+        jobs = [("target", m.shapes[m.targets[u]], int(m.seeds[u]), None) for u in range(n)]
+        what = f"playTargetSequence, {m.T} samples, trajectory built per sample on the CPU"
+    return cpu_baseline(jobs, args.fs, n, gpu_out, what, config1_frames(args.fs))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +331,10 @@ def main() -> None:
                     help="static: config-4 shard of static vowels (default); fricatives: config 5 "
                          "(fricatives + velum 1.0 cm^2); vcv: config-3 VCV utterances through "
                          "playTargetSequence (per-sample tubes, hop 1)")
+    ap.add_argument("--no-sub-configs", action="store_true",
+                    help="skip the config-5 / config-3 sub-objects (one GPU, default workload only)")
+    ap.add_argument("--sub-steps", type=int, default=2)
+    ap.add_argument("--sub-cpu-utterances", type=int, default=16)
     args = ap.parse_args()
 
     import torch
@@ -171,177 +350,83 @@ def main() -> None:
     dev = torch.device("cuda", local)
 
     from areafunctionsynthesis_amd import sharding
-    from areafunctionsynthesis_amd.frames import FRAME_DTYPE
+    from areafunctionsynthesis_amd.build import kernel_digest
     from areafunctionsynthesis_amd.synthesizer import Comm, Context, comm_unique_id
-    from areafunctionsynthesis_amd.workloads import build_frames, fricatives, static_vowels, vcv_targets
 
+    digest = kernel_digest()
     B = args.batch
     ctx = Context(args.fs, solver=args.solver, device=local, async_calls=True, profile=True)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
-
     first, _ = sharding.shard_range(rank, world, B)
-    if args.workload in ("static", "fricatives"):
-        gen = static_vowels if args.workload == "static" else fricatives
-        w = gen(B, seconds=args.seconds, fs=args.fs, first_utterance=first)
-        frames = build_frames(w, ctx.af_to_frames)
-        F, hop, T = w.num_frames, w.hop, w.samples_per_utterance
-        seeds = w.seeds
-        frames_dev = torch.from_numpy(frames.view(np.uint8).reshape(B, F, FRAME_DTYPE.itemsize)).to(dev)
-
-        def synth():
-            ctx.synthesize(frames_dev, hop, seeds=seeds_dev, out=out_dev)
-    else:
-        shapes, targets, seeds = vcv_targets(B, first_utterance=first)
-        hop, T = 1, ctx.target_sequence_samples()
-
-        def synth():
-            ctx.play_target_sequences(shapes, targets, seeds=seeds_dev, out=out_dev)
-    seeds_dev = torch.from_numpy(seeds.astype(np.int32)).to(dev)
-    out_dev = torch.empty((B, T), dtype=torch.float64, device=dev)
-
-    # the reference's output format (int16, Synthesizer.cpp:955-973) is produced on the GPU and
-    # gathered to rank 0 by the library's RCCL gather while the next step synthesizes
     comm = None
     if world > 1:
         uid = [comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = Comm(ctx, uid[0], rank, world)
-        transport = sharding.CommTransport(comm)
-    else:
-        transport = _NoGather()
-    pcm = sharding.PcmGather(lambda x, o: ctx.to_int16(x, out=o), (B, T), world, rank, transport, device=dev)
 
-    def step():
-        synth()
-        pcm.submit(out_dev)
-
-    for _ in range(args.warmup):
-        step()
-    pcm.drain()
-    torch.cuda.synchronize(dev)
-    ctx.kernel_times()  # drop the warm-up launches
-
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
-        synth()
-        ev[k][1].record(stream)
-        pcm.submit(out_dev)
-    pcm.drain()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    synth_ms = [a.elapsed_time(b) for a, b in ev]
-    kt = ctx.kernel_times()
-    t = torch.tensor([elapsed], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    m = measure(args, ctx, dev, stream, args.workload, B, first, world, rank, comm, args.steps, args.warmup)
+    # one GPU: config 5 and config 3 are timed too (sub-objects, a few steps each)
+    subs = []
+    if world == 1 and args.workload == "static" and not args.no_sub_configs:
+        for wl, label in (("fricatives", "config5"), ("vcv", "config3")):
+            subs.append((label, measure(args, ctx, dev, stream, wl, B, first, world, rank, None, args.sub_steps, 1)))
 
     if rank == 0:
-        total_samples = float(world) * B * T * args.steps
-        value = total_samples / elapsed
-        ms_step = elapsed / args.steps * 1e3
-        kname = "lane_synth_kernel" if args.solver in ("cholesky", "sor") else "tree_synth_kernel"
-        launches = max(1, kt["synth_launches"])
-        avg_launch_s = kt["synth_ms"] / launches / 1e3
-        samples_per_launch = B * T * args.steps / launches
-        bps = frame_bytes_per_sample(hop)
-        alg_bytes = samples_per_launch * bps
-        achieved_gbs = alg_bytes / avg_launch_s / 1e9
-        tkey = f"{kname}|{args.workload}|B={B}|T={T}|hop={hop}"
-        tr = pmc_entry("pmc_traffic.json", tkey)
-        per, per_src = flops_per_sample(args.workload)
-        sq = pmc_entry("pmc_sq_fp64.json", tkey)
-        fp64 = None
-        if per is not None:
-            alg_tf = per["flops"] * samples_per_launch / avg_launch_s / 1e12
-            fp64 = {
-                "algorithmic_flops_per_sample": per["flops"],
-                "algorithmic_transcendentals_per_sample": per["transc"],
-                "algorithmic_source": f"profiles/flops_per_sample.json [{per_src}]: the restatement in the "
-                                      "reference's operation order (envelope Cholesky), instrumented per IR block",
-                "achieved_tflops": alg_tf,
-                "peak_tflops": FP64_PEAK_TFLOPS,
-                "frac": alg_tf / FP64_PEAK_TFLOPS,
-                "executed_lane_flops_per_sample": sq["lane_flops_per_sample"] if sq else None,
-                "executed_source": f"profiles/pmc_sq_fp64.json [{sq['tag']}] (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes / "
-                                   "4 utterances per wave)" if sq else None,
-            }
+        d = describe(args, m, world, digest)
         result = {
             "metric": "audio samples/s (whole node) on 64k-utterance batch; max-abs err vs CPU ref",
-            "value": value,
+            "value": d["value"],
             "unit": "samples/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": ms_step,
+            "ms_per_step": d["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": {
-                    "static": f"BASELINE config 4 shard: {B} static-vowel utterances/GPU x {args.seconds:g} s "
-                              f"@ {args.fs:g} Hz ({B * 8} at 8 GPUs), frames resident in HBM",
-                    "fricatives": f"BASELINE config 5: {B} fricative utterances (s f z S Z x C R v) + velum "
-                                  f"1.0 cm^2/GPU x {args.seconds:g} s @ {args.fs:g} Hz, frames resident in HBM",
-                    "vcv": f"BASELINE config 3 (fp64 state): {B} VCV utterances/GPU through playTargetSequence "
-                           f"({T} samples @ {args.fs:g} Hz, per-sample area-function tubes built on the GPU)",
-                }[args.workload],
+                "workload": WORKLOAD_TEXT[args.workload].format(B=B, B8=B * 8, sec=args.seconds, fs=args.fs, T=m.T),
                 "batch_per_gpu": B,
                 "global_batch": B * world,
-                "samples_per_utterance": T,
+                "samples_per_utterance": m.T,
                 "fs_hz": args.fs,
-                "hop": hop,
+                "hop": m.hop,
                 "solver": args.solver,
+                "kernel_sources": digest,
                 "parallelism": f"dp{world} (utterance shards; int16 audio gathered to rank 0 by afs_gather_pcm over "
                                "RCCL, overlapped with the next step)" if world > 1 else "dp1",
             },
-            "x_realtime": value / args.fs,
-            "step_device_ms": float(np.mean(synth_ms)),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved_gbs,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved_gbs / HBM_PEAK_GBS,
-                "traffic": tr["traffic_bytes_per_launch"] if tr else None,
-                "traffic_unit": "bytes per launch (rocprofv3 PMC)",
-                "traffic_correction": tr["correction"] if tr else None,
-                "traffic_source": f"profiles/pmc_traffic.json [{tr['tag']}]" if tr else None,
-                "algorithmic_bytes_per_launch": alg_bytes,
-                "bytes_per_sample": bps,
-                "kernel": kname,
-                "avg_launch_ms": avg_launch_s * 1e3,
-                "launches_per_step": kt["synth_launches"] / args.steps,
-                "launch_timing": "HIP events around every launch on the library's stream (afs_kernel_times)",
-                "plan_kernel_ms_per_step": kt["plan_ms"] / args.steps,
-                "binding_resource": "neither HBM nor MFMA: the latency of the per-sample fp64 recurrence "
-                                    "(SURVEY.md 8(d)); see fp64",
-            },
-            "fp64": fp64,
+            "x_realtime": d["value"] / args.fs,
+            "step_device_ms": d["step_device_ms"],
+            "roofline": d["roofline"],
+            "fp64": d["fp64"],
         }
         if world == 1 and not args.no_cpu_baseline:
-            n = min(args.cpu_utterances, B)
-            gpu_out = out_dev[:n].cpu().numpy()
-            if args.workload != "vcv":
-                jobs = [("frames", frames[u], int(seeds[u]), hop) for u in range(n)]
-                what = f"{F - 1} frames x {hop} samples"
-            else:
-                jobs = [("target", shapes[targets[u]], int(seeds[u]), None) for u in range(n)]
-                what = f"playTargetSequence, {T} samples, trajectory built per sample on the CPU"
-            cb, max_abs, max_rms = cpu_baseline(jobs, args.fs, n, gpu_out, what, config1_frames(args.fs))
+            cb, max_abs, max_rms = cpu_leg(args, m, min(args.cpu_utterances, B))
             result["cpu_baseline"] = cb
             result["max_abs_err_vs_cpu_ref"] = max_abs
             result["max_rms_err_vs_cpu_ref"] = max_rms
+        if subs:
+            result["configs"] = {}
+            for label, ms in subs:
+                ds = describe(args, ms, world, digest)
+                o = {
+                    "workload": WORKLOAD_TEXT[ms.workload].format(B=B, B8=B * 8, sec=args.seconds, fs=args.fs, T=ms.T),
+                    "value": ds["value"], "unit": "samples/s", "steps": ms.steps, "warmup": ms.warmup,
+                    "ms_per_step": ds["ms_per_step"], "samples_per_utterance": ms.T, "hop": ms.hop,
+                    "avg_launch_ms": ds["roofline"]["avg_launch_ms"], "roofline": ds["roofline"], "fp64": ds["fp64"],
+                }
+                if not args.no_cpu_baseline:
+                    cb, max_abs, max_rms = cpu_leg(args, ms, min(args.sub_cpu_utterances, B))
+                    o["cpu_reference_per_core_samples_per_s"] = cb["per_core_samples_per_s"]
+                    o["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample",
+                                                            "per_core_samples_per_s")}
+                    o["max_abs_err_vs_cpu_ref"] = max_abs
+                    o["max_rms_err_vs_cpu_ref"] = max_rms
+                result["configs"][label] = o
         print(json.dumps(result), flush=True)
     if comm is not None:
         comm.close()

@@ -168,6 +168,15 @@ afs_status afs_synthesize(afs_ctx *ctx, const afs_frame *frames, const uint32_t 
  * count that differs from the reference's means a noise source switched on or off at a
  * different sample (TdsModel.cpp:1647-1666).  Tree solver only (else AFS_ERR_UNSUPPORTED). */
 afs_status afs_rng_draws(afs_ctx *ctx, int32_t batch, int64_t *draws);
+/* Diagnostics: the noise-source plan records the tree / seg solvers compute ahead of the time
+ * loop (kernel K5; AFS_PLAN_WORDS u64 words per sample, layout in csrc/tree_plan.h) for samples
+ * [s_begin, s_end) of frames[rows][num_frames] at this hop: plans[rows][s_end - s_begin]
+ * [AFS_PLAN_WORDS] (host or device).  Everything calcNoiseSources decides from the geometry
+ * (TdsModel.cpp:1188-1508); tests compare it bit for bit with the host restatement.  Other
+ * solvers: AFS_ERR_UNSUPPORTED. */
+#define AFS_PLAN_WORDS 16
+afs_status afs_noise_plans(afs_ctx *ctx, const afs_frame *frames, int32_t rows, int32_t num_frames, int32_t hop,
+                           int64_t s_begin, int64_t s_end, uint64_t *plans);
 
 /* Stateful sessions: B independent Synthesizer instances living on the device. */
 afs_status afs_session_create(afs_ctx *ctx, int32_t batch, const uint32_t *seeds, afs_session **s);

@@ -3,6 +3,8 @@
 //   adapter_main frames <file>        print afs_frame fields of a mock tube (CPU)
 //   adapter_main nodevice             create a context on a missing device -> afs::Error (CPU)
 //   adapter_main synth <in> <out>     run TdsVoices (batch 1) over frames read from <in> (GPU)
+//   adapter_main latency <in> <out>   the same, writing the wall time of every call (ms) to <out>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -67,7 +69,8 @@ int main(int argc, char **argv) {
     }
     return 0;
   }
-  if (!std::strcmp(argv[1], "synth") && argc >= 5) {
+  const bool latency = !std::strcmp(argv[1], "latency");
+  if ((!std::strcmp(argv[1], "synth") || latency) && argc >= 5) {
     // <in>: int32 F, int32 hop, double fs, uint32 seed, then F afs_frame records
     FILE *fi = std::fopen(argv[2], "rb");
     if (!fi) return 3;
@@ -83,14 +86,19 @@ int main(int argc, char **argv) {
     (void)argv[4];
     afs::Context ctx(fs, 0);
     afs::TdsVoices<MockTube> voice(ctx, 1, &seed);
-    std::vector<double> out;
+    std::vector<double> out, ms;
     std::vector<double> buf((size_t)hop);
     for (int k = 0; k < F; ++k) {
       MockTube t;
       fill(t, fr[(size_t)k]);
+      // (one call as SynthesisThread makes it: tube + glottis in, hop samples back in host memory)
+      const auto t0 = std::chrono::steady_clock::now();
       int n = voice.synthesizeSignalTds(&t, fr[(size_t)k].glottis, hop, buf.data());
+      const auto t1 = std::chrono::steady_clock::now();
+      ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
       out.insert(out.end(), buf.begin(), buf.begin() + n);
     }
+    if (latency) out = ms;
     FILE *fo = std::fopen(argv[3], "wb");
     std::fwrite(out.data(), sizeof(double), out.size(), fo);
     std::fclose(fo);

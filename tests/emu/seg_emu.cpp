@@ -129,3 +129,31 @@ extern "C" int emu_seg_tables_ok(double fs) {
   build_seg_tables(T, &S);
   return S.ok;
 }
+
+// The noise-source plan records (tree_plan.h plan_sample, as K5 evaluates them) of samples
+// [s0, s1) of frames[rows][F] at this hop: out[rows][s1 - s0][PLAN_WORDS].  seg_layout: the X_UN
+// offsets of the seg kernel's LDS layout instead of the tree kernel's.
+extern "C" int emu_plan_records(const afs_frame *frames, int rows, int F, int hop, long s0, long s1, double fs,
+                                int two_mass, int seg_layout, uint64_t *out) {
+  static Tables T;
+  static SegTables S;
+  afs_options opt = afs::default_options();
+  opt.glottis_model = two_mass ? AFS_GLOTTIS_TWO_MASS : AFS_GLOTTIS_TRIANGULAR;
+  build_tables(&T, fs, opt);
+  const SecRec *uo = T.consts.sec;
+  if (seg_layout) {
+    build_seg_tables(T, &S);
+    if (!S.ok) return -3;
+    uo = S.uo;
+  }
+  for (int r = 0; r < rows; ++r)
+    for (long s = s0; s < s1; ++s) {
+      const long k = s / hop + 1;
+      const int i = (int)(s - (k - 1) * hop);
+      const double ratio = (double)i / (double)hop;
+      const afs_frame *f = frames + (long)r * F;
+      tree::plan_sample(f + k - 1, f + k, ratio, uo, two_mass != 0,
+                        out + ((long)r * (s1 - s0) + (s - s0)) * tree::PLAN_WORDS);
+    }
+  return 0;
+}

@@ -336,3 +336,21 @@ def oracle_parallel(frames: np.ndarray, hop: int, seeds, fs: float, workers: int
         with mp.get_context("spawn").Pool(workers) as pool:
             res = pool.map(_draws_job, jobs)
     return np.stack([r[0] for r in res]), np.array([r[1] for r in res], dtype=np.int64)
+
+
+def _target_job(args):
+    shapes4, seed, fs = args
+    o = Oracle()
+    return o.utterance_draws(o.target_frames(shapes4, fs), 1, seed, fs)
+
+
+def oracle_target_parallel(shapes4: np.ndarray, seeds, fs: float, workers: int = 0):
+    """playTargetSequence in the oracle for shapes4[B, 4, 16] (the trajectory is built in each
+    worker), one utterance per task.  Returns (audio[B, T], rand() calls[B])."""
+    import multiprocessing as mp
+    B = shapes4.shape[0]
+    jobs = [(np.ascontiguousarray(shapes4[u]), int(seeds[u]), float(fs)) for u in range(B)]
+    workers = workers or max(1, min(16, (os.cpu_count() or 1), B))
+    with mp.get_context("spawn").Pool(workers) as pool:
+        res = pool.map(_target_job, jobs)
+    return np.stack([r[0] for r in res]), np.array([r[1] for r in res], dtype=np.int64)

@@ -60,6 +60,38 @@ def test_adapter_single_voice_vs_oracle(adapter_bin, oracle, tmp_path):
     assert np.abs(y - x).max() <= 1e-9
 
 
+@pytest.mark.gpu
+def test_adapter_realtime_latency(adapter_bin, oracle, tmp_path, parity_report):
+    """The real-time drop-in: one voice (TdsVoices<Tube>, batch 1) called like
+    SynthesisThread (SynthesisThread.cpp:18-35) with 1102-sample chunks -- 50 ms of audio at
+    22.05 kHz, the reference's buffer (Synthesizer.cpp:953, Synthesizer.h:63) -- for 100 calls
+    (5.5 s of a gliding fricative).  Every call must return within the 50 ms its audio lasts:
+    p99 of the wall time per call (tube conversion, upload, plan + synthesis launches, download)
+    < 50 ms."""
+    f = oracle.af_to_frame(default_shapes()["s"])
+    f["velum_opening_cm2"] = 0.2
+    f["glottis"] = DEFAULT_GLOTTIS
+    F = 101
+    frames = np.repeat(f[None], F)
+    frames["glottis"][:, 0] = 110 + 20 * np.sin(np.linspace(0, 6, F))
+    hop, fs, seed = 1102, 22050.0, 9
+    src = tmp_path / "in.bin"
+    with open(src, "wb") as fh:
+        fh.write(np.array([F, hop], np.int32).tobytes())
+        fh.write(np.array([fs], np.float64).tobytes())
+        fh.write(np.array([seed], np.uint32).tobytes())
+        fh.write(np.ascontiguousarray(frames, FRAME_DTYPE).tobytes())
+    dst = tmp_path / "ms.bin"
+    subprocess.run([adapter_bin, "latency", str(src), str(dst), "x"], check=True, capture_output=True)
+    ms = np.fromfile(dst, np.float64)[1:]  # (the first call latches the tube and makes no samples)
+    assert ms.shape == (F - 1,)
+    p50, p99 = np.percentile(ms, 50), np.percentile(ms, 99)
+    parity_report.append(
+        f"real-time drop-in (TdsVoices<Tube>, batch 1, {hop}-sample calls @ {fs:g} Hz = {hop / fs * 1e3:.0f} ms of "
+        f"audio per call, {F - 1} calls): wall time per call p50 {p50:.2f} ms p99 {p99:.2f} ms max {ms.max():.2f} ms")
+    assert p99 < 50.0, (p50, p99)
+
+
 REF_BACKEND = "/root/reference/src/Backend"
 REF_TUBE_O = os.path.join(ROOT, "oracle", "_ref", "obj", "Tube.o")
 

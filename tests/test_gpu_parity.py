@@ -308,6 +308,38 @@ def test_full_second_fricatives_config5(contexts, parity_report, solver):
                        solver)
 
 
+@pytest.mark.parametrize("solver", ("tree", "seg"))
+def test_full_length_vcv_config3(contexts, parity_report, solver):
+    """Config 3 at the reference's playTargetSequence timing (stationary 0.2/0.05/0.2/0.1 s,
+    transitions 0.05 s: 30870 samples @ 44.1 kHz): 512 VCV utterances (V, (V)C(V):, V, V over
+    the 15 vowel-consonant pairs, Synthesizer.cpp:1299-1422) through afs_play_target_sequences,
+    every 8th (64) against the oracle over the whole utterance, with the rand() call counts
+    compared utterance by utterance (TdsModel.cpp:1647-1666)."""
+    from oracle_lib import oracle_target_parallel
+    from areafunctionsynthesis_amd.workloads import vcv_targets
+    ctx = contexts(44100.0, solver)
+    B = 512
+    shapes, targets, seeds = vcv_targets(B)
+    y, rep = ctx.play_target_sequences(shapes, targets, seeds=seeds, report=True)
+    assert y.shape == (B, 30870)
+    assert rep["nonfinite_utterances"] == 0
+    idx = np.arange(0, B, 8)
+    x, draws = oracle_target_parallel(shapes[targets[idx]], seeds[idx], 44100.0)
+    err = y[idx] - x
+    rms = np.sqrt(np.mean(err ** 2, axis=1))
+    mx = np.abs(err).max(axis=1)
+    gd = ctx.rng_draws(B)[idx]
+    flips = int(np.count_nonzero(gd != draws))
+    parity_report.append(
+        f"config 3 (VCV playTargetSequence, 30870 samples @ 44.1 kHz) [{solver}]: {len(idx)}/{B} utterances vs "
+        f"oracle: per-utterance RMS max {rms.max():.2e} p99 {np.percentile(rms, 99):.2e} median {np.median(rms):.2e}; "
+        f"max |err| {mx.max():.2e}; pass (RMS < {RMS_TOL:g}) {int(np.count_nonzero(rms < RMS_TOL))}/{len(idx)}; "
+        f"rand() call counts differing from the oracle: {flips} (oracle total {int(draws.sum())})")
+    for k, u in enumerate(idx):
+        assert rms[k] < RMS_TOL, (int(u), float(rms[k]), float(mx[k]))
+    assert flips == 0
+
+
 OPTION_VARIANTS = [
     {"turbulence_losses": 0}, {"soft_walls": 0}, {"generate_noise_sources": 0},
     {"radiation_from_skin": 0}, {"piriform_fossa": 1}, {"inner_length_corrections": 0},

@@ -12,7 +12,7 @@ for rep in 1 2; do
       PP_LIB=libphase_prof_$t.so timeout -k 10 240 python tools/phase_prof/run.py --batch 8192 --seconds ${PP_SECONDS:-0.05} > gpurun_out/ab_pp_${t}_$rep.txt 2>&1 || { echo "STOP pp $t"; exit 3; }
       head -1 gpurun_out/ab_pp_${t}_$rep.txt; tail -1 gpurun_out/ab_pp_${t}_$rep.txt
     fi
-    AFS_LIB=$PWD/areafunctionsynthesis_amd/libafs_$t.so timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 --seconds ${AB_SECONDS:-0.25} ${AB_ARGS:-} > gpurun_out/ab_bench_${t}_$rep.txt 2>&1 || { echo "STOP bench $t"; exit 3; }
+    AFS_LIB=$PWD/areafunctionsynthesis_amd/libafs_$t.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-sub-configs --steps 2 --warmup 1 --seconds ${AB_SECONDS:-0.25} ${AB_ARGS:-} > gpurun_out/ab_bench_${t}_$rep.txt 2>&1 || { echo "STOP bench $t"; exit 3; }
     python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split('\n')[-1]); print('$t bench', round(d['value']/1e6,2), 'M samples/s', round(d['ms_per_step'],1), 'ms', 'launch', round(d['roofline']['avg_launch_ms'],2), 'plan', round(d['roofline']['plan_kernel_ms_per_step'],2))" gpurun_out/ab_bench_${t}_$rep.txt
   done
 done

@@ -45,6 +45,13 @@ def main() -> None:
     plain = Oracle()
     lib = fc.lib if hasattr(fc, "lib") else ctypes.CDLL(so)
     cnt = (ctypes.c_uint64 * len(KINDS))()
+    blocks = json.load(open(os.path.join(HERE, "_build", "fc_blocks.json")))
+    nb = lib.fc_nblocks()
+    assert nb == len(blocks["ops"])
+    hits = (ctypes.c_uint64 * nb)()
+    ops = np.array(blocks["ops"], dtype=np.float64)
+    chol = np.array([f == "tds_cholesky" for f in blocks["fn"]])
+    FL = [KINDS.index(k) for k in ("add", "sub", "mul", "div", "sqrt")]
     fs = 44100.0
     result = {"source": "oracle/afs_oracle.c (reference operation order), clang -O0 IR, no fp contraction; "
                         "flops = fadd + fsub + fmul + fdiv + sqrt on double; transcendental calls "
@@ -59,14 +66,23 @@ def main() -> None:
     cases[f"config2 static vowels {args.batch} x {args.seconds:g} s"] = (frames_of(plain, w), w.hop, list(w.seeds))
     w = workloads.fricatives(args.batch, seconds=args.seconds, fs=fs)
     cases[f"config5 fricatives+velum {args.batch} x {args.seconds:g} s"] = (frames_of(plain, w), w.hop, list(w.seeds))
+    # config 3: playTargetSequence trajectories (one tube per sample, hop 1); the synthesis only
+    # (the per-sample area-function -> tube evaluation is not counted)
+    shapes, targets, seeds = workloads.vcv_targets(2)
+    vf = np.stack([plain.target_frames(shapes[t], fs) for t in targets])
+    cases["config3 vcv 2 x playTargetSequence"] = (vf, 1, list(seeds))
     for name, (frames, hop, seeds) in cases.items():
         tot = np.zeros(len(KINDS))
+        tot_chol = 0.0
         samples = 0
         for u, seed in enumerate(seeds):
             fr = frames if frames.ndim == 1 else frames[u]
             lib.fc_reset()
             x = fc.utterance(fr, hop, int(seed), fs)
             lib.fc_read(cnt)
+            lib.fc_hits(hits)
+            h = np.array(hits[:], dtype=np.float64)
+            tot_chol += float((h[chol, None] * ops[chol][:, FL]).sum())
             y = plain.utterance(fr, hop, int(seed), fs)
             if not np.array_equal(x, y, equal_nan=True):
                 raise SystemExit(f"{name}: the instrumented build differs from the oracle")
@@ -74,10 +90,19 @@ def main() -> None:
             samples += x.size
         per = {k: tot[i] / samples for i, k in enumerate(KINDS)}
         per["flops"] = sum(per[k] for k in ("add", "sub", "mul", "div", "sqrt"))
+        # this framework's algorithm: the same model with the envelope Cholesky
+        # (solveEquationsCholesky, TdsModel.cpp:2231-2314) replaced by the LDL^T in arm order
+        # over the current graph's TREE_NE = 104 edges and NC = 97 currents: per current one
+        # reciprocal of the pivot and one product with it, per edge 3 flops in the factor
+        # (l = a / d, d_parent -= l a), 2 forward and 2 backward
+        per["cholesky_flops"] = tot_chol / samples
+        per["arm_ldlt_flops"] = 2 * 97 + 7 * 104
+        per["own_algorithm_flops"] = per["flops"] - per["cholesky_flops"] + per["arm_ldlt_flops"]
         result["workloads"][name] = {"samples": samples, "per_sample": per}
         print(f"{name}: {per['flops']:.0f} flops/sample (add {per['add']:.0f} sub {per['sub']:.0f} "
               f"mul {per['mul']:.0f} div {per['div']:.0f} sqrt {per['sqrt']:.1f}), "
-              f"transcendental {per['transc']:.1f}, cmp {per['cmp']:.0f}")
+              f"transcendental {per['transc']:.1f}, cmp {per['cmp']:.0f}; envelope Cholesky {per['cholesky_flops']:.0f}, "
+              f"own algorithm {per['own_algorithm_flops']:.0f}")
     json.dump(result, open(args.out, "w"), indent=1)
     print("->", args.out)
 

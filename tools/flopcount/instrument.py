@@ -54,8 +54,9 @@ def classify(line: str):
 
 
 def instrument(ll: str):
-    out, table = [], []
+    out, table, fns = [], [], []
     in_fn = False
+    fn = None
     pending = None  # counts of the block being emitted (inserted once its phis are done)
     cur = None
 
@@ -63,10 +64,13 @@ def instrument(ll: str):
         nonlocal cur, pending
         cur = [0] * len(KINDS)
         table.append(cur)
+        fns.append(fn)
         pending = len(table) - 1
 
     for line in ll.splitlines():
         if line.startswith("define "):
+            m = re.search(r"@([A-Za-z0-9_.$]+)\(", line)
+            fn = m.group(1) if m else "?"
             in_fn = True
             out.append(line)
             open_block()
@@ -91,7 +95,7 @@ def instrument(ll: str):
             cur[KINDS.index(k)] += 1
         out.append(line)
     out.append("declare void @fc_bb(i32)")
-    return "\n".join(out) + "\n", table
+    return "\n".join(out) + "\n", table, fns
 
 
 def main() -> None:
@@ -100,7 +104,10 @@ def main() -> None:
     ll = os.path.join(build, "oracle.ll")
     subprocess.check_call([CLANG, "-O0", "-ffp-contract=off", "-fno-builtin", "-S", "-emit-llvm", "-o", ll,
                            os.path.join(ROOT, "oracle", "afs_oracle.c")])
-    text, table = instrument(open(ll).read())
+    text, table, fns = instrument(open(ll).read())
+    # the static table with each block's function (count.py splits the counts by function)
+    import json
+    json.dump({"kinds": KINDS, "ops": table, "fn": fns}, open(os.path.join(build, "fc_blocks.json"), "w"))
     ill = os.path.join(build, "oracle_fc.ll")
     open(ill, "w").write(text)
     rt = os.path.join(build, "fc_table.c")
@@ -112,6 +119,8 @@ def main() -> None:
         f.write("};\nstatic uint64_t hits[NB];\n")
         f.write("void fc_bb(int32_t id) { ++hits[id]; }\n")
         f.write("void fc_reset(void) { memset(hits, 0, sizeof hits); }\n")
+        f.write("int fc_nblocks(void) { return NB; }\n")
+        f.write("void fc_hits(uint64_t *out) { memcpy(out, hits, sizeof hits); }\n")
         f.write("void fc_read(uint64_t *out) { for (int k = 0; k < NK; ++k) { out[k] = 0; "
                 "for (int b = 0; b < NB; ++b) out[k] += hits[b] * ops[b][k]; } }\n")
     so = os.path.join(build, "liboracle_fc.so")

@@ -13,10 +13,33 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def store(path: str, key: str, entry: dict, digest: str) -> None:
+    """Merge entry into the JSON summary at path under key and the kernel sources' digest
+    (areafunctionsynthesis_amd.build.kernel_digest of the tree the counters were taken on), with
+    the commit it was measured at."""
+    import subprocess
+    try:
+        entry["commit"] = subprocess.check_output(["git", "-C", ROOT, "rev-parse", "--short=10", "HEAD"],
+                                                  text=True).strip()
+    except Exception:
+        entry["commit"] = None
+    entry["digest"] = digest
+    db = json.load(open(path)) if os.path.exists(path) else {}
+    cur = db.get(key)
+    if not isinstance(cur, dict) or "tag" in cur:  # (old layout: one entry per key)
+        cur = {}
+    cur[digest] = entry
+    db[key] = cur
+    with open(path, "w") as f:
+        json.dump(db, f, indent=1, sort_keys=True)
+        f.write("\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--digest", default=None, help="kernel_digest() of the measured tree (default: this tree)")
     ap.add_argument("--kernel", default="tree_synth_kernel")
     ap.add_argument("--workload", default="static")
     ap.add_argument("--batch", type=int, default=8192)
@@ -42,10 +65,11 @@ def main():
         "note": "SQ_WAVE_CYCLES / SQ_WAIT_ANY / SQ_ACTIVE_INST_VALU count quad-cycles (x 4); per wave-sample = "
                 "per wave and audio sample (a wave holds 4 utterances)",
     }
-    path = os.path.join(ROOT, "profiles", "pmc_sq_fp64.json")
-    db = json.load(open(path)) if os.path.exists(path) else {}
-    db[f"{a.kernel}|{a.workload}|B={a.batch}|T={a.samples}|hop={a.hop}"] = entry
-    json.dump(db, open(path, "w"), indent=1, sort_keys=True)
+    import sys
+    sys.path.insert(0, ROOT)
+    from areafunctionsynthesis_amd.build import kernel_digest
+    store(os.path.join(ROOT, "profiles", "pmc_sq_fp64.json"), f"{a.kernel}|{a.workload}|B={a.batch}|T={a.samples}|hop={a.hop}",
+          entry, a.digest or kernel_digest())
     print(json.dumps(entry))
 
 

@@ -18,6 +18,28 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def store(path: str, key: str, entry: dict, digest: str) -> None:
+    """Merge entry into the JSON summary at path under key and the kernel sources' digest
+    (areafunctionsynthesis_amd.build.kernel_digest of the tree the counters were taken on), with
+    the commit it was measured at."""
+    import subprocess
+    try:
+        entry["commit"] = subprocess.check_output(["git", "-C", ROOT, "rev-parse", "--short=10", "HEAD"],
+                                                  text=True).strip()
+    except Exception:
+        entry["commit"] = None
+    entry["digest"] = digest
+    db = json.load(open(path)) if os.path.exists(path) else {}
+    cur = db.get(key)
+    if not isinstance(cur, dict) or "tag" in cur:  # (old layout: one entry per key)
+        cur = {}
+    cur[digest] = entry
+    db[key] = cur
+    with open(path, "w") as f:
+        json.dump(db, f, indent=1, sort_keys=True)
+        f.write("\n")
+
+
 def key(kernel: str, workload: str, batch: int, samples: int, hop: int) -> str:
     return f"{kernel}|{workload}|B={batch}|T={samples}|hop={hop}"
 
@@ -30,13 +52,15 @@ def per_launch(path: str, kernel: str) -> list[float]:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
-    ap.add_argument("--dir", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--dir", default=None)
+    ap.add_argument("--digest", default=None, help="kernel_digest() of the measured tree (default: this tree)")
     ap.add_argument("--kernel", default="tree_synth_kernel")
     ap.add_argument("--workload", default="static")
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--samples", type=int, default=44100)
     ap.add_argument("--hop", type=int, default=441)
     a = ap.parse_args()
+    a.dir = a.dir or os.path.join(ROOT, "gpurun_out", a.tag)
     fetch = per_launch(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"), a.kernel)
     write = per_launch(os.path.join(a.dir, "pmc_write", "run_counter_collection.csv"), a.kernel)
     if not fetch or not write:
@@ -59,12 +83,11 @@ def main() -> None:
     }
     if plan_f and plan_w:  # K5, the noise-source plan producer of the same launches
         entry["plan_kernel_traffic_bytes_per_launch"] = 2.0 * kib * sum(plan_f) / len(plan_f) + kib * sum(plan_w) / len(plan_w)
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    db = json.load(open(path)) if os.path.exists(path) else {}
-    db[key(a.kernel, a.workload, a.batch, a.samples, a.hop)] = entry
-    with open(path, "w") as f:
-        json.dump(db, f, indent=1, sort_keys=True)
-        f.write("\n")
+    import sys
+    sys.path.insert(0, ROOT)
+    from areafunctionsynthesis_amd.build import kernel_digest
+    store(os.path.join(ROOT, "profiles", "pmc_traffic.json"), key(a.kernel, a.workload, a.batch, a.samples, a.hop),
+          entry, a.digest or kernel_digest())
     print(json.dumps(entry))
 
 
