@@ -89,7 +89,7 @@ constexpr int64_t PLAN_BUDGET_DEFAULT = (int64_t)4 << 30;
 // between launches.  rows: number of distinct frame rows (B, or the target sequences).
 // AFS_PROFILE: record an event on the context's stream (a pooled one; recording stops past
 // the pool's cap until afs_kernel_times drains it).
-hipEvent_t prof_event(afs_ctx *c) {
+hipEvent_t prof_event(afs_ctx *c, hipStream_t st) {
   if (!(c->cfg.flags & AFS_PROFILE)) return nullptr;
   constexpr size_t CAP = 1 << 14;
   if (c->pev_used == c->pev.size()) {
@@ -101,9 +101,10 @@ hipEvent_t prof_event(afs_ctx *c) {
     c->pev.push_back(e);
   }
   hipEvent_t e = c->pev[c->pev_used++];
-  if (hipEventRecord(e, c->stream) != hipSuccess) return nullptr;
+  if (hipEventRecord(e, st) != hipSuccess) return nullptr;
   return e;
 }
+hipEvent_t prof_event(afs_ctx *c) { return prof_event(c, c->stream); }
 void prof_pair(afs_ctx *c, hipEvent_t a, hipEvent_t b, int kind) {
   if (a && b) c->timed.push_back({a, b, kind});
 }
@@ -112,25 +113,48 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
                       double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B,
                       const int32_t *frame_row = nullptr) {
   if (tree(c)) {
+    // Launch chunks of `per` samples.  K5 (the noise-source plans of chunk k + 1) runs on the
+    // plan stream while K1 synthesizes chunk k on the context's stream: two plan buffers, K5
+    // of chunk k + 1 waits until K1 of chunk k - 1 has read that buffer, K1 of chunk k waits for
+    // its plans.  K5 (80 VGPRs, 4 KB of LDS per block) fits beside K1's wave (432 registers,
+    // 142 KB of LDS per CU) and takes issue slots K1's dependency stalls leave idle.
     const int64_t S = (int64_t)ntrans * hop;
     const int64_t per = std::max<int64_t>(1, std::min<int64_t>({S, 65536, c->plan_budget / ((int64_t)rows * afs::PLAN_RECORD_BYTES)}));
-    afs_status st = ensure(c, &c->plan, &c->plan_bytes, (size_t)rows * (size_t)per * afs::PLAN_RECORD_BYTES);
+    const int64_t nch = (S + per - 1) / per;
+    const size_t pbytes = (size_t)rows * (size_t)per * afs::PLAN_RECORD_BYTES;
+    afs_status st = ensure(c, &c->plan, &c->plan_bytes, pbytes);
     if (st != AFS_OK) return st;
-    for (int64_t s0 = 0; s0 < S; s0 += per) {
-      const int64_t s1 = std::min(S, s0 + per);
-      afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)c->plan, per,
-                       c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0,
-                       seg(c) ? c->dev_seg->uo : c->dev_tab->consts.sec};
-      hipEvent_t e0 = prof_event(c);
-      HIP_TRY(c, afs::launch_plan(pa, c->stream));
-      hipEvent_t e1 = prof_event(c);
+    if (nch > 1 && (st = ensure(c, &c->plan2, &c->plan2_bytes, pbytes)) != AFS_OK) return st;
+    void *buf[2] = {c->plan, c->plan2};
+    const int two = c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0;
+    const afs::SecRec *uo = seg(c) ? c->dev_seg->uo : c->dev_tab->consts.sec;
+    auto plan_chunk = [&](int64_t k) -> afs_status {
+      const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
+      afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)buf[k & 1], per, two, uo};
+      hipEvent_t e0 = prof_event(c, c->plan_stream);
+      HIP_TRY(c, afs::launch_plan(pa, c->plan_stream));
+      prof_pair(c, e0, prof_event(c, c->plan_stream), 1);
+      HIP_TRY(c, hipEventRecord(c->ev_plan[k & 1], c->plan_stream));
+      return AFS_OK;
+    };
+    // (the frames may have been uploaded on the context's stream just before)
+    HIP_TRY(c, hipEventRecord(c->ev_go, c->stream));
+    HIP_TRY(c, hipStreamWaitEvent(c->plan_stream, c->ev_go, 0));
+    if ((st = plan_chunk(0)) != AFS_OK) return st;
+    for (int64_t k = 0; k < nch; ++k) {
+      if (k + 1 < nch) {
+        if (k >= 1) HIP_TRY(c, hipStreamWaitEvent(c->plan_stream, c->ev_free[(k + 1) & 1], 0));
+        if ((st = plan_chunk(k + 1)) != AFS_OK) return st;
+      }
+      HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_plan[k & 1], 0));
+      const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
-                      (const uint64_t *)c->plan, per, lanes, (double *)ws, B, c->host_tab.uni};
+                      (const uint64_t *)buf[k & 1], per, lanes, (double *)ws, B, c->host_tab.uni};
+      hipEvent_t e1 = prof_event(c);
       if (seg(c)) HIP_TRY(c, afs::launch_seg_synth(afs::SegArgs{a, c->dev_seg}, c->stream));
       else HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
-      hipEvent_t e2 = prof_event(c);
-      prof_pair(c, e0, e1, 1);
-      prof_pair(c, e1, e2, 0);
+      prof_pair(c, e1, prof_event(c), 0);
+      HIP_TRY(c, hipEventRecord(c->ev_free[k & 1], c->stream));
     }
     return AFS_OK;
   }
@@ -222,7 +246,7 @@ void afs_config_default(afs_config *cfg) {
   std::memset(cfg, 0, sizeof *cfg);
   cfg->sampling_rate_hz = 22050.0;
   cfg->precision = AFS_FP64;
-  cfg->solver = AFS_SOLVER_TREE;  // (AFS_SOLVER_SEG once its GPU figures are in: see DESIGN.md 4)
+  cfg->solver = AFS_SOLVER_TREE;  // (the fastest measured: DESIGN.md 4, K1 and the seg kernel)
   cfg->device = 0;
   cfg->flags = 0;
   cfg->options = afs::default_options();
@@ -277,6 +301,9 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
     return bail(AFS_ERR_OUT_OF_MEMORY);
   *ctx->hcount = 0;
   if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return bail(AFS_ERR_HIP);
+  if (hipStreamCreateWithFlags(&ctx->plan_stream, hipStreamNonBlocking) != hipSuccess) return bail(AFS_ERR_HIP);
+  for (hipEvent_t *e : {&ctx->ev_go, &ctx->ev_plan[0], &ctx->ev_plan[1], &ctx->ev_free[0], &ctx->ev_free[1]})
+    if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return bail(AFS_ERR_HIP);
   {
     ctx->plan_budget = PLAN_BUDGET_DEFAULT;
     if (const char *e = std::getenv("AFS_PLAN_BUDGET_MB")) {
@@ -301,7 +328,12 @@ void afs_destroy(afs_ctx *c) {
   if (c->stage_out) (void)hipFree(c->stage_out);
   if (c->stage_seeds) (void)hipFree(c->stage_seeds);
   if (c->tgt) (void)hipFree(c->tgt);
+  if (c->plan_stream) (void)hipStreamSynchronize(c->plan_stream);
   if (c->plan) (void)hipFree(c->plan);
+  if (c->plan2) (void)hipFree(c->plan2);
+  if (c->plan_stream) (void)hipStreamDestroy(c->plan_stream);
+  for (hipEvent_t e : {c->ev_go, c->ev_plan[0], c->ev_plan[1], c->ev_free[0], c->ev_free[1]})
+    if (e) (void)hipEventDestroy(e);
   if (c->stage_nf) (void)hipFree(c->stage_nf);
   if (c->dcount) (void)hipFree(c->dcount);
   if (c->hcount) (void)hipHostFree(c->hcount);

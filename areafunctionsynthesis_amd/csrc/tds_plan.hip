@@ -15,19 +15,20 @@ namespace {
 // (hops >= 128), the frames are staged in LDS first: the plan's scans read every section's
 // area / length / articulator several times, and from LDS those reads cost a fraction of the
 // cache-hit latency of global loads.  Shorter hops (target sequences, hop 1) read the frames
-// from global memory.  The block's records are contiguous in memory: they are assembled in LDS
-// and written with one 16-byte store per lane and step over the whole range (a thread's own
-// 128-B record written directly would spread each store instruction over 64 lines).
+// from global memory.  Each thread stores its own 128-B record with eight 16-byte stores (the
+// block's records are contiguous; L2 merges the partial lines): no LDS for the records, so a K5
+// block (4.3 KB of LDS, 80 VGPRs) fits on a CU beside the synthesis kernel's block, which K5 of
+// the next launch runs concurrently with (afs_capi.cpp run_chunks).  Assembling the records in
+// LDS first for one coalesced store per lane and step measured within 2 %.
 #ifndef AFS_PLAN_BLOCK
 #define AFS_PLAN_BLOCK 256
 #endif
-constexpr int PLAN_BLOCK = AFS_PLAN_BLOCK, PLAN_STAGE = 4, PLAN_PITCH = PLAN_WORDS + 1;  // (odd pitch: fewer bank conflicts)
+constexpr int PLAN_BLOCK = AFS_PLAN_BLOCK, PLAN_STAGE = 4;
 constexpr int FRAME_WORDS = (int)(sizeof(afs_frame) / 8);
 static_assert(sizeof(afs_frame) % 8 == 0, "frames are copied as 8-byte words");
 
 __global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
   __shared__ uint64_t fr_lds[PLAN_STAGE][FRAME_WORDS];
-  __shared__ uint64_t rec_lds[PLAN_BLOCK * PLAN_PITCH];
   const int64_t n = a.s_end - a.s_begin;
   const int64_t row = blockIdx.x;
   const int64_t t_first = (int64_t)blockIdx.y * PLAN_BLOCK;
@@ -56,16 +57,9 @@ __global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
                   a.two_mass != 0, w);
     else
       plan_sample(f + (k - 1), f + k, ratio, a.uo, a.two_mass != 0, w);
+    ulonglong2 *o = (ulonglong2 *)(a.plan + (row * a.plan_stride + t) * PLAN_WORDS);
 #pragma unroll
-    for (int q = 0; q < PLAN_WORDS; ++q) rec_lds[threadIdx.x * PLAN_PITCH + q] = w[q];
-  }
-  __syncthreads();
-  // the block's (t_last - t_first + 1) records, 16 bytes per lane and step
-  const int chunks = (int)(t_last - t_first + 1) * (PLAN_WORDS / 2);
-  ulonglong2 *o = (ulonglong2 *)(a.plan + (row * a.plan_stride + t_first) * PLAN_WORDS);
-  for (int c = threadIdx.x; c < chunks; c += PLAN_BLOCK) {
-    const int r = c / (PLAN_WORDS / 2), q = 2 * (c % (PLAN_WORDS / 2));
-    o[c] = make_ulonglong2(rec_lds[r * PLAN_PITCH + q], rec_lds[r * PLAN_PITCH + q + 1]);
+    for (int q = 0; q < PLAN_WORDS / 2; ++q) o[q] = make_ulonglong2(w[2 * q], w[2 * q + 1]);
   }
 }
 

@@ -29,7 +29,8 @@ for s in $STEPS; do
     calib) (cd /tmp && timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/$OUT/calib -o run -- $R/tools/microbench/fetch_calib) > $OUT/calib.log 2>&1; ok $? calib ;;
     avail) (cd /tmp && timeout -k 10 120 rocprofv3 --list-avail) > $OUT/avail.txt 2>&1; ok $? avail ;;
     mix)   (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 --kernel-trace --output-format csv -d $R/$OUT/pmc_mix1 -o run -- python3 $R/bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline --no-sub-configs) > $OUT/pmc_mix1.log 2>&1; ok $? pmc_mix1
-           (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU_CVT SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --kernel-trace --output-format csv -d $R/$OUT/pmc_mix2 -o run -- python3 $R/bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline --no-sub-configs) > $OUT/pmc_mix2.log 2>&1; ok $? pmc_mix2 ;;
+           (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU_CVT SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --kernel-trace --output-format csv -d $R/$OUT/pmc_mix2 -o run -- python3 $R/bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline --no-sub-configs) > $OUT/pmc_mix2.log 2>&1; ok $? pmc_mix2
+           (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_WAIT_ANY --kernel-trace --output-format csv -d $R/$OUT/pmc_mix3 -o run -- python3 $R/bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline --no-sub-configs) > $OUT/pmc_mix3.log 2>&1; ok $? pmc_mix3 ;;
     pp)    timeout -k 10 300 python tools/phase_prof/run.py --batch 8192 --seconds 0.02 > $OUT/phase_prof.txt 2>&1; ok $? phase_prof; cat $OUT/phase_prof.txt ;;
     spp)   timeout -k 10 300 python tools/phase_prof/seg_run.py --batch 8192 --seconds 0.02 > $OUT/seg_phase_prof.txt 2>&1; ok $? seg_phase_prof; cat $OUT/seg_phase_prof.txt ;;
   esac
