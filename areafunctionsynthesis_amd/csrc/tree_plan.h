@@ -221,6 +221,8 @@ AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double 
           po[c] = p;
         }
       p += l;
+      // (every constriction's section found: the rest of the scan changes nothing)
+      if ((!has[1] || mo[1] >= 0) && (!has[2] || mo[2] >= 0) && (!has[3] || mo[3] >= 0) && mo[0] >= 0) break;
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
