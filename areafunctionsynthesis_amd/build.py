@@ -30,7 +30,12 @@ HEADERS = ["afs_model.h", "afs_ctx.h", "afs_gather.h", "afs_af.h", "afs_lane.h",
 # lanes' loop-invariant comparisons out of the time loop kept ~50 lane masks alive in SGPR
 # pairs, more than the wave has, and their spills cost ~100 v_readlane/v_writelane and ~130
 # AGPR moves per sample (A/B: 89.0 vs 89.25 ms per launch).
-TREE_FLAGS = ["-mllvm", "-disable-machine-licm", "-ffp-contract=fast"]
+# The machine scheduler's iterative-ilp strategy (re-schedules each region for latency once
+# the register budget is known): 25.9 k -> 25.2 k cycles per wave-sample, +1.5-2 % end to
+# end (A/B alternated, profiles/r03k_sched_ab.txt; iterative-minreg -16 %, post-RA machine
+# scheduler / no machine sinking / no memop clustering neutral or slower).  Instruction order
+# only: the results are bit-identical.
+TREE_FLAGS = ["-mllvm", "-disable-machine-licm", "-ffp-contract=fast", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 PER_SOURCE: dict = {"tds_tree.hip": list(TREE_FLAGS), "tds_seg.hip": list(TREE_FLAGS)}
 # (AFS_TREE_FLAGS: extra compiler flags for the tree kernel, for A/B builds of scheduler options)
 if os.environ.get("AFS_TREE_FLAGS"):

@@ -9,17 +9,19 @@ FLAGS=${2:-}
 C=areafunctionsynthesis_amd/csrc
 O=/tmp/afs_variant_$TAG
 mkdir -p $O
+# the tree kernel's flags as build.py TREE_FLAGS (TREE_BASE overrides them, TREE_EXTRA adds)
+TREE_BASE=${TREE_BASE:-"-mllvm -disable-machine-licm -ffp-contract=fast -mllvm -amdgpu-sched-strategy=iterative-ilp"}
 COMMON="-O3 -std=c++17 -fPIC -Wall -Wno-unused-function -ffp-contract=off -fno-strict-aliasing -Wno-unknown-pragmas --offload-arch=gfx950 $FLAGS"
 objs=""
 for s in afs_capi.cpp afs_comm.cpp afs_tables.cpp seg_tables.cpp tds_lane.hip tds_tree.hip tds_seg.hip tds_plan.hip af_kernels.hip audio_kernels.hip; do
   o=$O/${s%.*}.o
   extra=""
-  { [ $s = tds_tree.hip ] || [ $s = tds_seg.hip ]; } && extra="-mllvm -disable-machine-licm -ffp-contract=fast ${TREE_EXTRA:-}"  # (as build.py)
+  { [ $s = tds_tree.hip ] || [ $s = tds_seg.hip ]; } && extra="$TREE_BASE ${TREE_EXTRA:-}"  # (as build.py)
   [ $s = tds_plan.hip ] && extra="${PLAN_EXTRA:-}"
   /opt/rocm/bin/hipcc -c -x hip $C/$s -o $o $COMMON $extra &
   objs="$objs $o"
 done
 wait
 /opt/rocm/bin/hipcc -shared -o areafunctionsynthesis_amd/libafs_$TAG.so --offload-arch=gfx950 -fPIC $objs -ldl
-/opt/rocm/bin/hipcc -shared -o tools/phase_prof/libphase_prof_$TAG.so $COMMON -mllvm -disable-machine-licm -ffp-contract=fast -I$C -Iinclude ${TREE_EXTRA:-} tools/phase_prof/phase_prof.hip -x hip $C/afs_tables.cpp $C/tds_tree.hip $C/tds_plan.hip
+/opt/rocm/bin/hipcc -shared -o tools/phase_prof/libphase_prof_$TAG.so $COMMON $TREE_BASE -I$C -Iinclude ${TREE_EXTRA:-} tools/phase_prof/phase_prof.hip -x hip $C/afs_tables.cpp $C/tds_tree.hip $C/tds_plan.hip
 echo built $TAG
