@@ -89,17 +89,25 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return LIB
 
 
-def kernel_digest() -> str:
-    """Digest of what libafs.so is built from (every source and header, the compiler flags):
-    the committed PMC summaries (profiles/pmc_*.json) are keyed by it, so bench.py quotes a
-    counter figure only for the kernel it is timing."""
+# the headers the synthesis kernels' objects are compiled from (host-only headers excluded)
+KERNEL_HEADERS = {"tds_tree.hip": ["afs_model.h", "afs_tree.h", "tree_core.h", "tree_plan.h", "tree_kernel.h",
+                                   os.path.join("..", "..", "include", "afs.h")],
+                  "tds_seg.hip": ["afs_model.h", "afs_tree.h", "tree_core.h", "tree_plan.h", "seg_model.h",
+                                  "seg_core.h", "seg_kernel.h", "afs_seg.h", os.path.join("..", "..", "include", "afs.h")],
+                  "tds_plan.hip": ["afs_model.h", "afs_tree.h", "tree_plan.h", os.path.join("..", "..", "include", "afs.h")]}
+
+
+def kernel_digest(source: str = "tds_tree.hip") -> str:
+    """Digest of what one kernel's object is built from (the source file, the headers it
+    includes, its compiler flags): the committed PMC summaries (profiles/pmc_*.json) are keyed
+    by it, so bench.py quotes a counter figure only for the kernel it is timing."""
     import hashlib
     h = hashlib.sha1()
-    for f in SOURCES + HEADERS:
+    for f in [source] + KERNEL_HEADERS.get(source, HEADERS):
         h.update(f.encode())
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
-    h.update(repr((COMMON, sorted(PER_SOURCE.items()))).encode())
+    h.update(repr((COMMON, PER_SOURCE.get(source, []))).encode())
     return h.hexdigest()[:12]
 
 

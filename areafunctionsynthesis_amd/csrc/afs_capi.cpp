@@ -113,40 +113,48 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
                       double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B,
                       const int32_t *frame_row = nullptr) {
   if (tree(c)) {
-    // Launch chunks of `per` samples.  K5 (the noise-source plans of chunk k + 1) runs on the
-    // plan stream while K1 synthesizes chunk k on the context's stream: two plan buffers, K5
-    // of chunk k + 1 waits until K1 of chunk k - 1 has read that buffer, K1 of chunk k waits for
-    // its plans.  K5 (80 VGPRs, 4 KB of LDS per block) fits beside K1's wave (432 registers,
-    // 142 KB of LDS per CU) and takes issue slots K1's dependency stalls leave idle.
+    // Launch chunks of `per` samples: K5 (the chunk's noise-source plans), then K1.  With
+    // AFS_PLAN_OVERLAP=1 in the environment (afs_ctx::overlap), K5 of chunk k + 1 runs on the
+    // plan stream beside K1 of chunk k instead: two plan buffers, K5 of chunk k + 1 waits until
+    // K1 of chunk k - 1 has read that buffer, K1 of chunk k waits for its plans.  K5 (80 VGPRs,
+    // 4 KB of LDS per block) fits beside K1's wave, but the measured gain (+1.4 %) came with
+    // runs where K1 slowed by 9 % beside it, so the default is sequential.
     const int64_t S = (int64_t)ntrans * hop;
     const int64_t per = std::max<int64_t>(1, std::min<int64_t>({S, 65536, c->plan_budget / ((int64_t)rows * afs::PLAN_RECORD_BYTES)}));
     const int64_t nch = (S + per - 1) / per;
     const size_t pbytes = (size_t)rows * (size_t)per * afs::PLAN_RECORD_BYTES;
     afs_status st = ensure(c, &c->plan, &c->plan_bytes, pbytes);
     if (st != AFS_OK) return st;
-    if (nch > 1 && (st = ensure(c, &c->plan2, &c->plan2_bytes, pbytes)) != AFS_OK) return st;
-    void *buf[2] = {c->plan, c->plan2};
+    const bool ov = c->overlap && nch > 1;
+    if (ov && (st = ensure(c, &c->plan2, &c->plan2_bytes, pbytes)) != AFS_OK) return st;
+    void *buf[2] = {c->plan, ov ? c->plan2 : c->plan};
+    hipStream_t ps = ov ? c->plan_stream : c->stream;
     const int two = c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0;
     const afs::SecRec *uo = seg(c) ? c->dev_seg->uo : c->dev_tab->consts.sec;
     auto plan_chunk = [&](int64_t k) -> afs_status {
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)buf[k & 1], per, two, uo};
-      hipEvent_t e0 = prof_event(c, c->plan_stream);
-      HIP_TRY(c, afs::launch_plan(pa, c->plan_stream));
-      prof_pair(c, e0, prof_event(c, c->plan_stream), 1);
-      HIP_TRY(c, hipEventRecord(c->ev_plan[k & 1], c->plan_stream));
+      hipEvent_t e0 = prof_event(c, ps);
+      HIP_TRY(c, afs::launch_plan(pa, ps));
+      prof_pair(c, e0, prof_event(c, ps), 1);
+      if (ov) HIP_TRY(c, hipEventRecord(c->ev_plan[k & 1], ps));
       return AFS_OK;
     };
-    // (the frames may have been uploaded on the context's stream just before)
-    HIP_TRY(c, hipEventRecord(c->ev_go, c->stream));
-    HIP_TRY(c, hipStreamWaitEvent(c->plan_stream, c->ev_go, 0));
-    if ((st = plan_chunk(0)) != AFS_OK) return st;
+    if (ov) {  // (the frames may have been uploaded on the context's stream just before)
+      HIP_TRY(c, hipEventRecord(c->ev_go, c->stream));
+      HIP_TRY(c, hipStreamWaitEvent(ps, c->ev_go, 0));
+      if ((st = plan_chunk(0)) != AFS_OK) return st;
+    }
     for (int64_t k = 0; k < nch; ++k) {
-      if (k + 1 < nch) {
-        if (k >= 1) HIP_TRY(c, hipStreamWaitEvent(c->plan_stream, c->ev_free[(k + 1) & 1], 0));
-        if ((st = plan_chunk(k + 1)) != AFS_OK) return st;
+      if (!ov) {
+        if ((st = plan_chunk(k)) != AFS_OK) return st;
+      } else {
+        if (k + 1 < nch) {
+          if (k >= 1) HIP_TRY(c, hipStreamWaitEvent(ps, c->ev_free[(k + 1) & 1], 0));
+          if ((st = plan_chunk(k + 1)) != AFS_OK) return st;
+        }
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_plan[k & 1], 0));
       }
-      HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_plan[k & 1], 0));
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
                       (const uint64_t *)buf[k & 1], per, lanes, (double *)ws, B, c->host_tab.uni};
@@ -154,7 +162,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       if (seg(c)) HIP_TRY(c, afs::launch_seg_synth(afs::SegArgs{a, c->dev_seg}, c->stream));
       else HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
       prof_pair(c, e1, prof_event(c), 0);
-      HIP_TRY(c, hipEventRecord(c->ev_free[k & 1], c->stream));
+      if (ov) HIP_TRY(c, hipEventRecord(c->ev_free[k & 1], c->stream));
     }
     return AFS_OK;
   }
@@ -301,6 +309,7 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
     return bail(AFS_ERR_OUT_OF_MEMORY);
   *ctx->hcount = 0;
   if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return bail(AFS_ERR_HIP);
+  if (const char *e = std::getenv("AFS_PLAN_OVERLAP")) ctx->overlap = std::atoi(e) != 0;
   if (hipStreamCreateWithFlags(&ctx->plan_stream, hipStreamNonBlocking) != hipSuccess) return bail(AFS_ERR_HIP);
   for (hipEvent_t *e : {&ctx->ev_go, &ctx->ev_plan[0], &ctx->ev_plan[1], &ctx->ev_free[0], &ctx->ev_free[1]})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return bail(AFS_ERR_HIP);

@@ -37,7 +37,8 @@ struct afs_ctx {
   size_t plan_bytes = 0;
   void *plan2 = nullptr;  // the second plan buffer: K5 fills one while K1 reads the other
   size_t plan2_bytes = 0;
-  hipStream_t plan_stream = nullptr;  // K5 of the next launch, beside K1 of this one
+  hipStream_t plan_stream = nullptr;  // K5 of the next launch, beside K1 of this one (overlap)
+  bool overlap = false;                // AFS_PLAN_OVERLAP=1 (afs_capi.cpp run_chunks)
   hipEvent_t ev_go = nullptr, ev_plan[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
   int64_t plan_budget = 0;  // bytes of plans one launch may use (afs_capi.cpp)
   void *stage_nf = nullptr;  // per-utterance non-finite flags staged for a host array

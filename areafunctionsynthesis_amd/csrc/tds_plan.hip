@@ -43,6 +43,13 @@ __global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
     const int words = (int)(k_hi - k_lo + 1) * FRAME_WORDS;
     for (int w = threadIdx.x; w < words; w += PLAN_BLOCK) (&fr_lds[0][0])[w] = src[w];
     __syncthreads();
+    // the areas clamped once per frame (Tube::setPharynxMouthGeometry's MIN_AREA, idempotent)
+    // instead of twice per sample and section
+    for (int q = threadIdx.x; q < (int)(k_hi - k_lo + 1) * NPM; q += PLAN_BLOCK) {
+      double *ar = ((afs_frame *)fr_lds[q / NPM])->area_cm2 + q % NPM;
+      *ar = plan_clampA(*ar);
+    }
+    __syncthreads();
   }
   if (t < n) {
     const int64_t s = a.s_begin + t;
@@ -53,8 +60,8 @@ __global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
     // two instantiations of the scans: LDS frames (ds_read) and global frames (global loads);
     // one pointer that may point at either would make every frame read a flat load
     if (staged)
-      plan_sample((const afs_frame *)fr_lds[k - 1 - k_lo], (const afs_frame *)fr_lds[k - k_lo], ratio, a.uo,
-                  a.two_mass != 0, w);
+      plan_sample<true>((const afs_frame *)fr_lds[k - 1 - k_lo], (const afs_frame *)fr_lds[k - k_lo], ratio, a.uo,
+                        a.two_mass != 0, w);
     else
       plan_sample(f + (k - 1), f + k, ratio, a.uo, a.two_mass != 0, w);
     ulonglong2 *o = (ulonglong2 *)(a.plan + (row * a.plan_stride + t) * PLAN_WORDS);

@@ -66,17 +66,23 @@ AFS_HD inline double plan_double(uint64_t b) {
 }
 
 AFS_HD inline double plan_clampA(double a) { return a < AMIN ? AMIN : a; }
+// The scans over the 40 sections unrolled twice: fully unrolled they hold 134 VGPRs with the
+// pre-clamped areas (K5: 57 at unroll 2, 30.5 vs 35.8 ms per step of 8192 utterances x 1 s,
+// DESIGN.md 4).
+#define PLAN_LOOP _Pragma("unroll 2")
 
 // The interpolated pharynx/mouth geometry of one sample, evaluated on demand (no per-thread
 // arrays: K5 keeps its registers for occupancy).  Every value is computed with the operations
 // of tree_core.h phase_interpolate and Tube::calcPositions, with contraction into fmas off in
 // both (the pragmas below and in phase_interpolate), so K5 and the synthesis kernel see the same
 // bits whatever the compiler's -ffp-contract default, and re-evaluation gives the same value.
-struct PlanGeom {
+template <bool PRE>  // PRE: the frames' areas are clamped already (K5's LDS copy)
+struct PlanGeomT {
   const afs_frame *fl, *fr;
   double r1, ratio;
   AFS_HD double area(int m) const {
 #pragma clang fp contract(off)
+    if constexpr (PRE) return plan_clampA(r1 * fl->area_cm2[m] + ratio * fr->area_cm2[m]);
     return plan_clampA(r1 * plan_clampA(fl->area_cm2[m]) + ratio * plan_clampA(fr->area_cm2[m]));
   }
   AFS_HD double len(int m) const {
@@ -92,6 +98,7 @@ struct PlanGeom {
   AFS_HD int argmin(int a, double &amin, int skip_lo = 1, int skip_hi = 0) const {
     int n = -1;
     amin = 1000000.0;
+    PLAN_LOOP
     for (int m = 0; m < NPM; ++m) {
       const double A = area(m);
       if (art(m) == a && A < amin && (m < skip_lo || m > skip_hi)) { amin = A; n = m; }
@@ -125,10 +132,11 @@ struct PlanGeom {
 // constriction, one running position sum for every position the obstacles need, and one
 // obstacle search for all four constrictions.  Every value is the one the separate scans give
 // (the same comparisons and the same sequential sums).
+template <bool PRE = false>
 AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double ratio, const SecRec *sec,
                                bool two_mass, uint64_t *w) {
 #pragma clang fp contract(off)
-  const PlanGeom g{fl, fr, 1.0 - ratio, ratio};
+  const PlanGeomT<PRE> g{fl, fr, 1.0 - ratio, ratio};
   const double teeth = g.r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm;
   const double asp_db = two_mass ? GLOTTIS_DEFAULT_ASPIRATION_DB : g.r1 * fl->glottis[5] + ratio * fr->glottis[5];
 
@@ -136,6 +144,7 @@ AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double 
   // first strict minimum from 1e6
   int n1 = -1, nl = -1;
   double amin1 = 1000000.0, aminl = 1000000.0;
+  PLAN_LOOP
   for (int m = 0; m < NPM; ++m) {
     const double A = g.area(m);
     const int a = g.art(m);
@@ -179,6 +188,7 @@ AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double 
   double P1 = 0.0, P2 = 0.0, P3 = 0.0;
   {
     double p = 0.0;
+    PLAN_LOOP
     for (int m = 0; m <= imax; ++m) {
       if (m == i1) P1 = p;
       if (m == i2) P2 = p;
@@ -212,6 +222,7 @@ AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double 
     int mo[4] = {-1, -1, -1, -1};
     double po[4] = {0.0, 0.0, 0.0, 0.0};
     double p = 0.0;
+    PLAN_LOOP
     for (int m = 0; m < NPM; ++m) {
       const double l = g.len(m);
 #pragma unroll
