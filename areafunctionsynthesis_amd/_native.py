@@ -31,7 +31,7 @@ EXPORTED = (
     "afs_last_error", "afs_set_stream", "afs_synchronize", "afs_synthesize",
     "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_session_destroy",
     "afs_af_to_frames", "afs_to_int16", "afs_target_sequence_default", "afs_target_sequence_samples",
-    "afs_play_target_sequences", "afs_rng_draws", "afs_noise_plans", "afs_session_rng_draws", "afs_kernel_times",
+    "afs_play_target_sequences", "afs_rng_draws", "afs_noise_plans", "afs_tube_interpolate", "afs_session_rng_draws", "afs_kernel_times",
     "afs_shard_range", "afs_comm_unique_id", "afs_comm_create", "afs_comm_create_all", "afs_comm_destroy",
     "afs_gather_pcm", "afs_comm_fence", "afs_comm_synchronize", "afs_multi_synthesize",
 )
@@ -94,6 +94,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.afs_synthesize.argtypes = [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp,
                                    ctypes.POINTER(AfsReport)]
     lib.afs_rng_draws.argtypes = [vp, ctypes.c_int32, vp]
+    lib.afs_tube_interpolate.argtypes = [vp, vp, vp, vp, ctypes.c_int32, vp, vp]
     lib.afs_noise_plans.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                     ctypes.c_int64, vp]
     lib.afs_session_rng_draws.argtypes = [vp, vp]

@@ -508,6 +508,31 @@ afs_status afs_noise_plans(afs_ctx *c, const afs_frame *frames, int32_t rows, in
   return AFS_OK;
 }
 
+afs_status afs_tube_interpolate(afs_ctx *c, const afs_frame *fl, const afs_frame *fr, const double *ratio, int32_t n,
+                                double *area, double *length) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (c->cfg.solver != AFS_SOLVER_TREE) return fail(c, AFS_ERR_UNSUPPORTED, "afs_tube_interpolate: tree solver only");
+  if (!fl || !fr || !ratio || !area || !length || n <= 0)
+    return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_tube_interpolate: need left, right, ratio, area, length, n>0");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  const size_t fb = (size_t)n * sizeof(afs_frame), rb = (size_t)n * 8, ob = (size_t)n * AFS_NUM_TUBE_SECTIONS * 8;
+  char *d = nullptr;
+  HIP_TRY(c, hipMalloc((void **)&d, 2 * fb + rb + 2 * ob));
+  afs_frame *dl = (afs_frame *)d, *dr = (afs_frame *)(d + fb);
+  double *dratio = (double *)(d + 2 * fb), *da = (double *)(d + 2 * fb + rb), *dlen = (double *)(d + 2 * fb + rb + ob);
+  hipError_t e = hipMemcpyAsync(dl, fl, fb, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dr, fr, fb, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dratio, ratio, rb, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(da, 0, 2 * ob, c->stream);
+  if (e == hipSuccess) e = afs::launch_tree_interp(c->dev_tab, dl, dr, dratio, n, da, dlen, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(area, da, ob, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(length, dlen, ob, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d);
+  HIP_TRY(c, e);
+  return AFS_OK;
+}
+
 afs_status afs_session_create(afs_ctx *c, int32_t B, const uint32_t *seeds, afs_session **out) {
   if (!c || !out || B <= 0) return c ? fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_session_create: bad args") : AFS_ERR_INVALID_ARGUMENT;
   HIP_TRY(c, hipSetDevice(c->cfg.device));

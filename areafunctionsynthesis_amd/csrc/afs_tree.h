@@ -58,5 +58,8 @@ hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st);
 hipError_t launch_tree_nonfinite(const double *lds_state, int B, int32_t *count, uint8_t *flags, hipStream_t st);
 hipError_t launch_tree_draws(const double *lds_state, int B, int64_t *draws, hipStream_t st);
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st);
+// diagnostics: the tree kernel's tube interpolation (afs_tube_interpolate)
+hipError_t launch_tree_interp(const Tables *tab, const afs_frame *fl, const afs_frame *fr, const double *ratio, int n,
+                              double *area, double *len, hipStream_t st);
 
 }  // namespace afs

@@ -41,7 +41,41 @@ __global__ void tree_draws_kernel(const double *lds, int B, int64_t *draws) {
   draws[u] = (int64_t)*(const uint64_t *)(lds + (int64_t)u * X_TOTAL + X_NDRAW);
 }
 
+// Diagnostics (afs_tube_interpolate): the synthesis kernel's own frame_load + phase_interpolate,
+// compiled in this file with its flags, for n (frame pair, ratio) samples; thread (i, gl) writes
+// the pharynx/mouth sections of lane gl's slots.  X: a private stand-in of the LDS block's frame
+// values (only X_FRAME .. X_FRAME + 3 are read).
+__global__ void tree_interp_kernel(const Tables *tab, const afs_frame *fl, const afs_frame *fr, const double *ratio,
+                                   int n, double *area, double *len) {
+  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (int64_t)n * TW) return;
+  const int i = (int)(id / TW), gl = (int)(id % TW);
+  Lane<TW> R = Lane<TW>{};
+  double X[X_FRAME + 16];
+  for (int k = 0; k < X_FRAME + 16; ++k) X[k] = 0.0;
+  frame_load<TW>(0, R, X, fl + i, fr + i);  // (lane 0's frame values for every thread)
+  frame_load<TW>(gl, R, X, fl + i, fr + i);
+  phase_interpolate<TW>(gl, R, X, tab->consts, ratio[i]);
+#pragma unroll
+  for (int j = 0; j < Shape<TW>::ND; ++j) {
+    const int m = dyn_section(TW, j, gl) - S_PHARYNX0;
+    if (m >= 0 && m < NPM) {
+      area[(int64_t)i * NPM + m] = R.acur[j];
+      len[(int64_t)i * NPM + m] = R.lcur[j];
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_tree_interp(const Tables *tab, const afs_frame *fl, const afs_frame *fr, const double *ratio, int n,
+                              double *area, double *len, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t t = (int64_t)n * TW;
+  hipLaunchKernelGGL(tree_interp_kernel, dim3((unsigned)((t + 127) / 128)), dim3(128), 0, st, tab, fl, fr, ratio, n,
+                     area, len);
+  return hipGetLastError();
+}
 
 int64_t tree_lane_bytes() { return (int64_t)sizeof(Lane<TW>); }
 int64_t tree_lds_doubles() { return X_TOTAL; }

@@ -149,6 +149,22 @@ class Context:
         _native.check(st, self._h, "afs_noise_plans")
         return out
 
+    def tube_interpolate(self, left: np.ndarray, right: np.ndarray, ratio: np.ndarray):
+        """Diagnostics (tree solver): the synthesis kernel's interpolated pharynx/mouth areas and
+        lengths for frames left[n], right[n] at ratio[n] -> (area[n, 40], length[n, 40])."""
+        left = np.ascontiguousarray(left, dtype=FRAME_DTYPE)
+        right = np.ascontiguousarray(right, dtype=FRAME_DTYPE)
+        ratio = np.ascontiguousarray(ratio, dtype=np.float64)
+        n = ratio.shape[0]
+        if left.shape != (n,) or right.shape != (n,):
+            raise ValueError("left, right and ratio must have n entries")
+        area = np.zeros((n, 40))
+        length = np.zeros((n, 40))
+        st = self._lib.afs_tube_interpolate(self._h, _vp(_addr(left)), _vp(_addr(right)), _vp(_addr(ratio)), n,
+                                            _vp(_addr(area)), _vp(_addr(length)))
+        _native.check(st, self._h, "afs_tube_interpolate")
+        return area, length
+
     def kernel_times(self) -> dict:
         """(profile=True contexts) summed device time and count of the synthesis-kernel and
         noise-source-plan launches since the previous call (waits for the stream)."""

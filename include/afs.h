@@ -175,6 +175,13 @@ afs_status afs_rng_draws(afs_ctx *ctx, int32_t batch, int64_t *draws);
  * (TdsModel.cpp:1188-1508); tests compare it bit for bit with the host restatement.  Other
  * solvers: AFS_ERR_UNSUPPORTED. */
 #define AFS_PLAN_WORDS 16
+/* Diagnostics: Tube::interpolate (Tube.cpp:438-505) of the pharynx/mouth areas and lengths as
+ * the tree solver's synthesis kernel computes them, for n samples: frames left[n] and right[n]
+ * at ratio[n] -> area[n][40], length[n][40] (host pointers).  The reference rounds each product
+ * of r1 * a + ratio * b; so do the kernel and K5 (no fma contraction), which tests check bit for
+ * bit.  Other solvers: AFS_ERR_UNSUPPORTED. */
+afs_status afs_tube_interpolate(afs_ctx *ctx, const afs_frame *left, const afs_frame *right, const double *ratio,
+                                int32_t n, double *area, double *length);
 afs_status afs_noise_plans(afs_ctx *ctx, const afs_frame *frames, int32_t rows, int32_t num_frames, int32_t hop,
                            int64_t s_begin, int64_t s_end, uint64_t *plans);
 

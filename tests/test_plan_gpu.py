@@ -144,3 +144,40 @@ def test_plan_unsupported_solver():
     f = np.zeros((1, 3), dtype=FRAME_DTYPE)
     with pytest.raises(AfsError):
         ctx.noise_plans(f, 10)
+
+
+def test_k1_interpolation_equals_k5_geometry(oracle):
+    """The synthesis kernel's tube interpolation (frame_load + phase_interpolate, compiled in
+    tds_tree.hip with the kernel's -ffp-contract=fast) is bit-identical to the uncontracted
+    r1 * a + ratio * b that K5 (tree_plan.h PlanGeom), the host restatement and the reference
+    (Tube::interpolate, Tube.cpp:438-505) evaluate: the constriction decisions K5 makes are made
+    on the areas the tube network uses."""
+    from areafunctionsynthesis_amd.params import default_shapes
+    from areafunctionsynthesis_amd.synthesizer import Context
+    sh = default_shapes()
+    rng = np.random.default_rng(7)
+    names = sorted(sh)
+    n = 4096
+    left = np.stack([oracle.af_to_frame(sh[names[k]]) for k in rng.integers(0, len(names), n)])
+    right = np.stack([oracle.af_to_frame(sh[names[k]]) for k in rng.integers(0, len(names), n)])
+    # areas below MIN_AREA on both sides (the clamps), and the ratios of every hop used
+    left["area_cm2"][::7, 5] = 1e-5
+    right["area_cm2"][::5, 6] = -0.3
+    ratio = np.concatenate([np.arange(441) / 441.0, rng.random(n - 441)])
+    ctx = Context(22050.0, solver="tree")
+    area, length = ctx.tube_interpolate(left, right, ratio)
+    amin = 0.001
+    aL = np.maximum(left["area_cm2"], amin)
+    aR = np.maximum(right["area_cm2"], amin)
+    r1 = (1.0 - ratio)[:, None]
+    r = ratio[:, None]
+    a_ref = r1 * aL + r * aR  # numpy rounds each product: no fma
+    a_ref = np.where(a_ref < amin, amin, a_ref)
+    l_ref = r1 * left["length_cm"] + r * right["length_cm"]
+    assert np.array_equal(area, a_ref), int(np.count_nonzero(area != a_ref))
+    assert np.array_equal(length, l_ref), int(np.count_nonzero(length != l_ref))
+    # (the check has teeth: a contracted fma(r1, a, ratio * b) -- evaluated here in extended
+    # precision -- rounds differently for a share of these inputs)
+    ld = np.longdouble
+    a_fma = (ld(1.0) * r1.astype(ld) * aL.astype(ld) + (r * aR).astype(ld)).astype(np.float64)
+    assert np.count_nonzero(a_fma != r1 * aL + r * aR) > 0
