@@ -20,7 +20,9 @@ HEADERS = ["afs_model.h", "afs_ctx.h", "afs_gather.h", "afs_af.h", "afs_lane.h",
            "seg_model.h", "seg_core.h", "seg_kernel.h", "afs_seg.h",
            os.path.join("..", "..", "include", "afs.h")]
 # Per-source extra flags.
-# The tree kernel contracts a*b+c into fma (-ffp-contract=fast after COMMON's =off): 8 % fewer
+# The tree kernel contracts a*b+c into fma (-ffp-contract=fast-honor-pragmas after COMMON's
+# =off; plain "fast" ignores the `#pragma clang fp contract(off)` that keeps the tube
+# interpolation uncontracted like K5's and the reference's, tests/test_plan_gpu.py): 8 % fewer
 # VALU instructions in its time loop, +3.5 % end to end (A/B, profiles/r02ac_contract_ab.txt);
 # its results stay within the parity tolerances (the reference's own build with FMA
 # contraction differs from its -O2 build by up to 5.7e-9 over a second).  The
@@ -35,7 +37,7 @@ HEADERS = ["afs_model.h", "afs_ctx.h", "afs_gather.h", "afs_af.h", "afs_lane.h",
 # end (A/B alternated, profiles/r03k_sched_ab.txt; iterative-minreg -16 %, post-RA machine
 # scheduler / no machine sinking / no memop clustering neutral or slower).  Instruction order
 # only: the results are bit-identical.
-TREE_FLAGS = ["-mllvm", "-disable-machine-licm", "-ffp-contract=fast", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+TREE_FLAGS = ["-mllvm", "-disable-machine-licm", "-ffp-contract=fast-honor-pragmas", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 PER_SOURCE: dict = {"tds_tree.hip": list(TREE_FLAGS), "tds_seg.hip": list(TREE_FLAGS)}
 # (AFS_TREE_FLAGS: extra compiler flags for the tree kernel, for A/B builds of scheduler options)
 if os.environ.get("AFS_TREE_FLAGS"):

@@ -148,7 +148,7 @@ def test_plan_unsupported_solver():
 
 def test_k1_interpolation_equals_k5_geometry(oracle):
     """The synthesis kernel's tube interpolation (frame_load + phase_interpolate, compiled in
-    tds_tree.hip with the kernel's -ffp-contract=fast) is bit-identical to the uncontracted
+    tds_tree.hip with the kernel's -ffp-contract=fast-honor-pragmas) is bit-identical to the uncontracted
     r1 * a + ratio * b that K5 (tree_plan.h PlanGeom), the host restatement and the reference
     (Tube::interpolate, Tube.cpp:438-505) evaluate: the constriction decisions K5 makes are made
     on the areas the tube network uses."""
