@@ -149,13 +149,20 @@ struct ArmCarry {
 struct D4 { double v[4]; };
 
 
-// 1/d for the pivots: v_rcp_f64 and two Newton steps on the device (within an ulp of the
-// division, a fraction of its latency); plain division in the CPU emulator.
+// 1/d for the pivots, areas and surfaces: v_rcp_f64 and one Newton step on the device (within
+// 11 ulps of the division, profiles/r02ad_f64_ops.txt).  A second step makes it exactly rounded;
+// dropping it measured +2.3 % end to end (profiles/r03s_rcp_rows_ab.txt) with the parity
+// figures still 5-6 orders inside the bounds and 0 rand() count differences.
+// Plain division in the CPU emulator.
+#ifndef AFS_RCP_NEWTON
+#define AFS_RCP_NEWTON 1
+#endif
 AFS_HD inline double pivot_recip(double d) {
 #if defined(__HIP_DEVICE_COMPILE__)
   double r = __builtin_amdgcn_rcp(d);
   double e = fma(-d, r, 1.0);
   r = fma(r, e, r);
+  if constexpr (AFS_RCP_NEWTON == 1) return r;
   e = fma(-d, r, 1.0);
   return fma(r, e, r);
 #else
@@ -1094,7 +1101,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
                               const Uni &U, const Consts &C) {
   // X (reads) and Xw (writes) are the same utterance block; the phase writes only the
   // solver arrays (X_DIAG, X_RHS, X_OFF), which it never reads.  The slot loop is one
-  // branch-free block: both row forms are evaluated and selected per lane, an absent slot
+  // branch-free block: one row form serves simple and bifurcation rows, an absent slot
   // writes into the sink slots; the radiation rows follow.
   using S = Shape<W>;
   const double idt = C.h.inv_dtTH;
@@ -1139,28 +1146,25 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     double Sx = 0.0;
     Sx -= xsx[j];  // dipole sample (pharynx/mouth) or the lung pressure (section 0)
     const double uu = R.u[j], uur = R.ur[j];
-    // the source section bifurcates: its other output is current br
+    // the source section bifurcates: its other output is current br (else the zero slot: 0.0)
     const double uD = xub[j], uDr = xurb[j];
-    const double Fb = LAB0 * idt + RAB;
-    const double Hb = -idt * (LAB0 * uu + LA * uD) - (TH1 / TH) * (LAB0 * uur + LA * uDr) + Sx;
-    const double mb = -EB - EA - Fb;
-    const double rb = Hb + DB - DA;
-    // simple junction, with Sondhi's inner length correction between pharynx/mouth sections
+    // One row form for both cases: the bifurcation form (:1913-1965) with the partner's flows
+    // 0.0 is the simple junction (:1966-2001), whose inductance may carry Sondhi's inner
+    // length correction between pharynx/mouth sections.
     double LAB = LAB0;
     if (dyn) {
       const double jl = junction_l(xrad[j], X[X_RAD + s - DYN0]);
-      const bool use = (opt.inner_length_corrections != 0) & ((q.flags & SR_JUNCTION) != 0);
+      const bool use = (opt.inner_length_corrections != 0) & ((q.flags & SR_JUNCTION) != 0) & ((q.flags & SR_BIF) == 0);
       LAB = use ? LAB + jl : LAB;  // (a select: no branch around the radii loads)
     }
     const double G = LAB * idt + RAB;
-    const double H = -uur * LAB * (TH1 / TH) - (LAB * uu) * idt + Sx;
+    const double H = -idt * (LAB * uu + LA * uD) - (TH1 / TH) * (LAB * uur + LA * uDr) + Sx;
     double m = -EB - G;
     m -= EA;    // 0.0 without a source
     double rhs = H + DB;
     rhs -= DA;  // 0.0 without a source
-    const bool bif = (q.flags & SR_BIF) != 0;
-    Xw[X_DIAG + i] = -(bif ? mb : m);
-    Xw[X_RHS + i] = -(bif ? rb : rhs);
+    Xw[X_DIAG + i] = -m;
+    Xw[X_RHS + i] = -rhs;
     // edges of section s: (in, out0) = -E, (in, out1) = -E, (out0, out1) = E + L/(dt th) + R1
     xat(Xw, q.x_e0) = -EB;
     xat(Xw, q.x_e1) = -EB;
