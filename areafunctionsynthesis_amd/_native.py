@@ -20,6 +20,8 @@ AFS_SOLVER_TREE = 1
 AFS_SOLVER_SOR = 2
 AFS_SOLVER_SEG = 3
 AFS_PLAN_WORDS = 16  # afs.h
+AFS_PLAN_HOP_BYTES = 544  # afs.h
+AFS_PLAN_HOP_MIN = 32  # afs.h
 AFS_FP64 = 0
 AFS_ASYNC = 0x1
 AFS_PROFILE = 0x2
@@ -31,7 +33,7 @@ EXPORTED = (
     "afs_last_error", "afs_set_stream", "afs_synchronize", "afs_synthesize",
     "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_session_destroy",
     "afs_af_to_frames", "afs_to_int16", "afs_target_sequence_default", "afs_target_sequence_samples",
-    "afs_play_target_sequences", "afs_rng_draws", "afs_noise_plans", "afs_tube_interpolate", "afs_session_rng_draws", "afs_kernel_times",
+    "afs_play_target_sequences", "afs_rng_draws", "afs_noise_plans", "afs_noise_plan_hops", "afs_tube_interpolate", "afs_session_rng_draws", "afs_kernel_times",
     "afs_shard_range", "afs_comm_unique_id", "afs_comm_create", "afs_comm_create_all", "afs_comm_destroy",
     "afs_gather_pcm", "afs_comm_fence", "afs_comm_synchronize", "afs_multi_synthesize",
 )
@@ -97,6 +99,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.afs_tube_interpolate.argtypes = [vp, vp, vp, vp, ctypes.c_int32, vp, vp]
     lib.afs_noise_plans.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                     ctypes.c_int64, vp]
+    lib.afs_noise_plan_hops.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
+                                        ctypes.c_int64, vp, vp]
     lib.afs_session_rng_draws.argtypes = [vp, vp]
     lib.afs_session_create.argtypes = [vp, ctypes.c_int32, vp, ctypes.POINTER(vp)]
     lib.afs_session_synthesize.argtypes = [vp, vp, ctypes.c_int32, vp, vp, ctypes.POINTER(ctypes.c_int32),

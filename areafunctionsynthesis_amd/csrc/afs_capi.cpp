@@ -128,14 +128,27 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     const bool ov = c->overlap && nch > 1;
     if (ov && (st = ensure(c, &c->plan2, &c->plan2_bytes, pbytes)) != AFS_OK) return st;
     void *buf[2] = {c->plan, ov ? c->plan2 : c->plan};
+    // hop mode (tree solver, hops >= PLAN_HOP_MIN): K5 writes one record per (row, hop) and the
+    // dense records of mixed hops only; K1 evaluates the words from the hop records
+    const bool hops = !seg(c) && !c->plan_dense && hop >= afs::tree::PLAN_HOP_MIN;
+    const int64_t hstride = afs::plan_hop_slots(0, per, hop) + 1;  // (a chunk may start inside a hop)
+    afs::tree::PlanHop *hbuf[2] = {nullptr, nullptr};
+    if (hops) {
+      const size_t hbytes = (size_t)rows * (size_t)hstride * sizeof(afs::tree::PlanHop);
+      for (int q = 0; q < (ov ? 2 : 1); ++q)
+        if ((st = ensure(c, &c->hops[q], &c->hops_bytes[q], hbytes)) != AFS_OK) return st;
+      hbuf[0] = (afs::tree::PlanHop *)c->hops[0];
+      hbuf[1] = (afs::tree::PlanHop *)c->hops[ov ? 1 : 0];
+    }
     hipStream_t ps = ov ? c->plan_stream : c->stream;
     const int two = c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0;
     const afs::SecRec *uo = seg(c) ? c->dev_seg->uo : c->dev_tab->consts.sec;
     auto plan_chunk = [&](int64_t k) -> afs_status {
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
-      afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)buf[k & 1], per, two, uo};
+      afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)buf[k & 1], per, two, uo,
+                       hbuf[k & 1], hstride};
       hipEvent_t e0 = prof_event(c, ps);
-      HIP_TRY(c, afs::launch_plan(pa, ps));
+      HIP_TRY(c, hops ? afs::launch_plan_hops(pa, ps) : afs::launch_plan(pa, ps));
       prof_pair(c, e0, prof_event(c, ps), 1);
       if (ov) HIP_TRY(c, hipEventRecord(c->ev_plan[k & 1], ps));
       return AFS_OK;
@@ -157,7 +170,8 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       }
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
-                      (const uint64_t *)buf[k & 1], per, lanes, (double *)ws, B, c->host_tab.uni};
+                      (const uint64_t *)buf[k & 1], per, lanes, (double *)ws, B, c->host_tab.uni,
+                      hbuf[k & 1], hstride};
       hipEvent_t e1 = prof_event(c);
       if (seg(c)) HIP_TRY(c, afs::launch_seg_synth(afs::SegArgs{a, c->dev_seg}, c->stream));
       else HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
@@ -310,6 +324,7 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   *ctx->hcount = 0;
   if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return bail(AFS_ERR_HIP);
   if (const char *e = std::getenv("AFS_PLAN_OVERLAP")) ctx->overlap = std::atoi(e) != 0;
+  if (const char *e = std::getenv("AFS_PLAN_DENSE")) ctx->plan_dense = std::atoi(e) != 0;
   if (hipStreamCreateWithFlags(&ctx->plan_stream, hipStreamNonBlocking) != hipSuccess) return bail(AFS_ERR_HIP);
   for (hipEvent_t *e : {&ctx->ev_go, &ctx->ev_plan[0], &ctx->ev_plan[1], &ctx->ev_free[0], &ctx->ev_free[1]})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return bail(AFS_ERR_HIP);
@@ -340,6 +355,8 @@ void afs_destroy(afs_ctx *c) {
   if (c->plan_stream) (void)hipStreamSynchronize(c->plan_stream);
   if (c->plan) (void)hipFree(c->plan);
   if (c->plan2) (void)hipFree(c->plan2);
+  for (void *h : c->hops)
+    if (h) (void)hipFree(h);
   if (c->plan_stream) (void)hipStreamDestroy(c->plan_stream);
   for (hipEvent_t e : {c->ev_go, c->ev_plan[0], c->ev_plan[1], c->ev_free[0], c->ev_free[1]})
     if (e) (void)hipEventDestroy(e);
@@ -504,6 +521,50 @@ afs_status afs_noise_plans(afs_ctx *c, const afs_frame *frames, int32_t rows, in
                    seg(c) ? c->dev_seg->uo : c->dev_tab->consts.sec};
   HIP_TRY(c, afs::launch_plan(pa, c->stream));
   if (host_out) HIP_TRY(c, hipMemcpyAsync(plans, dplans, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return AFS_OK;
+}
+
+afs_status afs_noise_plan_hops(afs_ctx *c, const afs_frame *frames, int32_t rows, int32_t F, int32_t hop, int64_t s0,
+                               int64_t s1, uint8_t *hops, uint64_t *plans) {
+  static_assert(AFS_PLAN_HOP_BYTES == sizeof(afs::tree::PlanHop), "afs.h / tree_plan.h hop record size");
+  static_assert(AFS_PLAN_HOP_MIN == afs::tree::PLAN_HOP_MIN, "afs.h / tree_plan.h hop mode threshold");
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (c->cfg.solver != AFS_SOLVER_TREE || hop < AFS_PLAN_HOP_MIN)
+    return fail(c, AFS_ERR_UNSUPPORTED, "afs_noise_plan_hops: tree solver and hop >= AFS_PLAN_HOP_MIN only");
+  if (!frames || !hops || !plans || rows <= 0 || F < 2 || s0 < 0 || s1 <= s0 || s1 > (int64_t)(F - 1) * hop)
+    return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_noise_plan_hops: need frames, hops, plans, rows>0, num_frames>=2, "
+                                             "0 <= s_begin < s_end <= (num_frames-1)*hop");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  afs_status s;
+  const afs_frame *dframes = frames;
+  if (!is_device_ptr(frames)) {
+    const size_t bytes = (size_t)rows * F * sizeof(afs_frame);
+    if ((s = ensure(c, &c->stage_in, &c->stage_in_bytes, bytes)) != AFS_OK) return s;
+    HIP_TRY(c, hipMemcpyAsync(c->stage_in, frames, bytes, hipMemcpyHostToDevice, c->stream));
+    dframes = (const afs_frame *)c->stage_in;
+  }
+  const int64_t n = s1 - s0, slots = afs::plan_hop_slots(s0, s1, hop);
+  const size_t pbytes = (size_t)rows * (size_t)n * afs::PLAN_RECORD_BYTES;
+  const size_t hbytes = (size_t)rows * (size_t)slots * sizeof(afs::tree::PlanHop);
+  uint64_t *dplans = plans;
+  uint8_t *dhops = hops;
+  const bool host_plans = !is_device_ptr(plans), host_hops = !is_device_ptr(hops);
+  if (host_plans) {
+    if ((s = ensure(c, &c->plan, &c->plan_bytes, pbytes)) != AFS_OK) return s;
+    dplans = (uint64_t *)c->plan;
+    HIP_TRY(c, hipMemcpyAsync(dplans, plans, pbytes, hipMemcpyHostToDevice, c->stream));
+  }
+  if (host_hops) {
+    if ((s = ensure(c, &c->hops[0], &c->hops_bytes[0], hbytes)) != AFS_OK) return s;
+    dhops = (uint8_t *)c->hops[0];
+  }
+  afs::PlanArgs pa{c->dev_tab, dframes, F, rows, hop, s0, s1, dplans, n,
+                   c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0, c->dev_tab->consts.sec,
+                   (afs::tree::PlanHop *)dhops, slots};
+  HIP_TRY(c, afs::launch_plan_hops(pa, c->stream));
+  if (host_plans) HIP_TRY(c, hipMemcpyAsync(plans, dplans, pbytes, hipMemcpyDeviceToHost, c->stream));
+  if (host_hops) HIP_TRY(c, hipMemcpyAsync(hops, dhops, hbytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return AFS_OK;
 }

@@ -37,6 +37,9 @@ struct afs_ctx {
   size_t plan_bytes = 0;
   void *plan2 = nullptr;  // the second plan buffer: K5 fills one while K1 reads the other
   size_t plan2_bytes = 0;
+  void *hops[2] = {nullptr, nullptr};  // tree solver, hops >= PLAN_HOP_MIN: hop records (tree_plan.h PlanHop)
+  size_t hops_bytes[2] = {0, 0};
+  bool plan_dense = false;             // AFS_PLAN_DENSE=1: dense records at every hop (A/B, tests)
   hipStream_t plan_stream = nullptr;  // K5 of the next launch, beside K1 of this one (overlap)
   bool overlap = false;                // AFS_PLAN_OVERLAP=1 (afs_capi.cpp run_chunks)
   hipEvent_t ev_go = nullptr, ev_plan[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "afs_model.h"
+#include "tree_plan.h"
 
 namespace afs {
 
@@ -24,6 +25,11 @@ struct TreeArgs {
   double *lds_state;        // per-utterance LDS block, B * tree_lds_doubles()
   int B;
   Uni uni;                  // copy of tab->uni: scalar kernel arguments
+  // hop records (tree_plan.h PlanHop; null: every sample reads its dense record):
+  // hops[row(u) * hop_stride + s / hop - s_begin / hop]; the dense records are written for the
+  // samples of mixed hops only
+  const tree::PlanHop *hops = nullptr;
+  int64_t hop_stride = 0;
 };
 // K5: the noise-source plans of samples [s_begin, s_end) of `rows` frame rows.
 struct PlanArgs {
@@ -37,8 +43,12 @@ struct PlanArgs {
   int two_mass;
   const SecRec *uo;         // the synthesis kernel's LDS offsets of the section outputs' noise-
                             // smoothed flows (tree: tab->consts.sec; seg: SegTables::uo)
+  tree::PlanHop *hops = nullptr;  // hop mode (launch_plan_hops): as TreeArgs::hops
+  int64_t hop_stride = 0;
 };
 constexpr int64_t PLAN_RECORD_BYTES = 128;
+// Hop slots a launch of samples [s0, s1) spans.
+inline int64_t plan_hop_slots(int64_t s0, int64_t s1, int hop) { return (s1 - 1) / hop - s0 / hop + 1; }
 
 #ifndef AFS_TREE_W
 #define AFS_TREE_W 16
@@ -58,6 +68,8 @@ hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st);
 hipError_t launch_tree_nonfinite(const double *lds_state, int B, int32_t *count, uint8_t *flags, hipStream_t st);
 hipError_t launch_tree_draws(const double *lds_state, int B, int64_t *draws, hipStream_t st);
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st);
+// K5 in hop mode: the hop records of the launch's hops, the dense records of its mixed hops
+hipError_t launch_plan_hops(const PlanArgs &a, hipStream_t st);
 // diagnostics: the tree kernel's tube interpolation (afs_tube_interpolate)
 hipError_t launch_tree_interp(const Tables *tab, const afs_frame *fl, const afs_frame *fr, const double *ratio, int n,
                               double *area, double *len, hipStream_t st);

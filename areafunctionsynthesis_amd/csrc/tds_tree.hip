@@ -9,11 +9,12 @@ using namespace tree;
 
 namespace {
 
-// one kernel per glottis model (TriangularGlottis, the reference's; TwoMassModel)
-template <int MODEL>
+// one kernel per glottis model (TriangularGlottis, the reference's; TwoMassModel) and plan mode
+// (HOPS: hop records, hops >= PLAN_HOP_MIN; dense records otherwise)
+template <int MODEL, bool HOPS>
 __global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_synth_kernel(TreeArgs a) {
   __shared__ WaveLds lds;
-  tree_synth_body<false, MODEL>(a, lds, nullptr);
+  tree_synth_body<false, MODEL, HOPS>(a, lds, nullptr);
 }
 
 // seeds == nullptr: utterance u is seeded u + 1 (afs.h)
@@ -90,10 +91,15 @@ hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const u
 
 hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st) {
   if (a.B <= 0 || a.s_end <= a.s_begin) return hipSuccess;
-  if (a.uni.opt.glottis_model == AFS_GLOTTIS_TWO_MASS)
-    hipLaunchKernelGGL(tree_synth_kernel<AFS_GLOTTIS_TWO_MASS>, dim3((a.B + UPB - 1) / UPB), dim3(64 * WPB), 0, st, a);
-  else
-    hipLaunchKernelGGL(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR>, dim3((a.B + UPB - 1) / UPB), dim3(64 * WPB), 0, st, a);
+  const dim3 grid((a.B + UPB - 1) / UPB), block(64 * WPB);
+  const bool two = a.uni.opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
+  if (a.hops) {
+    if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true>), grid, block, 0, st, a);
+  } else {
+    if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, false>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false>), grid, block, 0, st, a);
+  }
   return hipGetLastError();
 }
 

@@ -205,6 +205,32 @@ AFS_HD inline double fast_div(double a, double b) {
 #endif
 }
 
+// Word `kind` of a hop record at `ratio` (tree_plan.h plan_word_eval), branch-free on the
+// device: every lane evaluates one square root and one quotient and keeps its kind's value.
+// The interpolation is K5's and phase_interpolate's (uncontracted); the square roots are exact
+// (fast_sqrt), the quotients within an ulp of K5's divisions (fast_div).
+AFS_HD inline uint64_t plan_word_fast(uint32_t kind, const double *p, double ratio) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double x, y;
+  {
+#pragma clang fp contract(off)
+    const double r1 = 1.0 - ratio;
+    x = r1 * p[0] + ratio * p[1];
+    y = r1 * p[2] + ratio * p[3];
+  }
+  double a = x < AMIN ? AMIN : x;
+  a = a < 0.1 ? 0.1 : a;
+  const bool invd = kind == PK_INVD, fdn = kind == PK_FDN;
+  // (a constant word's inputs are no area: its lane computes on them and discards the value)
+  const double s = fast_sqrt(invd ? (4.0 * a) * (1.0 / PI) : a);
+  const double q = fast_div(fdn ? x : 1.0, fdn ? y : (invd ? s : a));
+  const double v = kind == PK_SQRT ? s : q;
+  return kind == PK_CONST ? plan_bits(p[0]) : plan_bits(v);
+#else
+  return plan_word_eval(kind, p, ratio);
+#endif
+}
+
 // The double at LDS byte offset b of an utterance block (SecRec / ArmRec fields).
 AFS_HD inline double &xat(double *X, uint32_t b) { return *reinterpret_cast<double *>(reinterpret_cast<char *>(X) + b); }
 AFS_HD inline const double &xat(const double *X, uint32_t b) {

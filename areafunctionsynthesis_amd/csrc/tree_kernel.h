@@ -170,7 +170,10 @@ struct WaveLds {
 };
 
 // prof (PROF only): per wave, PH_COUNT cycle sums (s_memtime) over the launch.
-template <bool PROF, int MODEL>
+// HOPS: the plan words come from hop records (a.hops, tree_plan.h PlanHop): lane gl keeps word
+// gl's kind and inputs for the hop and evaluates the word at every sample; a mixed hop's samples
+// read their dense records as without HOPS.
+template <bool PROF, int MODEL, bool HOPS = false>
 __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds, uint64_t *prof) {
   const int lane = threadIdx.x;  // 0 .. 64 WPB - 1
   const int g = lane / TW, gl = lane % TW;
@@ -204,13 +207,34 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   // that ends inside a hop filters the part it has
   const bool defer = hop >= OUT_DEFER_MIN_HOP;
   frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
+  // hop mode: this hop's record (word gl % 16: its kind and inputs; whether the hop is mixed)
+  const PlanHop *hr = HOPS ? a.hops + row * a.hop_stride : nullptr;
+  double hp[4] = {0.0, 0.0, 0.0, 0.0};
+  uint32_t hkind = PK_CONST;
+  bool hmixed = !HOPS;
+  auto hop_load = [&](const PlanHop *h) {
+    const double2 *q = reinterpret_cast<const double2 *>(h->p[gl & (PLAN_WORDS - 1)]);
+    const double2 v0 = q[0], v1 = q[1];
+    hp[0] = v0.x; hp[1] = v0.y; hp[2] = v1.x; hp[3] = v1.y;
+    hkind = h->kind[gl & (PLAN_WORDS - 1)];
+    hmixed = h->mixed != 0;
+  };
+  if constexpr (HOPS) hop_load(hr);
   ex.sync();
-  uint64_t next = pl[0];
+  uint64_t next = hmixed ? pl[0] : 0;
   int64_t t0 = 0;
   for (int64_t t = 0; t < n; ++t) {
-    R.planw = next;
-    next = pl[(t + 1 < n ? t + 1 : t) * PLAN_WORDS];  // the next sample's word, a sample ahead
     const double ratio = (double)i / (double)hop;
+    const int64_t tn = t + 1 < n ? t + 1 : t;
+    if constexpr (HOPS) {
+      const uint64_t ev = plan_word_fast(hkind, hp, ratio);
+      R.planw = hmixed ? next : ev;
+      // (a hop that is not mixed reads its own record's first word: a cache hit, no branch)
+      next = *(hmixed ? pl + tn * PLAN_WORDS : reinterpret_cast<const uint64_t *>(hr));
+    } else {
+      R.planw = next;
+      next = pl[tn * PLAN_WORDS];  // the next sample's word, a sample ahead
+    }
     sample_step<TW, MODEL>(ex, X, a.uni, C, ratio, defer);
     if (valid && gl == 0) o[t] = R.sample;
     if (++i == hop) {
@@ -218,7 +242,13 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
       t0 = t + 1;
       i = 0;
       ++k;
-      if (t + 1 < n) frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
+      if (t + 1 < n) {
+        frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
+        if constexpr (HOPS) {
+          hop_load(++hr);
+          if (hmixed) next = pl[(t + 1) * PLAN_WORDS];
+        }
+      }
       ex.sync();
     }
   }

@@ -124,22 +124,37 @@ struct PlanGeomT {
   }
 };
 
-// The plan of the sample at `ratio` between frames fl and fr.  sec: the kernel tables' section
-// records (X_UN offsets of the section outputs).  two_mass: the glottis is the TwoMassModel,
-// whose aspiration strength is Glottis::DEFAULT_ASPIRATION_STRENGTH_DB.
+// The discrete decisions of one sample's plan: which sections are the narrowest ones, where the
+// constrictions end, which obstacle formula applies and in which section each obstacle lies.
+// Everything else in the record is a continuous function of the interpolated geometry.
+struct PlanKey {
+  int n1, n2, nl;   // narrowest tongue section, second tongue constriction's, lower lip's (-1: none)
+  int l1, l2, ll;   // last sections of the three extents (-1: none)
+  int mo[4];        // obstacle section of glottis, tongue 1, tongue 2, lip (-1: none)
+  bool has_t1, has_t2, lip_c, has_l;
+  bool tb1, tb2;    // the tongue obstacle is the teeth (:1283-1299)
+  uint32_t flags;   // PF_*
+};
+// Two 64-bit words that are equal iff the keys are.
+AFS_HD inline void plan_key_pack(const PlanKey &k, uint64_t *q) {
+  auto b6 = [](int v) { return (uint64_t)(uint32_t)(v + 1) & 63u; };  // -1 .. 62
+  q[0] = b6(k.n1) | b6(k.n2) << 6 | b6(k.nl) << 12 | b6(k.l1) << 18 | b6(k.l2) << 24 | b6(k.ll) << 30 |
+         b6(k.mo[0]) << 36 | b6(k.mo[1]) << 42 | b6(k.mo[2]) << 48 | b6(k.mo[3]) << 54;
+  q[1] = (uint64_t)k.flags | (uint64_t)k.has_t1 << 8 | (uint64_t)k.has_t2 << 9 | (uint64_t)k.lip_c << 10 |
+         (uint64_t)k.has_l << 11 | (uint64_t)k.tb1 << 12 | (uint64_t)k.tb2 << 13;
+}
+
+// The discrete decisions at one sample (g: its interpolated geometry, teeth: its interpolated
+// teeth position) and the obstacle positions / the positions of the obstacle sections that go
+// into the downstream factors.
 // The reference's scans (argmin, extent, position, obstacle) are merged into four passes over
 // the 40 sections: the narrowest tongue and lip sections together, the second tongue
 // constriction, one running position sum for every position the obstacles need, and one
 // obstacle search for all four constrictions.  Every value is the one the separate scans give
 // (the same comparisons and the same sequential sums).
-template <bool PRE = false>
-AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double ratio, const SecRec *sec,
-                               bool two_mass, uint64_t *w) {
+template <bool PRE>
+AFS_HD inline void plan_decide(const PlanGeomT<PRE> &g, double teeth, PlanKey &key, double *obst, double *po) {
 #pragma clang fp contract(off)
-  const PlanGeomT<PRE> g{fl, fr, 1.0 - ratio, ratio};
-  const double teeth = g.r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm;
-  const double asp_db = two_mass ? GLOTTIS_DEFAULT_ASPIRATION_DB : g.r1 * fl->glottis[5] + ratio * fr->glottis[5];
-
   // narrowest tongue section (:1228-1240) and narrowest lower-lip section (:1399-1410): the
   // first strict minimum from 1e6
   int n1 = -1, nl = -1;
@@ -199,29 +214,33 @@ AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double 
   // obstacles of the tongue constrictions (:1283-1299): the teeth when the jet ends within
   // 2 cm of them, else the middle of the section after the constriction
   double min_teeth = 1000000.0;
-  auto tongue_obstacle = [&](double pl, int last, int narrow) {
+  bool tb[2] = {false, false};
+  auto tongue_obstacle = [&](double pl, int last, int narrow, bool &at_teeth) {
     const double jet = pl + g.len(last);
     if (teeth - jet < 2.0) {
       min_teeth = g.area(narrow);
+      at_teeth = true;
       return teeth;
     }
     return (pl + g.len(last)) + 0.5 * g.len(last + 1);  // pos[last + 1] + 0.5 len[last + 1]
   };
-  if (has_t1) obst1 = tongue_obstacle(P1, l1, n1);
-  if (has_t2) obst2 = tongue_obstacle(P2, l2, n2);
+  if (has_t1) obst1 = tongue_obstacle(P1, l1, n1, tb[0]);
+  if (has_t2) obst2 = tongue_obstacle(P2, l2, n2, tb[1]);
   // the lower lip counts when narrower than a tongue constriction at the teeth
   const bool has_l = lip_c && aminl < min_teeth;
   const double obstl = has_l ? P3 : 0.0;
 
-  // obstacle sections and source weights (:1456-1499)
-  const double obst[4] = {1.5, obst1, obst2, obstl};
+  // obstacle sections (:1456-1499)
+  obst[0] = 1.5;
+  obst[1] = obst1;
+  obst[2] = obst2;
+  obst[3] = obstl;
   const bool has[4] = {true, has_t1, has_t2, has_l};
-  uint32_t flags = 0, up[4] = {0, 0, 0, 0};
-  double fdn[4] = {0.0, 0.0, 0.0, 0.0};
+  uint32_t flags = 0;
+  int mo[4] = {-1, -1, -1, -1};
   {  // the first section whose extent contains each obstacle (:1462-1471), one pass for all four
-    int mo[4] = {-1, -1, -1, -1};
-    double po[4] = {0.0, 0.0, 0.0, 0.0};
     double p = 0.0;
+    for (int c = 0; c < 4; ++c) po[c] = 0.0;
     PLAN_LOOP
     for (int m = 0; m < NPM; ++m) {
       const double l = g.len(m);
@@ -236,38 +255,207 @@ AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double 
       if ((!has[1] || mo[1] >= 0) && (!has[2] || mo[2] >= 0) && (!has[3] || mo[3] >= 0) && mo[0] >= 0) break;
     }
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (mo[c] < 0) continue;
-      flags |= 1u << c;
-      up[c] = (uint32_t)mo[c];
-      fdn[c] = (obst[c] - po[c]) / g.len(mo[c]);
-    }
+    for (int c = 0; c < 4; ++c)
+      if (mo[c] >= 0) flags |= 1u << c;
   }
   if (lat1 > 0.1) flags |= PF_T1_LAT;
   if (lat2 > 0.1) flags |= PF_T2_LAT;
   if (fabs(obst1 - teeth) < 0.0001) flags |= PF_T1_TEETH;
   if (fabs(obst2 - teeth) < 0.0001) flags |= PF_T2_TEETH;
+  key.n1 = n1; key.n2 = n2; key.nl = nl;
+  key.l1 = l1; key.l2 = l2; key.ll = ll;
+  for (int c = 0; c < 4; ++c) key.mo[c] = mo[c];
+  key.has_t1 = has_t1; key.has_t2 = has_t2; key.lip_c = lip_c; key.has_l = has_l;
+  key.tb1 = tb[0]; key.tb2 = tb[1];
+  key.flags = flags;
+}
 
-  w[PW_HDR] = (uint64_t)flags | ((uint64_t)up[0] << 8) | ((uint64_t)up[1] << 16) | ((uint64_t)up[2] << 24) |
+// The words of a record that depend on the decisions alone: header and the outputs of the
+// narrowest sections (an absent constriction points at section 25's).
+AFS_HD inline void plan_key_words(const PlanKey &k, const SecRec *sec, uint64_t *w) {
+  uint32_t up[4];
+  for (int c = 0; c < 4; ++c) up[c] = k.mo[c] < 0 ? 0u : (uint32_t)k.mo[c];
+  w[PW_HDR] = (uint64_t)k.flags | ((uint64_t)up[0] << 8) | ((uint64_t)up[1] << 16) | ((uint64_t)up[2] << 24) |
               ((uint64_t)up[3] << 32);
-  // the outputs of the narrowest sections (an absent constriction points at section 25's)
-  const SecRec &q1 = sec[S_PHARYNX0 + (n1 < 0 ? 0 : n1)], &q2 = sec[S_PHARYNX0 + (n2 < 0 ? 0 : n2)];
-  const SecRec &ql = sec[S_PHARYNX0 + (nl < 0 ? 0 : nl)];
+  const SecRec &q1 = sec[S_PHARYNX0 + (k.n1 < 0 ? 0 : k.n1)], &q2 = sec[S_PHARYNX0 + (k.n2 < 0 ? 0 : k.n2)];
+  const SecRec &ql = sec[S_PHARYNX0 + (k.nl < 0 ? 0 : k.nl)];
   w[PW_UO] = (uint64_t)q1.x_uo0 | ((uint64_t)q1.x_uo1 << 16) | ((uint64_t)q2.x_uo0 << 32) | ((uint64_t)q2.x_uo1 << 48);
   w[PW_UOL] = (uint64_t)ql.x_uo0 | ((uint64_t)ql.x_uo1 << 16);
-  for (int c = 0; c < 4; ++c) w[PW_FDN + c] = plan_bits(fdn[c]);
-  // area terms of the narrowest sections, A clamped to 0.1 cm^2 (:1502-1508)
-  const int na[3] = {n1, n2, nl};
+}
+
+// The area terms of a narrowest section, A clamped to 0.1 cm^2 (:1502-1508): 1/A, sqrt(A) and
+// 1/d = 1/sqrt(4A/pi).
+AFS_HD inline void plan_area_terms(double a, double *t) {
+#pragma clang fp contract(off)
+  if (a < 0.1) a = 0.1;
+  t[0] = 1.0 / a;
+  t[1] = sqrt(a);
+  t[2] = 1.0 / sqrt(4.0 * a / PI);
+}
+
+// The glottis dipole gain 0.5e-7 * 10^(aspiration dB / 20) (TdsModel.cpp:1546).
+AFS_HD inline double plan_gain(double asp_db) { return 0.5e-7 * pow(10.0, asp_db / 20.0); }
+
+// The plan of the sample at `ratio` between frames fl and fr.  sec: the kernel tables' section
+// records (X_UN offsets of the section outputs).  two_mass: the glottis is the TwoMassModel,
+// whose aspiration strength is Glottis::DEFAULT_ASPIRATION_STRENGTH_DB.
+template <bool PRE = false>
+AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double ratio, const SecRec *sec,
+                               bool two_mass, uint64_t *w) {
+#pragma clang fp contract(off)
+  const PlanGeomT<PRE> g{fl, fr, 1.0 - ratio, ratio};
+  const double teeth = g.r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm;
+  const double asp_db = two_mass ? GLOTTIS_DEFAULT_ASPIRATION_DB : g.r1 * fl->glottis[5] + ratio * fr->glottis[5];
+  PlanKey k;
+  double obst[4], po[4];
+  plan_decide(g, teeth, k, obst, po);
+  plan_key_words(k, sec, w);
+  // downstream factors of the obstacle sections (:1472-1499)
+  for (int c = 0; c < 4; ++c) w[PW_FDN + c] = plan_bits(k.mo[c] < 0 ? 0.0 : (obst[c] - po[c]) / g.len(k.mo[c]));
+  const int na[3] = {k.n1, k.n2, k.nl};
   const int base[3] = {PW_T1, PW_T2, PW_L};
   for (int c = 0; c < 3; ++c) {
-    double a = na[c] < 0 ? 1.0 : g.area(na[c]);
-    if (a < 0.1) a = 0.1;
-    w[base[c] + 0] = plan_bits(1.0 / a);
-    w[base[c] + 1] = plan_bits(sqrt(a));
-    if (c < 2) w[base[c] + 2] = plan_bits(1.0 / sqrt(4.0 * a / PI));
+    double t[3];
+    plan_area_terms(na[c] < 0 ? 1.0 : g.area(na[c]), t);
+    w[base[c] + 0] = plan_bits(t[0]);
+    w[base[c] + 1] = plan_bits(t[1]);
+    if (c < 2) w[base[c] + 2] = plan_bits(t[2]);
   }
   w[PW_L + 2] = 0;
-  w[PW_GAIN_G] = plan_bits(0.5e-7 * pow(10.0, asp_db / 20.0));
+  w[PW_GAIN_G] = plan_bits(plan_gain(asp_db));
+}
+
+// ---------------------------------------------------------------------------
+// Hop records (hops >= PLAN_HOP_MIN).  Within one hop (one frame transition) the decisions are
+// almost always the same for every sample; the words then are functions of the ratio alone:
+// the three area-term words of a narrowest section n are the terms of its interpolated area
+// clampA((1-r) aL[n] + r aR[n]) (the same operations K5 and phase_interpolate perform), and a
+// downstream factor (obstacle - position of its section) / length of its section is the ratio
+// of two linear functions of r, whose values at the two frames K5 evaluates with the sample's
+// formula on the frame alone.  A hop record carries, per word, its kind and up to four inputs;
+// the synthesis kernel evaluates lane w's word at every sample (plan_word_eval).  A hop whose
+// samples do not all share one PlanKey (or whose aspiration strength changes) is *mixed*: its
+// samples keep the dense 128-B records.
+// ---------------------------------------------------------------------------
+enum : uint32_t { PK_CONST = 0, PK_INV = 1, PK_SQRT = 2, PK_INVD = 3, PK_FDN = 4 };
+struct PlanHop {
+  double p[PLAN_WORDS][4];  // lane w: its word's inputs (PK_CONST: the word's bits in p[w][0])
+  uint8_t kind[PLAN_WORDS];
+  uint32_t mixed;           // 1: the hop's samples use the dense records
+  uint32_t pad[3];
+};
+static_assert(sizeof(PlanHop) == 544, "hop record layout (K1 loads p[w] as two 16-byte words)");
+constexpr int PLAN_HOP_MIN = 32;  // shorter hops (target sequences: hop 1) keep dense records
+
+// Word w of the sample at `ratio` from its hop inputs, with the plan_sample operations (the
+// synthesis kernel's branch-free form is tree_core.h plan_word_fast).
+AFS_HD inline uint64_t plan_word_eval(uint32_t kind, const double *p, double ratio) {
+#pragma clang fp contract(off)
+  const double r1 = 1.0 - ratio;
+  const double x = r1 * p[0] + ratio * p[1];
+  const double y = r1 * p[2] + ratio * p[3];
+  double t[3];
+  plan_area_terms(plan_clampA(x), t);
+  switch (kind) {
+    case PK_INV: return plan_bits(t[0]);
+    case PK_SQRT: return plan_bits(t[1]);
+    case PK_INVD: return plan_bits(t[2]);
+    case PK_FDN: return plan_bits(x / y);
+    default: return plan_bits(p[0]);
+  }
+}
+
+// Position of section m's start on the frame behind g (Tube::calcPositions' sequential sum).
+template <bool PRE>
+AFS_HD inline double plan_pos(const PlanGeomT<PRE> &g, int m) {
+#pragma clang fp contract(off)
+  double p = 0.0;
+  for (int i = 0; i < m; ++i) p += g.len(i);
+  return p;
+}
+
+// The inputs of a hop whose samples share the decisions k (fl, fr: the hop's frames).  Returns
+// false when a word cannot be evaluated from them (the aspiration strength changes within the
+// hop: the glottis gain is kept constant per hop).
+AFS_HD inline bool plan_hop_inputs(const PlanKey &k, const afs_frame *fl, const afs_frame *fr, const SecRec *sec,
+                                   bool two_mass, PlanHop &h) {
+#pragma clang fp contract(off)
+  uint64_t w[PLAN_WORDS];
+  plan_key_words(k, sec, w);
+  for (int q = 0; q < PLAN_WORDS; ++q) {
+    h.kind[q] = PK_CONST;
+    h.p[q][0] = plan_double(q < 3 ? w[q] : 0);
+    h.p[q][1] = h.p[q][2] = h.p[q][3] = 0.0;
+  }
+  // downstream factors: (obstacle - position) and length at each frame
+  const afs_frame *end[2] = {fl, fr};
+  for (int e = 0; e < 2; ++e) {
+    const PlanGeomT<false> g{end[e], end[e], 1.0, 0.0};  // the frame itself: 1 a + 0 a = a
+    const double teeth = end[e]->teeth_position_cm;
+    double obst[4] = {1.5, 0.0, 0.0, 0.0};
+    const int last[2] = {k.l1, k.l2};
+    const bool at_teeth[2] = {k.tb1, k.tb2};
+    for (int c = 0; c < 2; ++c)
+      if (k.mo[1 + c] >= 0)
+        obst[1 + c] = at_teeth[c] ? teeth : (plan_pos(g, last[c]) + g.len(last[c])) + 0.5 * g.len(last[c] + 1);
+    if (k.mo[3] >= 0) obst[3] = plan_pos(g, k.ll + 1);
+    for (int c = 0; c < 4; ++c) {
+      if (k.mo[c] < 0) continue;
+      h.kind[PW_FDN + c] = PK_FDN;
+      h.p[PW_FDN + c][e] = obst[c] - plan_pos(g, k.mo[c]);
+      h.p[PW_FDN + c][2 + e] = g.len(k.mo[c]);
+    }
+  }
+  // area terms of the narrowest sections
+  const int na[3] = {k.n1, k.n2, k.nl};
+  const int base[3] = {PW_T1, PW_T2, PW_L};
+  for (int c = 0; c < 3; ++c) {
+    const int nt = c < 2 ? 3 : 2;
+    if (na[c] < 0) {
+      double t[3];
+      plan_area_terms(1.0, t);
+      for (int j = 0; j < nt; ++j) h.p[base[c] + j][0] = t[j];
+      continue;
+    }
+    for (int j = 0; j < nt; ++j) {
+      h.kind[base[c] + j] = (uint8_t)(PK_INV + j);
+      h.p[base[c] + j][0] = plan_clampA(fl->area_cm2[na[c]]);
+      h.p[base[c] + j][1] = plan_clampA(fr->area_cm2[na[c]]);
+    }
+  }
+  // glottis gain: constant over the hop
+  const double g0 = two_mass ? GLOTTIS_DEFAULT_ASPIRATION_DB : fl->glottis[5];
+  h.p[PW_GAIN_G][0] = plan_gain(g0);
+  return two_mass || fl->glottis[5] == fr->glottis[5];
+}
+
+// Host reference of K5's hop mode: the record of samples i0 .. i1-1 of the hop between fl and fr
+// (ratios i / hop); the words of a mixed hop's samples come from plan_sample.
+inline void plan_hop_host(const afs_frame *fl, const afs_frame *fr, int hop, int i0, int i1, const SecRec *sec,
+                          bool two_mass, PlanHop &h) {
+  uint64_t q0[2] = {0, 0};
+  PlanKey k0{};
+  bool mixed = false;
+  for (int i = i0; i < i1; ++i) {
+    const double ratio = (double)i / (double)hop;
+    const PlanGeomT<false> g{fl, fr, 1.0 - ratio, ratio};
+    const double teeth = g.r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm;
+    PlanKey k;
+    double obst[4], po[4];
+    plan_decide(g, teeth, k, obst, po);
+    uint64_t q[2];
+    plan_key_pack(k, q);
+    if (i == i0) {
+      k0 = k;
+      q0[0] = q[0];
+      q0[1] = q[1];
+    } else if (q[0] != q0[0] || q[1] != q0[1]) {
+      mixed = true;
+    }
+  }
+  h = PlanHop{};
+  if (!plan_hop_inputs(k0, fl, fr, sec, two_mass, h)) mixed = true;
+  h.mixed = mixed ? 1u : 0u;
 }
 
 }  // namespace tree

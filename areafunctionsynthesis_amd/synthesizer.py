@@ -149,6 +149,24 @@ class Context:
         _native.check(st, self._h, "afs_noise_plans")
         return out
 
+    def noise_plan_hops(self, frames: np.ndarray, hop: int, s_begin: int = 0, s_end: Optional[int] = None):
+        """Diagnostics (tree solver, hop >= AFS_PLAN_HOP_MIN): K5's hop records of the hops samples
+        [s_begin, s_end) span -> (uint8[rows, slots, AFS_PLAN_HOP_BYTES], the dense records of the
+        mixed hops' samples uint64[rows, s_end - s_begin, AFS_PLAN_WORDS], zero elsewhere)."""
+        if frames.dtype != FRAME_DTYPE or frames.ndim != 2:
+            raise ValueError("frames must be a 2-D FRAME_DTYPE array [rows, F]")
+        rows, F = frames.shape
+        if s_end is None:
+            s_end = (F - 1) * hop
+        frames = np.ascontiguousarray(frames)
+        slots = (s_end - 1) // hop - s_begin // hop + 1
+        hops = np.zeros((rows, slots, _native.AFS_PLAN_HOP_BYTES), dtype=np.uint8)
+        plans = np.zeros((rows, s_end - s_begin, _native.AFS_PLAN_WORDS), dtype=np.uint64)
+        st = self._lib.afs_noise_plan_hops(self._h, _vp(_addr(frames)), rows, F, hop, s_begin, s_end,
+                                           _vp(_addr(hops)), _vp(_addr(plans)))
+        _native.check(st, self._h, "afs_noise_plan_hops")
+        return hops, plans
+
     def tube_interpolate(self, left: np.ndarray, right: np.ndarray, ratio: np.ndarray):
         """Diagnostics (tree solver): the synthesis kernel's interpolated pharynx/mouth areas and
         lengths for frames left[n], right[n] at ratio[n] -> (area[n, 40], length[n, 40])."""

@@ -184,6 +184,16 @@ afs_status afs_tube_interpolate(afs_ctx *ctx, const afs_frame *left, const afs_f
                                 int32_t n, double *area, double *length);
 afs_status afs_noise_plans(afs_ctx *ctx, const afs_frame *frames, int32_t rows, int32_t num_frames, int32_t hop,
                            int64_t s_begin, int64_t s_end, uint64_t *plans);
+/* Diagnostics: the tree solver's hop mode (hops >= AFS_PLAN_HOP_MIN): K5's hop records of the
+ * hops samples [s_begin, s_end) span, hops[rows][(s_end - 1) / hop - s_begin / hop + 1]
+ * [AFS_PLAN_HOP_BYTES] (layout: csrc/tree_plan.h PlanHop: per plan word its kind and inputs, the
+ * mixed flag), and the dense records of the mixed hops' samples in plans (as afs_noise_plans;
+ * the other samples' records are left as they were).  Host or device pointers.  Other solvers or
+ * shorter hops: AFS_ERR_UNSUPPORTED. */
+#define AFS_PLAN_HOP_BYTES 544
+#define AFS_PLAN_HOP_MIN 32
+afs_status afs_noise_plan_hops(afs_ctx *ctx, const afs_frame *frames, int32_t rows, int32_t num_frames, int32_t hop,
+                               int64_t s_begin, int64_t s_end, uint8_t *hops, uint64_t *plans);
 
 /* Stateful sessions: B independent Synthesizer instances living on the device. */
 afs_status afs_session_create(afs_ctx *ctx, int32_t batch, const uint32_t *seeds, afs_session **s);

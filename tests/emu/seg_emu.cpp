@@ -157,3 +157,24 @@ extern "C" int emu_plan_records(const afs_frame *frames, int rows, int F, int ho
     }
   return 0;
 }
+
+// The hop records (tree_plan.h plan_hop_host, as K5's hop mode builds them) of the hops that
+// samples [s0, s1) of frames[rows][F] span at this hop (>= PLAN_HOP_MIN), with the tree
+// kernel's LDS offsets: out[rows][plan_hop_slots(s0, s1, hop)] PlanHop records.
+extern "C" int emu_plan_hops(const afs_frame *frames, int rows, int F, int hop, long s0, long s1, double fs,
+                             int two_mass, tree::PlanHop *out) {
+  static Tables T;
+  afs_options opt = afs::default_options();
+  opt.glottis_model = two_mass ? AFS_GLOTTIS_TWO_MASS : AFS_GLOTTIS_TRIANGULAR;
+  build_tables(&T, fs, opt);
+  const long slots = (s1 - 1) / hop - s0 / hop + 1;  // (afs_tree.h plan_hop_slots)
+  for (int r = 0; r < rows; ++r)
+    for (long q = 0; q < slots; ++q) {
+      const long h = s0 / hop + q;
+      const long lo = h * hop > s0 ? h * hop : s0, hi = (h + 1) * hop < s1 ? (h + 1) * hop : s1;
+      const afs_frame *f = frames + (long)r * F;
+      tree::plan_hop_host(f + h, f + h + 1, hop, (int)(lo - h * hop), (int)(hi - h * hop), T.consts.sec,
+                          two_mass != 0, out[(long)r * slots + q]);
+    }
+  return 0;
+}

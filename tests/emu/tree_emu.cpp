@@ -73,6 +73,12 @@ struct CpuExec {
   }
 };
 
+// Hop mode (tree_plan.h PlanHop): hops >= PLAN_HOP_MIN take their plan words from the hop
+// record (plan_hop_host, as K5 builds it) evaluated per sample (plan_word_fast, as the synthesis
+// kernel), mixed hops from the dense records.  Off by default (dense records at every hop).
+int g_hop_mode = 0;
+long g_hops = 0, g_mixed_hops = 0;
+
 template <int W>
 long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, const afs_options &opt,
          double *out, double *dump_p, double *dump_u, int ndump) {
@@ -86,13 +92,24 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
   CpuExec<W> ex{R.data()};
   long t = 0;
   const bool defer = hop >= OUT_DEFER_MIN_HOP;  // as the GPU kernel (tree_kernel.h)
+  const bool two = opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
+  const bool hops = g_hop_mode && hop >= PLAN_HOP_MIN;
   for (int k = 1; k < F; ++k) {
     for (int gl = 0; gl < W; ++gl) frame_load<W>(gl, R[gl], X.data(), frames + k - 1, frames + k);
+    PlanHop H{};
+    if (hops) {
+      plan_hop_host(frames + k - 1, frames + k, hop, 0, hop, T.consts.sec, two, H);
+      ++g_hops;
+      g_mixed_hops += H.mixed ? 1 : 0;
+    }
     const long t0 = t;
     for (int i = 0; i < hop; ++i) {
       double ratio = (double)i / (double)hop;
       uint64_t w[PLAN_WORDS];  // K5's record of this sample (tree_plan.h)
-      plan_sample(frames + k - 1, frames + k, ratio, T.consts.sec, opt.glottis_model == AFS_GLOTTIS_TWO_MASS, w);
+      if (hops && !H.mixed)
+        for (int q = 0; q < PLAN_WORDS; ++q) w[q] = plan_word_fast(H.kind[q], H.p[q], ratio);
+      else
+        plan_sample(frames + k - 1, frames + k, ratio, T.consts.sec, two, w);
       for (int gl = 0; gl < W; ++gl) R[gl].planw = w[gl % PLAN_WORDS];
       if (opt.glottis_model == AFS_GLOTTIS_TWO_MASS)
         sample_step<W, AFS_GLOTTIS_TWO_MASS>(ex, X.data(), T.uni, T.consts, ratio, defer);
@@ -143,6 +160,14 @@ extern "C" long emu_tree_utterance_opt(const afs_frame *frames, int F, int hop, 
   opt.glottis_model = iopt[8];
   opt.flow_separation_area_ratio = ratio;
   return run<16>(frames, F, hop, seed, fs, opt, out, nullptr, nullptr, 0);
+}
+
+extern "C" void emu_tree_set_hop_mode(int on) { g_hop_mode = on; }
+// hops run in hop mode since the last call, and how many of them were mixed
+extern "C" void emu_tree_hop_counts(long *hops, long *mixed) {
+  *hops = g_hops;
+  *mixed = g_mixed_hops;
+  g_hops = g_mixed_hops = 0;
 }
 
 extern "C" int emu_tree_rounds(double fs) {

@@ -1,9 +1,13 @@
 """Multi-process path of bench.py on CPU (gloo, world size 2): shards cover the batch
 exactly once, rank-local workloads equal the rows of the full batch, seeds are the global
-u + 1, and the gather reassembles the audio in utterance order.  The GPU synthesis is
-replaced by a deterministic stand-in of the same shape (no GPU here)."""
+u + 1, and the gather reassembles the audio in utterance order.  The synthesis on each rank is
+the tree kernel's own phase code run on the CPU (tests/emu: the host build of tree_core.h, the
+code the GPU kernel executes lane by lane), so the gathered audio is real synthesized audio,
+checked against a single-process run of the whole batch and against the oracle."""
+import ctypes
 import os
 import socket
+import subprocess
 
 import numpy as np
 import pytest
@@ -16,11 +20,35 @@ from areafunctionsynthesis_amd import sharding, workloads
 B, SECONDS, FS = 6, 0.03, 44100.0
 
 
-def _standin(w) -> torch.Tensor:
-    """[B, T] float64 that depends on every row's parameters, glottis and seed."""
-    T = w.samples_per_utterance
-    base = w.params[:, 0, :].sum(axis=1) + w.glottis[:, 0, 0] * 1e-3 + w.seeds.astype(np.float64) * 1e-6
-    return torch.from_numpy(base[:, None] + np.arange(T)[None, :] * 1e-9)
+EMU = os.path.join(os.path.dirname(os.path.abspath(__file__)), "emu")
+
+
+def _frames(w):
+    from oracle_lib import Oracle
+    orc = Oracle()
+    return workloads.build_frames(w, lambda p: np.stack([orc.af_to_frame(r) for r in p]))
+
+
+def _synth(w) -> torch.Tensor:
+    """[B, T] float64: the rank's utterances synthesized by the tree kernel's phase code on the
+    CPU (tests/emu/tree_emu.cpp, 16 lanes per utterance as on the GPU)."""
+    from areafunctionsynthesis_amd.frames import FRAME_DTYPE
+    lib = ctypes.CDLL(os.path.join(EMU, "libtree_emu.so"))
+    vp = ctypes.c_void_p
+    lib.emu_tree_utterance.restype = ctypes.c_long
+    lib.emu_tree_utterance.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_double,
+                                       ctypes.c_int, vp, vp, vp, ctypes.c_int]
+    frames = _frames(w)
+    out = np.zeros((w.batch, w.samples_per_utterance))
+    dummy = np.zeros(97)
+    for u in range(w.batch):
+        fr = np.ascontiguousarray(frames[u], dtype=FRAME_DTYPE)
+        o = np.zeros(out.shape[1])
+        n = lib.emu_tree_utterance(fr.ctypes.data, fr.size, w.hop, int(w.seeds[u]), w.fs, 16, o.ctypes.data,
+                                   dummy.ctypes.data, dummy.ctypes.data, 0)
+        assert n == o.size
+        out[u] = o
+    return torch.from_numpy(out)
 
 
 def _to_int16(x: torch.Tensor, out: torch.Tensor) -> None:
@@ -41,7 +69,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     first, n = sharding.shard_range(rank, world, B)
     w = workloads.static_vowels(n, seconds=SECONDS, fs=FS, first_utterance=first)
-    out = _standin(w)
+    out = _synth(w)
     got = sharding.gather_to_rank0(out, world, rank, dist)
     pcm = []
     pg = sharding.PcmGather(_to_int16, out.shape, world, rank, sharding.TorchTransport(dist, world, rank), depth=2)
@@ -70,6 +98,7 @@ def test_shard_range():
 
 def test_gloo_world2_gather_matches_single_process():
     world = 2
+    subprocess.check_call(["make", "-s", "-C", EMU])
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -84,11 +113,16 @@ def test_gloo_world2_gather_matches_single_process():
     audio, seeds0, numel, pcm = gathered
     seeds1 = next(r[1] for r in res if isinstance(r[0], str))
     full = workloads.static_vowels(world * B, seconds=SECONDS, fs=FS)
-    assert np.array_equal(audio, _standin(full).numpy())
+    ref = _synth(full).numpy()
+    assert np.array_equal(audio, ref)
+    from oracle_lib import Oracle
+    fr = _frames(full)
+    for u in (0, B - 1, B, 2 * B - 1):  # shard edges: the oracle on the same frames and seeds
+        y = Oracle().utterance(fr[u], full.hop, int(full.seeds[u]), FS)
+        assert np.abs(audio[u] - y).max() <= 1e-9, u
     assert np.array_equal(np.concatenate([seeds0, seeds1]), np.arange(1, world * B + 1, dtype=np.uint32))
     assert numel == B * full.samples_per_utterance
-    from oracle_lib import Oracle
-    x = np.sin(_standin(full).numpy() * 1e3)
+    x = np.sin(ref * 1e3)
     assert len(pcm) == 2
     assert np.array_equal(pcm[0], Oracle().to_int16(x * -3.0).reshape(x.shape))  # step 2 (slot 1)
     assert np.array_equal(pcm[1], Oracle().to_int16(x).reshape(x.shape))  # step 3 reused slot 0

@@ -308,6 +308,33 @@ def test_full_second_fricatives_config5(contexts, parity_report, solver):
                        solver)
 
 
+def test_frame_rate_vcv_hop_records(contexts, parity_report, monkeypatch):
+    """Hop records (K5's hop mode, tree solver, hops >= 32) on frame-rate VCV trajectories
+    (workloads.vcv: hop 441, the constrictions form and release inside hops, so hops with one
+    decision and mixed hops -- which read dense records -- both occur): against the oracle over
+    the whole utterance with the rand() call counts, and against the dense-record kernel
+    (AFS_PLAN_DENSE=1)."""
+    from areafunctionsynthesis_amd.synthesizer import Context
+    from areafunctionsynthesis_amd.workloads import build_frames, vcv
+    ctx = contexts(44100.0, "tree")
+    w = vcv(256, fs=44100.0)
+    frames = build_frames(w, ctx.af_to_frames)
+    hops, _ = ctx.noise_plan_hops(frames, w.hop)
+    mixed = int(np.count_nonzero(hops[..., 528:532].view(np.uint32)))
+    assert 0 < mixed < hops.shape[0] * hops.shape[1]
+    y = _full_length_check(ctx, w, frames, 4, parity_report, "frame-rate VCV (hop 441, hop records)", "tree")
+    monkeypatch.setenv("AFS_PLAN_DENSE", "1")
+    dense = Context(44100.0, solver="tree")
+    try:
+        yd = dense.synthesize(frames, w.hop, seeds=w.seeds)
+    finally:
+        dense.close()
+    diff = np.abs(y - yd).max()
+    parity_report.append(f"hop records vs dense records [tree] (frame-rate VCV, {w.batch} utterances, "
+                         f"{mixed}/{hops.shape[0] * hops.shape[1]} hops mixed): max |diff| {diff:.2e}")
+    assert diff < 1e-7
+
+
 @pytest.mark.parametrize("solver", ("tree", "seg"))
 def test_full_length_vcv_config3(contexts, parity_report, solver):
     """Config 3 at the reference's playTargetSequence timing (stationary 0.2/0.05/0.2/0.1 s,

@@ -181,3 +181,92 @@ def test_k1_interpolation_equals_k5_geometry(oracle):
     ld = np.longdouble
     a_fma = (ld(1.0) * r1.astype(ld) * aL.astype(ld) + (r * aR).astype(ld)).astype(np.float64)
     assert np.count_nonzero(a_fma != r1 * aL + r * aR) > 0
+
+
+# ---------------------------------------------------------------------------
+# Hop mode (hops >= 32, the tree solver's default there): K5's hop records against the host
+# reference plan_hop_host (tests/emu/seg_emu.cpp emu_plan_hops), and the dense records of the
+# mixed hops' samples against plan_sample.
+# ---------------------------------------------------------------------------
+HOP_DTYPE = np.dtype([("p", "<u8", (PLAN_WORDS, 4)), ("kind", "u1", (PLAN_WORDS,)), ("mixed", "<u4"),
+                      ("pad", "<u4", (3,))])
+assert HOP_DTYPE.itemsize == 544
+
+
+@pytest.fixture(scope="module")
+def host_hops():
+    lib = ctypes.CDLL(os.path.join(EMU, "libseg_emu.so"))
+    vp = ctypes.c_void_p
+    lib.emu_plan_hops.restype = ctypes.c_int
+    lib.emu_plan_hops.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_long,
+                                  ctypes.c_double, ctypes.c_int, vp]
+
+    def run(frames, hop, s0, s1, fs, two_mass):
+        frames = np.ascontiguousarray(frames)
+        rows, F = frames.shape
+        slots = (s1 - 1) // hop - s0 // hop + 1
+        out = np.zeros((rows, slots), dtype=HOP_DTYPE)
+        assert lib.emu_plan_hops(frames.ctypes.data, rows, F, hop, s0, s1, fs, int(two_mass), out.ctypes.data) == 0
+        return out
+    return run
+
+
+def _compare_hops(ctx, host_hops, host_plans, frames, hop, s0, s1, fs, two_mass, label):
+    gh, gp = ctx.noise_plan_hops(frames, hop, s0, s1)
+    gh = gh.view(HOP_DTYPE)[..., 0]
+    hh = host_hops(frames, hop, s0, s1, fs, two_mass)
+    assert np.array_equal(gh["mixed"], hh["mixed"]), label
+    assert np.array_equal(gh["kind"], hh["kind"]), label
+    gw, hw = gh["p"].copy(), hh["p"].copy()
+    # the glottis gain (a constant word: p[15][0]) comes from the device pow: 1 ulp
+    ulps = np.abs(gw[..., 15, 0].view(np.int64) - hw[..., 15, 0].view(np.int64))
+    assert ulps.max() <= 1, (label, int(ulps.max()))
+    gw[..., 15, 0] = hw[..., 15, 0] = 0
+    diff = gw != hw
+    if diff.any():
+        r, q, w, j = np.argwhere(diff)[0]
+        raise AssertionError(f"{label}: {int(diff.sum())} inputs differ; first: row {r} slot {q} word {w} input {j}")
+    # the mixed hops' samples: their dense records
+    mixed_samples = np.zeros(gp.shape[:2], dtype=bool)
+    for r, q in np.argwhere(gh["mixed"] != 0):
+        h = s0 // hop + q
+        lo, hi = max(h * hop, s0), min((h + 1) * hop, s1)
+        mixed_samples[r, lo - s0:hi - s0] = True
+    if mixed_samples.any():
+        hp = host_plans(frames, hop, s0, s1, fs, two_mass, False)
+        _compare(gp[mixed_samples][None], hp[mixed_samples][None], label + " (mixed hops' dense records)")
+    assert not gp[~mixed_samples].any(), label  # nothing written for the other samples
+    return int(np.count_nonzero(gh["mixed"])), gh.size
+
+
+@pytest.mark.parametrize("two_mass", (False, True))
+def test_plan_hops_config2_config5(contexts, host_hops, host_plans, two_mass):
+    from areafunctionsynthesis_amd.workloads import build_frames, fricatives, static_vowels
+    ctx = contexts(44100.0, "tree", two_mass)
+    for w in (static_vowels(24, seconds=0.5, fs=44100.0), fricatives(27, seconds=0.5, fs=44100.0, velum_cm2=1.0)):
+        frames = build_frames(w, ctx.af_to_frames)
+        n = (frames.shape[1] - 1) * w.hop
+        for s0, s1 in ((0, n), (12345, 12345 + 2000)):
+            mixed, total = _compare_hops(ctx, host_hops, host_plans, frames, w.hop, s0, s1, 44100.0, two_mass,
+                                         f"{w.name} two_mass={two_mass} samples {s0}..{s1}")
+            assert mixed == 0, (w.name, mixed, total)  # static shapes: one decision per hop
+
+
+def test_plan_hops_transitions(contexts, host_hops, host_plans, oracle):
+    """Frame-rate VCV trajectories (hop 441: the constrictions form and release inside hops, so
+    some hops are mixed) and transitions between all Default.params shapes."""
+    from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS
+    from areafunctionsynthesis_amd.params import default_shapes
+    from areafunctionsynthesis_amd.workloads import build_frames, vcv
+    ctx = contexts(44100.0, "tree", False)
+    w = vcv(16, fs=44100.0)
+    frames = build_frames(w, ctx.af_to_frames)
+    n = (frames.shape[1] - 1) * w.hop
+    mixed, total = _compare_hops(ctx, host_hops, host_plans, frames, w.hop, 0, n, 44100.0, False, "vcv frames")
+    sh = default_shapes()
+    names = sorted(sh)
+    frames = np.stack([np.stack([oracle.af_to_frame(sh[names[(k + j) % len(names)]]) for j in range(6)])
+                       for k in range(len(names))]).astype(FRAME_DTYPE)
+    frames["glottis"] = DEFAULT_GLOTTIS
+    m2, t2 = _compare_hops(ctx, host_hops, host_plans, frames, 97, 0, 5 * 97, 44100.0, False, "all shapes")
+    assert 0 < mixed + m2 < total + t2
