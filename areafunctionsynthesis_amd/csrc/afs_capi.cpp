@@ -135,8 +135,11 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     afs::tree::PlanHop *hbuf[2] = {nullptr, nullptr};
     if (hops) {
       const size_t hbytes = (size_t)rows * (size_t)hstride * sizeof(afs::tree::PlanHop);
-      for (int q = 0; q < (ov ? 2 : 1); ++q)
+      const size_t wbytes = (size_t)afs::plan_work_bytes(rows, hstride);
+      for (int q = 0; q < (ov ? 2 : 1); ++q) {
         if ((st = ensure(c, &c->hops[q], &c->hops_bytes[q], hbytes)) != AFS_OK) return st;
+        if ((st = ensure(c, &c->plan_work[q], &c->plan_work_bytes[q], wbytes)) != AFS_OK) return st;
+      }
       hbuf[0] = (afs::tree::PlanHop *)c->hops[0];
       hbuf[1] = (afs::tree::PlanHop *)c->hops[ov ? 1 : 0];
     }
@@ -146,7 +149,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     auto plan_chunk = [&](int64_t k) -> afs_status {
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)buf[k & 1], per, two, uo,
-                       hbuf[k & 1], hstride};
+                       hbuf[k & 1], hstride, hops ? (uint32_t *)c->plan_work[ov ? (k & 1) : 0] : nullptr};
       hipEvent_t e0 = prof_event(c, ps);
       HIP_TRY(c, hops ? afs::launch_plan_hops(pa, ps) : afs::launch_plan(pa, ps));
       prof_pair(c, e0, prof_event(c, ps), 1);
@@ -357,6 +360,8 @@ void afs_destroy(afs_ctx *c) {
   if (c->plan2) (void)hipFree(c->plan2);
   for (void *h : c->hops)
     if (h) (void)hipFree(h);
+  for (void *w : c->plan_work)
+    if (w) (void)hipFree(w);
   if (c->plan_stream) (void)hipStreamDestroy(c->plan_stream);
   for (hipEvent_t e : {c->ev_go, c->ev_plan[0], c->ev_plan[1], c->ev_free[0], c->ev_free[1]})
     if (e) (void)hipEventDestroy(e);
@@ -559,9 +564,11 @@ afs_status afs_noise_plan_hops(afs_ctx *c, const afs_frame *frames, int32_t rows
     if ((s = ensure(c, &c->hops[0], &c->hops_bytes[0], hbytes)) != AFS_OK) return s;
     dhops = (uint8_t *)c->hops[0];
   }
+  if ((s = ensure(c, &c->plan_work[0], &c->plan_work_bytes[0], (size_t)afs::plan_work_bytes(rows, slots))) != AFS_OK)
+    return s;
   afs::PlanArgs pa{c->dev_tab, dframes, F, rows, hop, s0, s1, dplans, n,
                    c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0, c->dev_tab->consts.sec,
-                   (afs::tree::PlanHop *)dhops, slots};
+                   (afs::tree::PlanHop *)dhops, slots, (uint32_t *)c->plan_work[0]};
   HIP_TRY(c, afs::launch_plan_hops(pa, c->stream));
   if (host_plans) HIP_TRY(c, hipMemcpyAsync(plans, dplans, pbytes, hipMemcpyDeviceToHost, c->stream));
   if (host_hops) HIP_TRY(c, hipMemcpyAsync(hops, dhops, hbytes, hipMemcpyDeviceToHost, c->stream));

@@ -45,10 +45,14 @@ struct PlanArgs {
                             // smoothed flows (tree: tab->consts.sec; seg: SegTables::uo)
   tree::PlanHop *hops = nullptr;  // hop mode (launch_plan_hops): as TreeArgs::hops
   int64_t hop_stride = 0;
+  uint32_t *work = nullptr;  // hop mode: a counter and rows * hop slots entries (the hops decided
+                             // sample by sample)
 };
 constexpr int64_t PLAN_RECORD_BYTES = 128;
 // Hop slots a launch of samples [s0, s1) spans.
 inline int64_t plan_hop_slots(int64_t s0, int64_t s1, int hop) { return (s1 - 1) / hop - s0 / hop + 1; }
+// Bytes of the hop-mode work list of a launch.
+inline int64_t plan_work_bytes(int64_t rows, int64_t slots) { return (rows * slots + 1) * 4; }
 
 #ifndef AFS_TREE_W
 #define AFS_TREE_W 16

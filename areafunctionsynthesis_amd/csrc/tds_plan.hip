@@ -70,75 +70,113 @@ __global__ void __launch_bounds__(PLAN_BLOCK) plan_kernel(PlanArgs a) {
   }
 }
 
-// Hop mode (hops >= PLAN_HOP_MIN): one wave per (frame row, hop slot).  The hop's two frames
-// are staged in LDS (areas clamped once); lane L decides the samples L, L + 64, ... of the
-// hop's part inside the launch (the same scans as plan_kernel, without the doubles) and compares
-// each decision with the first sample's.  Lane 0 builds the hop record (plan_hop_inputs) in
-// LDS, the wave stores it; a mixed hop's samples also get their dense records.  Matches the
-// host reference plan_hop_host bit for bit (tests/test_plan_gpu.py).
-constexpr int HOP_WAVE = 64;
+// Hop mode (hops >= PLAN_HOP_MIN), two kernels.
+// plan_hop_iv_kernel: one thread per (frame row, hop slot) decides the hop's samples inside the
+// launch with one evaluation on the interval geometry (tree_plan.h plan_hop_decide_iv).  When
+// every comparison is decided for all of them -- static and slowly moving tubes, almost every
+// hop -- it writes the hop record (plan_hop_inputs); otherwise (a decision changes within the
+// hop or comes too close to call, or the aspiration strength changes) it appends the hop to
+// the work list.
+// plan_hop_wave_kernel: one wave per work-list hop, persistent over the list.  The hop's two
+// frames are staged in LDS (areas clamped once); lane L decides the samples L, L + 64, ... (the
+// scans of plan_kernel without the doubles) and compares each decision with the first sample's.
+// Lane 0 builds the hop record in LDS, the wave stores it; a mixed hop's samples also get their
+// dense records.  Both match the host reference plan_hop_host (per-sample decisions) bit for bit
+// (tests/test_plan_gpu.py).
+constexpr int HOP_WAVE = 64, HOP_IV_BLOCK = 64;
 constexpr int HOP_WORDS = (int)(sizeof(PlanHop) / 8);
 
-__global__ void __launch_bounds__(HOP_WAVE) plan_hop_kernel(PlanArgs a) {
+struct HopRange {
+  int64_t h;       // hop index: frames h, h + 1
+  int i0, i1;      // the hop's samples inside the launch
+};
+__device__ __forceinline__ HopRange hop_range(const PlanArgs &a, int64_t slot) {
+  const int64_t h = a.s_begin / a.hop + slot;
+  const int64_t s_lo = h * a.hop > a.s_begin ? h * a.hop : a.s_begin;
+  const int64_t s_hi = (h + 1) * a.hop < a.s_end ? (h + 1) * a.hop : a.s_end;
+  return HopRange{h, (int)(s_lo - h * a.hop), (int)(s_hi - h * a.hop)};
+}
+
+__global__ void __launch_bounds__(HOP_IV_BLOCK) plan_hop_iv_kernel(PlanArgs a, int64_t slots) {
+  const int64_t id = (int64_t)blockIdx.x * HOP_IV_BLOCK + threadIdx.x;
+  if (id >= (int64_t)a.rows * slots) return;
+  const int64_t row = id / slots, slot = id % slots;
+  const HopRange r = hop_range(a, slot);
+  const afs_frame *fl = a.frames + row * a.frame_stride + r.h, *fr = fl + 1;
+  PlanKey k;
+  bool ok = plan_hop_decide_iv<false>(fl, fr, a.hop, r.i0, r.i1, k);
+  if (ok) {
+    PlanHop &h = a.hops[row * a.hop_stride + slot];
+    h = PlanHop{};
+    ok = plan_hop_inputs(k, fl, fr, a.uo, a.two_mass != 0, h);
+  }
+  if (!ok) a.work[1 + atomicAdd(a.work, 1u)] = (uint32_t)id;
+}
+
+__global__ void __launch_bounds__(HOP_WAVE) plan_hop_wave_kernel(PlanArgs a, int64_t slots) {
   __shared__ uint64_t fr_lds[2][FRAME_WORDS];
   __shared__ uint64_t hop_lds[HOP_WORDS];
   const int lane = threadIdx.x;
-  const int64_t row = blockIdx.x, slot = blockIdx.y;
-  const int64_t h = a.s_begin / a.hop + slot;  // frames h, h + 1
-  const int64_t s_lo = h * a.hop > a.s_begin ? h * a.hop : a.s_begin;
-  const int64_t s_hi = (h + 1) * a.hop < a.s_end ? (h + 1) * a.hop : a.s_end;
-  const afs_frame *f = a.frames + row * a.frame_stride;
-  {
-    const uint64_t *src = (const uint64_t *)(f + h);
-    for (int w = lane; w < 2 * FRAME_WORDS; w += HOP_WAVE) (&fr_lds[0][0])[w] = src[w];
-    __syncthreads();
-    for (int q = lane; q < 2 * NPM; q += HOP_WAVE) {
-      double *ar = ((afs_frame *)fr_lds[q / NPM])->area_cm2 + q % NPM;
-      *ar = plan_clampA(*ar);
+  const uint32_t nwork = a.work[0];
+  for (uint32_t e = blockIdx.x; e < nwork; e += gridDim.x) {
+    const uint32_t id = a.work[1 + e];
+    const int64_t row = id / slots, slot = id % slots;
+    const HopRange r = hop_range(a, slot);
+    const int64_t h = r.h;
+    const afs_frame *f = a.frames + row * a.frame_stride;
+    {
+      const uint64_t *src = (const uint64_t *)(f + h);
+      for (int w = lane; w < 2 * FRAME_WORDS; w += HOP_WAVE) (&fr_lds[0][0])[w] = src[w];
+      __syncthreads();
+      for (int q = lane; q < 2 * NPM; q += HOP_WAVE) {
+        double *ar = ((afs_frame *)fr_lds[q / NPM])->area_cm2 + q % NPM;
+        *ar = plan_clampA(*ar);
+      }
+      __syncthreads();
+    }
+    const afs_frame *fl = (const afs_frame *)fr_lds[0], *fr = (const afs_frame *)fr_lds[1];
+    const int i0 = r.i0, i1 = r.i1;
+    PlanKey k0{};
+    uint64_t q0[2] = {0, 0};
+    bool diff = false;
+    for (int i = i0 + lane, it = 0; it == 0 || i < i1; i += HOP_WAVE, ++it) {
+      uint64_t q[2] = {0, 0};
+      PlanKey k{};
+      if (i < i1) {
+        const double ratio = (double)i / (double)a.hop;
+        const PlanGeomT<true> g{fl, fr, 1.0 - ratio, ratio};
+        double obst[4], po[4];
+        plan_decide(g, k, obst, po);
+        plan_key_pack(k, q);
+      }
+      if (it == 0) {  // (the hop's first sample is lane 0's first)
+        k0 = k;
+        q0[0] = __shfl(q[0], 0, HOP_WAVE);
+        q0[1] = __shfl(q[1], 0, HOP_WAVE);
+      }
+      if (i < i1) diff = diff || q[0] != q0[0] || q[1] != q0[1];
+    }
+    bool mixed = __ballot(diff) != 0;
+    if (lane == 0) {
+      PlanHop &hl = *reinterpret_cast<PlanHop *>(hop_lds);
+      hl = PlanHop{};
+      const bool ok = plan_hop_inputs(k0, fl, fr, a.uo, a.two_mass != 0, hl);
+      hl.mixed = (mixed || !ok) ? 1u : 0u;
     }
     __syncthreads();
-  }
-  const afs_frame *fl = (const afs_frame *)fr_lds[0], *fr = (const afs_frame *)fr_lds[1];
-  const int i0 = (int)(s_lo - h * a.hop), i1 = (int)(s_hi - h * a.hop);
-  PlanKey k0{};
-  uint64_t q0[2] = {0, 0};
-  bool diff = false;
-  for (int i = i0 + lane, it = 0; it == 0 || i < i1; i += HOP_WAVE, ++it) {
-    uint64_t q[2] = {0, 0};
-    PlanKey k{};
-    if (i < i1) {
-      const double ratio = (double)i / (double)a.hop;
-      const PlanGeomT<true> g{fl, fr, 1.0 - ratio, ratio};
-      double obst[4], po[4];
-      plan_decide(g, g.r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm, k, obst, po);
-      plan_key_pack(k, q);
-    }
-    if (it == 0) {  // (the hop's first sample is lane 0's first)
-      k0 = k;
-      q0[0] = __shfl(q[0], 0, HOP_WAVE);
-      q0[1] = __shfl(q[1], 0, HOP_WAVE);
-    }
-    if (i < i1) diff = diff || q[0] != q0[0] || q[1] != q0[1];
-  }
-  bool mixed = __ballot(diff) != 0;
-  if (lane == 0) {
-    PlanHop &hl = *reinterpret_cast<PlanHop *>(hop_lds);
-    hl = PlanHop{};
-    const bool ok = plan_hop_inputs(k0, fl, fr, a.uo, a.two_mass != 0, hl);
-    hl.mixed = (mixed || !ok) ? 1u : 0u;
-  }
-  __syncthreads();
-  mixed = reinterpret_cast<const PlanHop *>(hop_lds)->mixed != 0;
-  uint64_t *dst = reinterpret_cast<uint64_t *>(a.hops + row * a.hop_stride + slot);
-  for (int w = lane; w < HOP_WORDS; w += HOP_WAVE) dst[w] = hop_lds[w];
-  if (mixed) {  // (rare: the decisions change within the hop) the samples' dense records
-    for (int i = i0 + lane; i < i1; i += HOP_WAVE) {
-      uint64_t w[PLAN_WORDS];
-      plan_sample<true>(fl, fr, (double)i / (double)a.hop, a.uo, a.two_mass != 0, w);
-      ulonglong2 *o = (ulonglong2 *)(a.plan + (row * a.plan_stride + (h * a.hop + i - a.s_begin)) * PLAN_WORDS);
+    mixed = reinterpret_cast<const PlanHop *>(hop_lds)->mixed != 0;
+    uint64_t *dst = reinterpret_cast<uint64_t *>(a.hops + row * a.hop_stride + slot);
+    for (int w = lane; w < HOP_WORDS; w += HOP_WAVE) dst[w] = hop_lds[w];
+    if (mixed) {  // the decisions change within the hop: the samples' dense records
+      for (int i = i0 + lane; i < i1; i += HOP_WAVE) {
+        uint64_t w[PLAN_WORDS];
+        plan_sample<true>(fl, fr, (double)i / (double)a.hop, a.uo, a.two_mass != 0, w);
+        ulonglong2 *o = (ulonglong2 *)(a.plan + (row * a.plan_stride + (h * a.hop + i - a.s_begin)) * PLAN_WORDS);
 #pragma unroll
-      for (int q = 0; q < PLAN_WORDS / 2; ++q) o[q] = make_ulonglong2(w[2 * q], w[2 * q + 1]);
+        for (int q = 0; q < PLAN_WORDS / 2; ++q) o[q] = make_ulonglong2(w[2 * q], w[2 * q + 1]);
+      }
     }
+    __syncthreads();  // (the next entry overwrites the LDS frames and record)
   }
 }
 
@@ -148,8 +186,15 @@ hipError_t launch_plan_hops(const PlanArgs &a, hipStream_t st) {
   const int64_t n = a.s_end - a.s_begin;
   if (n <= 0 || a.rows <= 0) return hipSuccess;
   if (!a.hops || a.hop < PLAN_HOP_MIN) return hipErrorInvalidValue;
-  const int64_t slots = plan_hop_slots(a.s_begin, a.s_end, a.hop);
-  hipLaunchKernelGGL(plan_hop_kernel, dim3((unsigned)a.rows, (unsigned)slots), dim3(HOP_WAVE), 0, st, a);
+  if (!a.work) return hipErrorInvalidValue;
+  const int64_t slots = plan_hop_slots(a.s_begin, a.s_end, a.hop), n_hops = (int64_t)a.rows * slots;
+  hipError_t e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(plan_hop_iv_kernel, dim3((unsigned)((n_hops + HOP_IV_BLOCK - 1) / HOP_IV_BLOCK)),
+                     dim3(HOP_IV_BLOCK), 0, st, a, slots);
+  // (a fixed grid: the list's length is on the device; every wave leaves its loop at its end)
+  const int64_t waves = n_hops < 2048 ? n_hops : 2048;
+  hipLaunchKernelGGL(plan_hop_wave_kernel, dim3((unsigned)waves), dim3(HOP_WAVE), 0, st, a, slots);
   return hipGetLastError();
 }
 

@@ -78,6 +78,7 @@ AFS_HD inline double plan_clampA(double a) { return a < AMIN ? AMIN : a; }
 // bits whatever the compiler's -ffp-contract default, and re-evaluation gives the same value.
 template <bool PRE>  // PRE: the frames' areas are clamped already (K5's LDS copy)
 struct PlanGeomT {
+  using V = double;
   const afs_frame *fl, *fr;
   double r1, ratio;
   AFS_HD double area(int m) const {
@@ -93,36 +94,154 @@ struct PlanGeomT {
 #pragma clang fp contract(off)
     return r1 * fl->laterality[m] + ratio * fr->laterality[m];
   }
+  AFS_HD double teeth() const {
+#pragma clang fp contract(off)
+    return r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm;
+  }
   AFS_HD int art(int m) const { return fl->articulator[m]; }  // the left tube's (Tube.cpp:452)
-  // first section with the articulator and the smallest area (strict "<", from 1e6), -1: none
-  AFS_HD int argmin(int a, double &amin, int skip_lo = 1, int skip_hi = 0) const {
-    int n = -1;
-    amin = 1000000.0;
-    PLAN_LOOP
-    for (int m = 0; m < NPM; ++m) {
-      const double A = area(m);
-      if (art(m) == a && A < amin && (m < skip_lo || m > skip_hi)) { amin = A; n = m; }
-    }
-    return n;
-  }
-  // the reference's constriction extent (TdsModel.cpp:1247-1262): from the narrowest section
-  // outwards while the area stays below amin + 0.2 with the same articulator, then one back
-  AFS_HD void grow(int narrow, double amin, int a, int &first, int &last) const {
-    const double maxA = amin + 0.2;
-    first = narrow;
-    last = narrow;
-    while (area(first) < maxA && art(first) == a && first > 0) --first;
-    while (area(last) < maxA && art(last) == a && last < NPM - 1) ++last;
-    ++first;
-    --last;
-  }
-  AFS_HD double max_lat(int first, int last) const {
-    double l = 0.0;
-    for (int m = first; m <= last; ++m)
-      if (lat(m) > l) l = lat(m);
-    return l;
-  }
+  AFS_HD double pos0() const { return 0.0; }                  // the running position sums' start
+  // the decisions' comparisons
+  AFS_HD static bool lt(double a, double b) { return a < b; }
+  AFS_HD static bool le(double a, double b) { return a <= b; }
 };
+
+// ---------------------------------------------------------------------------
+// The same geometry over a range of samples of one hop (ratios i / hop, i = i0 .. i1-1), as
+// intervals that contain every value a sample of the range computes (K5's hop mode decides a
+// whole hop with one evaluation when every comparison of plan_decide is decided for all of
+// them).  Each interpolated value (1 - r) a + r b lies, for every sample, within
+// 2^-50 (|a| + |b|) of the interval spanned by the two end samples' own values (the exact
+// interpolation is monotone in r, the rounding of r, 1 - r, the products and the sum is below
+// that); sums and differences widen by 2^-51 of their magnitude.  Identical quantities -- the same
+// section's interpolated area or laterality (same inputs), the running position sums of the
+// position and obstacle passes -- carry an identity, so that they compare equal exactly (a tie
+// in the scans, the lip obstacle at the end of its own section).
+// ---------------------------------------------------------------------------
+struct PlanIv {
+  double lo, hi;
+  int kind;     // identity: IV_NONE, or what the value is (the same kind and inputs: equal everywhere)
+  double a, b;  // IV_AREA / IV_LAT / IV_TEETH: the interpolation's inputs; IV_POS / IV_LEN: the index
+  PlanIv() = default;
+  AFS_HD explicit PlanIv(double c) : lo(c), hi(c), kind(0), a(0.0), b(0.0) {}
+  AFS_HD PlanIv(double lo_, double hi_, int kind_, double a_, double b_) : lo(lo_), hi(hi_), kind(kind_), a(a_), b(b_) {}
+};
+enum : int { IV_NONE = 0, IV_AREA = 1, IV_POS = 2, IV_LEN = 3, IV_LAT = 4, IV_TEETH = 5 };
+AFS_HD inline PlanIv plan_iv(double c) { return PlanIv(c); }
+AFS_HD inline bool plan_iv_same(const PlanIv &x, const PlanIv &y) {
+  return x.kind != IV_NONE && x.kind == y.kind && x.a == y.a && x.b == y.b;
+}
+AFS_HD inline PlanIv plan_iv_widen(double lo, double hi) {
+  const double e = 4.440892098500626e-16;  // 2^-51
+  return PlanIv{lo - fabs(lo) * e, hi + fabs(hi) * e, IV_NONE, 0.0, 0.0};
+}
+AFS_HD inline PlanIv operator+(const PlanIv &x, const PlanIv &y) {
+  PlanIv r = plan_iv_widen(x.lo + y.lo, x.hi + y.hi);
+  if (x.kind == IV_POS && y.kind == IV_LEN && x.a == y.a) {  // pos[m] + len[m] = pos[m + 1]
+    r.kind = IV_POS;
+    r.a = x.a + 1.0;
+  }
+  return r;
+}
+AFS_HD inline PlanIv &operator+=(PlanIv &x, const PlanIv &y) { return x = x + y; }
+AFS_HD inline PlanIv operator+(const PlanIv &x, double c) { return plan_iv_widen(x.lo + c, x.hi + c); }
+AFS_HD inline PlanIv operator*(double c, const PlanIv &x) {  // (c >= 0)
+  return plan_iv_widen(c * x.lo, c * x.hi);
+}
+AFS_HD inline PlanIv operator-(const PlanIv &x, const PlanIv &y) {
+  if (plan_iv_same(x, y)) return plan_iv(0.0);
+  return plan_iv_widen(x.lo - y.hi, x.hi - y.lo);
+}
+AFS_HD inline double plan_abs(double x) { return fabs(x); }
+AFS_HD inline PlanIv plan_abs(const PlanIv &x) {
+  if (x.lo >= 0.0) return x;
+  if (x.hi <= 0.0) return PlanIv{-x.hi, -x.lo, IV_NONE, 0.0, 0.0};
+  return PlanIv{0.0, -x.lo > x.hi ? -x.lo : x.hi, IV_NONE, 0.0, 0.0};
+}
+
+template <bool PRE>
+struct PlanGeomIv {
+  using V = PlanIv;
+  const afs_frame *fl, *fr;
+  double r1lo, rlo, r1hi, rhi;  // the end samples' 1 - r and r
+  mutable int undecided;        // a comparison that is not the same for every sample of the range
+  AFS_HD PlanIv lerp(double a, double b, int kind, bool clamp) const {
+#pragma clang fp contract(off)
+    const double u0 = r1lo * a + rlo * b, u1 = r1hi * a + rhi * b;
+    const double w = (fabs(a) + fabs(b)) * 8.881784197001252e-16;  // 2^-50
+    double lo = (u0 < u1 ? u0 : u1) - w, hi = (u0 < u1 ? u1 : u0) + w;
+    if (clamp) {
+      lo = plan_clampA(lo);
+      hi = plan_clampA(hi);
+    }
+    return PlanIv{lo, hi, kind, a, b};
+  }
+  AFS_HD PlanIv area(int m) const {
+    const double a = PRE ? fl->area_cm2[m] : plan_clampA(fl->area_cm2[m]);
+    const double b = PRE ? fr->area_cm2[m] : plan_clampA(fr->area_cm2[m]);
+    return lerp(a, b, IV_AREA, true);
+  }
+  AFS_HD PlanIv len(int m) const {
+    PlanIv v = lerp(fl->length_cm[m], fr->length_cm[m], IV_LEN, false);
+    v.a = (double)m;
+    v.b = 0.0;
+    return v;
+  }
+  AFS_HD PlanIv lat(int m) const { return lerp(fl->laterality[m], fr->laterality[m], IV_LAT, false); }
+  AFS_HD PlanIv teeth() const { return lerp(fl->teeth_position_cm, fr->teeth_position_cm, IV_TEETH, false); }
+  AFS_HD int art(int m) const { return fl->articulator[m]; }
+  AFS_HD PlanIv pos0() const { return PlanIv{0.0, 0.0, IV_POS, 0.0, 0.0}; }
+  AFS_HD bool lt(const PlanIv &x, const PlanIv &y) const {
+    if (plan_iv_same(x, y)) return false;
+    if (x.hi < y.lo) return true;
+    if (x.lo >= y.hi) return false;
+    undecided = 1;
+    return false;
+  }
+  AFS_HD bool le(const PlanIv &x, const PlanIv &y) const {
+    if (plan_iv_same(x, y)) return true;
+    if (x.hi <= y.lo) return true;
+    if (x.lo > y.hi) return false;
+    undecided = 1;
+    return false;
+  }
+  AFS_HD bool lt(const PlanIv &x, double c) const { return lt(x, plan_iv(c)); }
+};
+
+// first section with the articulator and the smallest area (strict "<", from 1e6), -1: none
+template <class G>
+AFS_HD inline int plan_argmin(const G &g, int a, typename G::V &amin, int skip_lo = 1, int skip_hi = 0) {
+  using V = typename G::V;
+  int n = -1;
+  amin = V(1000000.0);
+  PLAN_LOOP
+  for (int m = 0; m < NPM; ++m) {
+    const V A = g.area(m);
+    if (g.art(m) == a && (m < skip_lo || m > skip_hi) && g.lt(A, amin)) { amin = A; n = m; }
+  }
+  return n;
+}
+// the reference's constriction extent (TdsModel.cpp:1247-1262): from the narrowest section
+// outwards while the area stays below amin + 0.2 with the same articulator, then one back
+template <class G>
+AFS_HD inline void plan_grow(const G &g, int narrow, const typename G::V &amin, int a, int &first, int &last) {
+#pragma clang fp contract(off)
+  using V = typename G::V;
+  const V maxA = amin + 0.2;
+  first = narrow;
+  last = narrow;
+  while (g.lt(g.area(first), maxA) && g.art(first) == a && first > 0) --first;
+  while (g.lt(g.area(last), maxA) && g.art(last) == a && last < NPM - 1) ++last;
+  ++first;
+  --last;
+}
+template <class G>
+AFS_HD inline typename G::V plan_max_lat(const G &g, int first, int last) {
+  using V = typename G::V;
+  V l = V(0.0);
+  for (int m = first; m <= last; ++m)
+    if (g.lt(l, g.lat(m))) l = g.lat(m);
+  return l;
+}
 
 // The discrete decisions of one sample's plan: which sections are the narrowest ones, where the
 // constrictions end, which obstacle formula applies and in which section each obstacle lies.
@@ -144,65 +263,68 @@ AFS_HD inline void plan_key_pack(const PlanKey &k, uint64_t *q) {
          (uint64_t)k.has_l << 11 | (uint64_t)k.tb1 << 12 | (uint64_t)k.tb2 << 13;
 }
 
-// The discrete decisions at one sample (g: its interpolated geometry, teeth: its interpolated
-// teeth position) and the obstacle positions / the positions of the obstacle sections that go
-// into the downstream factors.
+// The discrete decisions at one sample (g: its interpolated geometry; PlanGeomT) or, with the
+// interval geometry PlanGeomIv, for every sample of a range at once (valid unless g.undecided),
+// and the obstacle positions / the positions of the obstacle sections that go into the
+// downstream factors.
 // The reference's scans (argmin, extent, position, obstacle) are merged into four passes over
 // the 40 sections: the narrowest tongue and lip sections together, the second tongue
 // constriction, one running position sum for every position the obstacles need, and one
 // obstacle search for all four constrictions.  Every value is the one the separate scans give
 // (the same comparisons and the same sequential sums).
-template <bool PRE>
-AFS_HD inline void plan_decide(const PlanGeomT<PRE> &g, double teeth, PlanKey &key, double *obst, double *po) {
+template <class G>
+AFS_HD inline void plan_decide(const G &g, PlanKey &key, typename G::V *obst, typename G::V *po) {
 #pragma clang fp contract(off)
+  using V = typename G::V;
+  const V teeth = g.teeth();
   // narrowest tongue section (:1228-1240) and narrowest lower-lip section (:1399-1410): the
   // first strict minimum from 1e6
   int n1 = -1, nl = -1;
-  double amin1 = 1000000.0, aminl = 1000000.0;
+  V amin1 = V(1000000.0), aminl = V(1000000.0);
   PLAN_LOOP
   for (int m = 0; m < NPM; ++m) {
-    const double A = g.area(m);
+    const V A = g.area(m);
     const int a = g.art(m);
-    if (a == TONGUE && A < amin1) { amin1 = A; n1 = m; }
-    if (a == LOWER_LIP && A < aminl) { aminl = A; nl = m; }
+    if (a == TONGUE && g.lt(A, amin1)) { amin1 = A; n1 = m; }
+    if (a == LOWER_LIP && g.lt(A, aminl)) { aminl = A; nl = m; }
   }
   // tongue constriction 1 (:1228-1302)
-  const bool has_t1 = amin1 < 1.0;
+  const bool has_t1 = g.lt(amin1, V(1.0));
   int f1 = 0, l1 = -1;
-  double lat1 = 0.0, obst1 = 0.0;
+  V lat1 = V(0.0), obst1 = V(0.0);
   if (has_t1) {
-    g.grow(n1, amin1, TONGUE, f1, l1);
-    lat1 = g.max_lat(f1, l1);
+    plan_grow(g, n1, amin1, TONGUE, f1, l1);
+    lat1 = plan_max_lat(g, f1, l1);
   }
   // tongue constriction 2 (:1309-1392), kept when it does not touch the first
   bool has_t2 = false;
   int n2 = -1, l2 = -1;
-  double lat2 = 0.0, obst2 = 0.0;
+  V lat2 = V(0.0), obst2 = V(0.0);
   if (has_t1) {
-    double amin2;
-    n2 = g.argmin(TONGUE, amin2, f1, l1);
-    if (amin2 < 1.0) {
+    V amin2;
+    n2 = plan_argmin(g, TONGUE, amin2, f1, l1);
+    if (g.lt(amin2, V(1.0))) {
       int f2;
-      g.grow(n2, amin2, TONGUE, f2, l2);
+      plan_grow(g, n2, amin2, TONGUE, f2, l2);
       if (f2 > l1 + 1 || l2 < f1 - 1) {
         has_t2 = true;
-        lat2 = g.max_lat(f2, l2);
+        lat2 = plan_max_lat(g, f2, l2);
       }
     }
   }
   // extent of the lip constriction (:1399-1444)
-  const bool lip_c = aminl < 1.0;
+  const bool lip_c = g.lt(aminl, V(1.0));
   int ll = -1;
   if (lip_c) {
     int fl_;
-    g.grow(nl, aminl, LOWER_LIP, fl_, ll);
+    plan_grow(g, nl, aminl, LOWER_LIP, fl_, ll);
   }
   // positions of sections l1, l2 and ll + 1: Tube::calcPositions' sequential sum (:611-622)
   const int i1 = has_t1 ? l1 : -1, i2 = has_t2 ? l2 : -1, i3 = lip_c ? ll + 1 : -1;
   const int imax = i1 > i2 ? (i1 > i3 ? i1 : i3) : (i2 > i3 ? i2 : i3);
-  double P1 = 0.0, P2 = 0.0, P3 = 0.0;
+  V P1 = V(0.0), P2 = V(0.0), P3 = V(0.0);
   {
-    double p = 0.0;
+    V p = g.pos0();
     PLAN_LOOP
     for (int m = 0; m <= imax; ++m) {
       if (m == i1) P1 = p;
@@ -213,11 +335,11 @@ AFS_HD inline void plan_decide(const PlanGeomT<PRE> &g, double teeth, PlanKey &k
   }
   // obstacles of the tongue constrictions (:1283-1299): the teeth when the jet ends within
   // 2 cm of them, else the middle of the section after the constriction
-  double min_teeth = 1000000.0;
+  V min_teeth = V(1000000.0);
   bool tb[2] = {false, false};
-  auto tongue_obstacle = [&](double pl, int last, int narrow, bool &at_teeth) {
-    const double jet = pl + g.len(last);
-    if (teeth - jet < 2.0) {
+  auto tongue_obstacle = [&](const V &pl, int last, int narrow, bool &at_teeth) -> V {
+    const V jet = pl + g.len(last);
+    if (g.lt(teeth - jet, V(2.0))) {
       min_teeth = g.area(narrow);
       at_teeth = true;
       return teeth;
@@ -227,11 +349,11 @@ AFS_HD inline void plan_decide(const PlanGeomT<PRE> &g, double teeth, PlanKey &k
   if (has_t1) obst1 = tongue_obstacle(P1, l1, n1, tb[0]);
   if (has_t2) obst2 = tongue_obstacle(P2, l2, n2, tb[1]);
   // the lower lip counts when narrower than a tongue constriction at the teeth
-  const bool has_l = lip_c && aminl < min_teeth;
-  const double obstl = has_l ? P3 : 0.0;
+  const bool has_l = lip_c && g.lt(aminl, min_teeth);
+  const V obstl = has_l ? P3 : V(0.0);
 
   // obstacle sections (:1456-1499)
-  obst[0] = 1.5;
+  obst[0] = V(1.5);
   obst[1] = obst1;
   obst[2] = obst2;
   obst[3] = obstl;
@@ -239,14 +361,14 @@ AFS_HD inline void plan_decide(const PlanGeomT<PRE> &g, double teeth, PlanKey &k
   uint32_t flags = 0;
   int mo[4] = {-1, -1, -1, -1};
   {  // the first section whose extent contains each obstacle (:1462-1471), one pass for all four
-    double p = 0.0;
-    for (int c = 0; c < 4; ++c) po[c] = 0.0;
+    V p = g.pos0();
+    for (int c = 0; c < 4; ++c) po[c] = V(0.0);
     PLAN_LOOP
     for (int m = 0; m < NPM; ++m) {
-      const double l = g.len(m);
+      const V l = g.len(m);
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        if (has[c] && mo[c] < 0 && p <= obst[c] && p + l >= obst[c]) {
+        if (has[c] && mo[c] < 0 && g.le(p, obst[c]) && g.le(obst[c], p + l)) {
           mo[c] = m;
           po[c] = p;
         }
@@ -258,10 +380,10 @@ AFS_HD inline void plan_decide(const PlanGeomT<PRE> &g, double teeth, PlanKey &k
     for (int c = 0; c < 4; ++c)
       if (mo[c] >= 0) flags |= 1u << c;
   }
-  if (lat1 > 0.1) flags |= PF_T1_LAT;
-  if (lat2 > 0.1) flags |= PF_T2_LAT;
-  if (fabs(obst1 - teeth) < 0.0001) flags |= PF_T1_TEETH;
-  if (fabs(obst2 - teeth) < 0.0001) flags |= PF_T2_TEETH;
+  if (g.lt(V(0.1), lat1)) flags |= PF_T1_LAT;
+  if (g.lt(V(0.1), lat2)) flags |= PF_T2_LAT;
+  if (g.lt(plan_abs(obst1 - teeth), V(0.0001))) flags |= PF_T1_TEETH;
+  if (g.lt(plan_abs(obst2 - teeth), V(0.0001))) flags |= PF_T2_TEETH;
   key.n1 = n1; key.n2 = n2; key.nl = nl;
   key.l1 = l1; key.l2 = l2; key.ll = ll;
   for (int c = 0; c < 4; ++c) key.mo[c] = mo[c];
@@ -304,11 +426,10 @@ AFS_HD inline void plan_sample(const afs_frame *fl, const afs_frame *fr, double 
                                bool two_mass, uint64_t *w) {
 #pragma clang fp contract(off)
   const PlanGeomT<PRE> g{fl, fr, 1.0 - ratio, ratio};
-  const double teeth = g.r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm;
   const double asp_db = two_mass ? GLOTTIS_DEFAULT_ASPIRATION_DB : g.r1 * fl->glottis[5] + ratio * fr->glottis[5];
   PlanKey k;
   double obst[4], po[4];
-  plan_decide(g, teeth, k, obst, po);
+  plan_decide(g, k, obst, po);
   plan_key_words(k, sec, w);
   // downstream factors of the obstacle sections (:1472-1499)
   for (int c = 0; c < 4; ++c) w[PW_FDN + c] = plan_bits(k.mo[c] < 0 ? 0.0 : (obst[c] - po[c]) / g.len(k.mo[c]));
@@ -429,6 +550,18 @@ AFS_HD inline bool plan_hop_inputs(const PlanKey &k, const afs_frame *fl, const 
   return two_mass || fl->glottis[5] == fr->glottis[5];
 }
 
+// The decisions of every sample i0 .. i1-1 of the hop between fl and fr (ratios i / hop) with
+// one evaluation on the interval geometry: true when every comparison was decided for all of
+// them (k is then each sample's PlanKey), false when K5 has to decide the samples one by one.
+template <bool PRE>
+AFS_HD inline bool plan_hop_decide_iv(const afs_frame *fl, const afs_frame *fr, int hop, int i0, int i1, PlanKey &k) {
+  const double rlo = (double)i0 / (double)hop, rhi = (double)(i1 - 1) / (double)hop;
+  const PlanGeomIv<PRE> g{fl, fr, 1.0 - rlo, rlo, 1.0 - rhi, rhi, 0};
+  PlanIv obst[4], po[4];
+  plan_decide(g, k, obst, po);
+  return g.undecided == 0;
+}
+
 // Host reference of K5's hop mode: the record of samples i0 .. i1-1 of the hop between fl and fr
 // (ratios i / hop); the words of a mixed hop's samples come from plan_sample.
 inline void plan_hop_host(const afs_frame *fl, const afs_frame *fr, int hop, int i0, int i1, const SecRec *sec,
@@ -439,10 +572,9 @@ inline void plan_hop_host(const afs_frame *fl, const afs_frame *fr, int hop, int
   for (int i = i0; i < i1; ++i) {
     const double ratio = (double)i / (double)hop;
     const PlanGeomT<false> g{fl, fr, 1.0 - ratio, ratio};
-    const double teeth = g.r1 * fl->teeth_position_cm + ratio * fr->teeth_position_cm;
     PlanKey k;
     double obst[4], po[4];
-    plan_decide(g, teeth, k, obst, po);
+    plan_decide(g, k, obst, po);
     uint64_t q[2];
     plan_key_pack(k, q);
     if (i == i0) {

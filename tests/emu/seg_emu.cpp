@@ -178,3 +178,47 @@ extern "C" int emu_plan_hops(const afs_frame *frames, int rows, int F, int hop, 
     }
   return 0;
 }
+
+// The interval decisions of K5's hop mode (tree_plan.h plan_hop_decide_iv) against the per-sample
+// decisions: for every hop that samples [s0, s1) of frames[rows][F] span, a hop the interval
+// evaluation decides must give every one of its samples the same PlanKey as plan_decide on that
+// sample.  counts[0]: hops decided, [1]: hops left to the per-sample path, [2]: violations (decided
+// hops with a sample whose key differs), [3]: hops whose samples do not all share one key.
+extern "C" int emu_plan_iv_check(const afs_frame *frames, int rows, int F, int hop, long s0, long s1, long *counts) {
+  for (int q = 0; q < 4; ++q) counts[q] = 0;
+  const long slots = (s1 - 1) / hop - s0 / hop + 1;
+  for (int r = 0; r < rows; ++r)
+    for (long q = 0; q < slots; ++q) {
+      const long h = s0 / hop + q;
+      const long lo = h * hop > s0 ? h * hop : s0, hi = (h + 1) * hop < s1 ? (h + 1) * hop : s1;
+      const afs_frame *fl = frames + (long)r * F + h, *fr = fl + 1;
+      const int i0 = (int)(lo - h * hop), i1 = (int)(hi - h * hop);
+      tree::PlanKey kiv;
+      const bool dec = tree::plan_hop_decide_iv<false>(fl, fr, hop, i0, i1, kiv);
+      uint64_t qiv[2], q0[2] = {0, 0};
+      tree::plan_key_pack(kiv, qiv);
+      bool same = true, viol = false;
+      for (int i = i0; i < i1; ++i) {
+        const double ratio = (double)i / (double)hop;
+        const tree::PlanGeomT<false> g{fl, fr, 1.0 - ratio, ratio};
+        tree::PlanKey k;
+        double obst[4], po[4];
+        tree::plan_decide(g, k, obst, po);
+        uint64_t qq[2];
+        tree::plan_key_pack(k, qq);
+        if (i == i0) { q0[0] = qq[0]; q0[1] = qq[1]; }
+        same = same && qq[0] == q0[0] && qq[1] == q0[1];
+        viol = viol || (dec && (qq[0] != qiv[0] || qq[1] != qiv[1]));
+      }
+      counts[dec ? 0 : 1] += 1;
+      counts[2] += viol ? 1 : 0;
+      counts[3] += same ? 0 : 1;
+    }
+  return 0;
+}
+
+// The words of a hop record at `ratio` (tree_plan.h plan_word_eval, the host form of the
+// synthesis kernel's plan_word_fast): out[PLAN_WORDS].
+extern "C" void emu_plan_hop_words(const tree::PlanHop *h, double ratio, uint64_t *out) {
+  for (int q = 0; q < tree::PLAN_WORDS; ++q) out[q] = tree::plan_word_eval(h->kind[q], h->p[q], ratio);
+}
