@@ -229,8 +229,12 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
     if constexpr (HOPS) {
       const uint64_t ev = plan_word_fast(hkind, hp, ratio);
       R.planw = hmixed ? next : ev;
+#if defined(AFS_HOP_BRANCH_LOAD)  // (A/B variant: the dense word loaded under a branch)
+      if (hmixed) next = pl[tn * PLAN_WORDS];
+#else
       // (a hop that is not mixed reads its own record's first word: a cache hit, no branch)
       next = *(hmixed ? pl + tn * PLAN_WORDS : reinterpret_cast<const uint64_t *>(hr));
+#endif
     } else {
       R.planw = next;
       next = pl[tn * PLAN_WORDS];  // the next sample's word, a sample ahead

@@ -49,6 +49,14 @@ def per_launch(path: str, kernel: str) -> list[float]:
     return [float(r["Counter_Value"]) for r in rows]
 
 
+PLAN_KERNELS = ("plan_kernel", "plan_hop_iv_kernel", "plan_hop_wave_kernel")  # K5: dense / hop mode
+
+
+def plan_total(path: str) -> float:
+    return sum(float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+               if any(k in r["Kernel_Name"] for k in PLAN_KERNELS))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
@@ -68,8 +76,8 @@ def main() -> None:
     kib = 1024.0
     fetch_b = 2.0 * kib * sum(fetch) / len(fetch)   # gfx950: FETCH_SIZE = half the read bytes
     write_b = kib * sum(write) / len(write)
-    plan_f = per_launch(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"), "plan_kernel")
-    plan_w = per_launch(os.path.join(a.dir, "pmc_write", "run_counter_collection.csv"), "plan_kernel")
+    plan_f = plan_total(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"))
+    plan_w = plan_total(os.path.join(a.dir, "pmc_write", "run_counter_collection.csv"))
     entry = {
         "tag": a.tag,
         "launches": len(fetch),
@@ -81,8 +89,8 @@ def main() -> None:
                       "half the bytes of the 128-B lines it reads, profiles/r02_fetch_calib.txt), write = WRITE_SIZE; "
                       "KiB -> bytes",
     }
-    if plan_f and plan_w:  # K5, the noise-source plan producer of the same launches
-        entry["plan_kernel_traffic_bytes_per_launch"] = 2.0 * kib * sum(plan_f) / len(plan_f) + kib * sum(plan_w) / len(plan_w)
+    if plan_f or plan_w:  # K5 (all its kernels), the noise-source plan producer of the same launches
+        entry["plan_kernel_traffic_bytes_per_launch"] = (2.0 * kib * plan_f + kib * plan_w) / len(fetch)
     import sys
     sys.path.insert(0, ROOT)
     from areafunctionsynthesis_amd.build import kernel_digest
