@@ -1609,6 +1609,7 @@ AFS_HD inline double output_filter_one(double *X, const Consts &C, double flow) 
 // o[0..n) holds the radiated flows of n consecutive samples; they are replaced by the audio
 // samples.  The filter state stays in registers over the run; the loads of the next 8 samples
 // are issued before the current 8 are filtered (their latency hides behind the filter chain).
+#if defined(AFS_OUTF_SHIFT)  // (A/B variant: the state shifted per sample)
 AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int n) {
   double sx[8], sy[8], ca[9], cb[9];
 #pragma unroll
@@ -1653,6 +1654,79 @@ AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int 
   X[X_PREVFLOW] = prev;
   if (nonfin) X[X_NONFIN] = 1.0;
 }
+#else
+// Full blocks of 8 samples keep the filter's inputs and outputs in a 16-entry window (the 8
+// values before the block, then the block's): every sample reads its predecessors at fixed
+// window positions, and the window moves once per block (16 moves per 8 samples instead of 16
+// per sample).  The last samples of the run (fewer than 8) shift the state per sample.  The same
+// operations in the same order either way.
+AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int n) {
+  double hx[16], hy[16], ca[9], cb[9];  // hx[7 - k] = x[t - 1 - k] at a block's start
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { hx[7 - k] = X[X_OUTF + k]; hy[7 - k] = X[X_OUTF + 8 + k]; }
+#pragma unroll
+  for (int k = 0; k <= 8; ++k) { ca[k] = C.h.out_a[k]; cb[k] = C.h.out_b[k]; }
+  const double inv_dt = C.h.inv_dt;
+  double prev = X[X_PREVFLOW];
+  bool nonfin = false;
+  double f[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (i < n) ? o[i] : 0.0;
+  int t0 = 0;
+  for (; t0 + 8 <= n; t0 += 8) {
+    double g[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = (t0 + 8 + i < n) ? o[t0 + 8 + i] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const double op = (f[i] - prev) * inv_dt;
+      prev = f[i];
+      double acc = ca[0] * op;
+#pragma unroll
+      for (int k = 1; k <= 8; ++k) {
+        acc += ca[k] * hx[8 + i - k];
+        acc += cb[k] * hy[8 + i - k];
+      }
+      hx[8 + i] = op;
+      hy[8 + i] = acc;
+      double smp = acc * 0.004;
+      smp = smp * (1.0 / 32767);
+      nonfin = nonfin || !isfinite(smp);
+      o[t0 + i] = smp;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { hx[j] = hx[8 + j]; hy[j] = hy[8 + j]; f[j] = g[j]; }
+  }
+  double sx[8], sy[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sx[k] = hx[7 - k]; sy[k] = hy[7 - k]; }
+  for (int i = 0; t0 + i < n; ++i) {  // (fewer than 8 left: f[i] holds sample t0 + i)
+    double fi = f[0];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) fi = (i == q) ? f[q] : fi;
+    const double op = (fi - prev) * inv_dt;
+    prev = fi;
+    double acc = ca[0] * op;
+#pragma unroll
+    for (int k = 1; k <= 8; ++k) {
+      acc += ca[k] * sx[k - 1];
+      acc += cb[k] * sy[k - 1];
+    }
+#pragma unroll
+    for (int k = 7; k > 0; --k) { sx[k] = sx[k - 1]; sy[k] = sy[k - 1]; }
+    sx[0] = op;
+    sy[0] = acc;
+    double smp = acc * 0.004;
+    smp = smp * (1.0 / 32767);
+    nonfin = nonfin || !isfinite(smp);
+    o[t0 + i] = smp;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { X[X_OUTF + k] = sx[k]; X[X_OUTF + 8 + k] = sy[k]; }
+  X[X_PREVFLOW] = prev;
+  if (nonfin) X[X_NONFIN] = 1.0;
+}
+#endif
 
 // Hops of at least this many samples run the output filter once per hop (output_filter_run)
 // instead of inside the sample step.
