@@ -179,6 +179,8 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       if (seg(c)) HIP_TRY(c, afs::launch_seg_synth(afs::SegArgs{a, c->dev_seg}, c->stream));
       else HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
       prof_pair(c, e1, prof_event(c), 0);
+      if (!seg(c) && !afs::tree_output_in_kernel())  // K6: the output stage of the launch's samples
+        HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B, c->stream));
       if (ov) HIP_TRY(c, hipEventRecord(c->ev_free[k & 1], c->stream));
     }
     return AFS_OK;

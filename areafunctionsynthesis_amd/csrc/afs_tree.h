@@ -69,6 +69,12 @@ int64_t tree_lane_bytes();
 int64_t tree_lds_doubles();
 hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const uint32_t *seeds, hipStream_t st);
 hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st);
+// K6, after each tree_synth launch of samples [s_begin, s_end): the output stage over the flows
+// it stored (out[u * out_stride + s - s_begin], replaced by the audio).  Not needed when the
+// synthesis kernel was built to filter itself (tree_output_in_kernel(): the A/B variant).
+hipError_t launch_tree_output(const Tables *tab, double *lds_state, double *out, int64_t out_stride, int64_t n, int B,
+                              hipStream_t st);
+bool tree_output_in_kernel();
 hipError_t launch_tree_nonfinite(const double *lds_state, int B, int32_t *count, uint8_t *flags, hipStream_t st);
 hipError_t launch_tree_draws(const double *lds_state, int B, int64_t *draws, hipStream_t st);
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st);

@@ -17,6 +17,17 @@ __global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_synth_kerne
   tree_synth_body<false, MODEL, HOPS>(a, lds, nullptr);
 }
 
+// K6: the output stage of a launch's samples -- dU/dt, the 8-pole Chebyshev low-pass, x 0.004 /
+// 32767 (Synthesizer.cpp:614-627) -- over the radiated flows the synthesis kernel stored, in
+// place, one thread per utterance; the filter state (X_OUTF, X_PREVFLOW, X_NONFIN) lives in the
+// utterance's saved LDS image, which the synthesis kernel carries through unchanged.
+__global__ void __launch_bounds__(64) tree_output_kernel(const Tables *tab, double *lds_state, double *out,
+                                                         int64_t out_stride, int64_t n, int B) {
+  const int u = blockIdx.x * 64 + threadIdx.x;
+  if (u >= B) return;
+  output_filter_run(lds_state + (int64_t)u * X_TOTAL, tab->consts, out + (int64_t)u * out_stride, (int)n);
+}
+
 // seeds == nullptr: utterance u is seeded u + 1 (afs.h)
 __global__ void tree_reset_kernel(Lane<TW> *lanes, double *lds, int B, const uint32_t *seeds) {
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -75,6 +86,21 @@ hipError_t launch_tree_interp(const Tables *tab, const afs_frame *fl, const afs_
   const int64_t t = (int64_t)n * TW;
   hipLaunchKernelGGL(tree_interp_kernel, dim3((unsigned)((t + 127) / 128)), dim3(128), 0, st, tab, fl, fr, ratio, n,
                      area, len);
+  return hipGetLastError();
+}
+
+bool tree_output_in_kernel() {
+#if defined(AFS_K1_FILTER)
+  return true;
+#else
+  return false;
+#endif
+}
+
+hipError_t launch_tree_output(const Tables *tab, double *lds_state, double *out, int64_t out_stride, int64_t n, int B,
+                              hipStream_t st) {
+  if (B <= 0 || n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tree_output_kernel, dim3((B + 63) / 64), dim3(64), 0, st, tab, lds_state, out, out_stride, n, B);
   return hipGetLastError();
 }
 

@@ -543,6 +543,52 @@ AFS_HD inline void frame_load(int gl, Lane<W> &R, double *X, const afs_frame *fl
   }
 }
 
+// The fields of a frame that frame_load reads, loaded ahead (tree_kernel.h, dense kernel):
+// the areas / lengths of the lane's pharynx/mouth slots and the frame-rate values.
+template <int W>
+struct NextFrame {
+  double a[Shape<W>::ND], l[Shape<W>::ND], x[8];  // x: teeth, velum, glottis[6]
+  AFS_HD void load(int gl, const afs_frame *f) {
+#pragma unroll
+    for (int j = 0; j < Shape<W>::ND; ++j) {
+      const int m = dyn_section(W, j, gl) - S_PHARYNX0;
+      const int mm = (m >= 0 && m < NPM) ? m : 0;  // (other slots load section 25's and discard it)
+      a[j] = f->area_cm2[mm];
+      l[j] = f->length_cm[mm];
+    }
+    x[0] = f->teeth_position_cm;
+    x[1] = f->velum_opening_cm2;
+    for (int k = 0; k < 6; ++k) x[2 + k] = f->glottis[k];
+  }
+};
+// frame_load(fr, next) when fr was the previous transition's right frame: the right frame
+// becomes the left one, the right one comes from the loaded fields (the same values frame_load
+// gives).
+template <int W>
+AFS_HD inline void frame_shift(int gl, Lane<W> &R, double *X, const NextFrame<W> &nf) {
+  using S = Shape<W>;
+#pragma unroll
+  for (int j = 0; j < S::ND; ++j) {
+    const int m = dyn_section(W, j, gl) - S_PHARYNX0;
+    if (m >= 0 && m < NPM) {
+      R.aL[j] = R.aR[j];
+      R.lL[j] = R.lR[j];
+      R.aR[j] = clampA(nf.a[j]);
+      R.lR[j] = nf.l[j];
+    }
+  }
+  if (gl == 0) {
+    X[X_FRAME + 0] = X[X_FRAME + 1];
+    X[X_FRAME + 1] = nf.x[0];
+    X[X_FRAME + 2] = X[X_FRAME + 3];
+    X[X_FRAME + 3] = clampA(nf.x[1]);
+    for (int k = 0; k < 6; ++k) {
+      X[X_FRAME + 4 + k] = X[X_FRAME + 10 + k];
+      X[X_FRAME + 10 + k] = nf.x[2 + k];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Phase G: tube interpolation (all lanes) and the glottis (lane 0).
 // ---------------------------------------------------------------------------
@@ -567,11 +613,12 @@ AFS_HD inline void phase_interpolate(int gl, Lane<W> &R, double *X, const Consts
     const int s = DYN0 + k;
     const bool pm = s >= S_PHARYNX0 && s <= S_LAST_MOUTH;
     const bool nose = s >= S_NOSE0 && k < NDYNS;
-    const double apm = clampA(r1 * R.aL[j] + ratio * R.aR[j]);
+    const double apm = r1 * R.aL[j] + ratio * R.aR[j];
     const double lpm = r1 * R.lL[j] + ratio * R.lR[j];
     const int i = s - S_NOSE0;
-    const double anose = clampA(open + ((double)(i * i) * (C.h.nose4_area - open)) * (1.0 / 16));
-    const double a = pm ? apm : (nose ? anose : 1.0);
+    const double anose = open + ((double)(i * i) * (C.h.nose4_area - open)) * (1.0 / 16);
+    // (both candidates clamped: one clamp after the select measured -0.2 %, profiles/r03x_ab.txt)
+    const double a = pm ? clampA(apm) : (nose ? clampA(anose) : 1.0);
     R.acur[j] = a;
     R.lcur[j] = pm ? lpm : C.h.len_nose0;
   }
@@ -1597,6 +1644,7 @@ AFS_HD inline double section_pressure(const double *X, const Consts &C, int s) {
 // over a whole hop of flows afterwards (output_filter_run) or per sample (output_filter_one);
 // both evaluate the same operations on the same state (X_PREVFLOW, X_OUTF).
 AFS_HD inline double output_filter_one(double *X, const Consts &C, double flow) {
+#pragma clang fp contract(off)
   double op = (flow - X[X_PREVFLOW]) * C.h.inv_dt;
   X[X_PREVFLOW] = flow;
   double y = iir_run<8>(X + X_OUTF, C.h.out_a, C.h.out_b, op);
@@ -1609,8 +1657,15 @@ AFS_HD inline double output_filter_one(double *X, const Consts &C, double flow) 
 // o[0..n) holds the radiated flows of n consecutive samples; they are replaced by the audio
 // samples.  The filter state stays in registers over the run; the loads of the next 8 samples
 // are issued before the current 8 are filtered (their latency hides behind the filter chain).
-#if defined(AFS_OUTF_SHIFT)  // (A/B variant: the state shifted per sample)
+// (A 16-entry window moved once per 8-sample block instead of the per-sample shift -- the same
+// operations, 16 instead of 128 register moves per block -- measured 2 % slower end to end: the
+// window's 64 registers push persistent state into AGPRs, profiles/r03w_ab.txt.)
 AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int n) {
+  // (not contracted into fmas: each product and sum rounds as in the reference, so the result does
+  // not depend on where a run starts -- a session's per-call runs equal one run over the whole
+  // trajectory bit for bit; with contraction the compiler may pair the terms differently in
+  // different unrolled positions)
+#pragma clang fp contract(off)
   double sx[8], sy[8], ca[9], cb[9];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { sx[k] = X[X_OUTF + k]; sy[k] = X[X_OUTF + 8 + k]; }
@@ -1654,79 +1709,6 @@ AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int 
   X[X_PREVFLOW] = prev;
   if (nonfin) X[X_NONFIN] = 1.0;
 }
-#else
-// Full blocks of 8 samples keep the filter's inputs and outputs in a 16-entry window (the 8
-// values before the block, then the block's): every sample reads its predecessors at fixed
-// window positions, and the window moves once per block (16 moves per 8 samples instead of 16
-// per sample).  The last samples of the run (fewer than 8) shift the state per sample.  The same
-// operations in the same order either way.
-AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int n) {
-  double hx[16], hy[16], ca[9], cb[9];  // hx[7 - k] = x[t - 1 - k] at a block's start
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { hx[7 - k] = X[X_OUTF + k]; hy[7 - k] = X[X_OUTF + 8 + k]; }
-#pragma unroll
-  for (int k = 0; k <= 8; ++k) { ca[k] = C.h.out_a[k]; cb[k] = C.h.out_b[k]; }
-  const double inv_dt = C.h.inv_dt;
-  double prev = X[X_PREVFLOW];
-  bool nonfin = false;
-  double f[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) f[i] = (i < n) ? o[i] : 0.0;
-  int t0 = 0;
-  for (; t0 + 8 <= n; t0 += 8) {
-    double g[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) g[i] = (t0 + 8 + i < n) ? o[t0 + 8 + i] : 0.0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const double op = (f[i] - prev) * inv_dt;
-      prev = f[i];
-      double acc = ca[0] * op;
-#pragma unroll
-      for (int k = 1; k <= 8; ++k) {
-        acc += ca[k] * hx[8 + i - k];
-        acc += cb[k] * hy[8 + i - k];
-      }
-      hx[8 + i] = op;
-      hy[8 + i] = acc;
-      double smp = acc * 0.004;
-      smp = smp * (1.0 / 32767);
-      nonfin = nonfin || !isfinite(smp);
-      o[t0 + i] = smp;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { hx[j] = hx[8 + j]; hy[j] = hy[8 + j]; f[j] = g[j]; }
-  }
-  double sx[8], sy[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { sx[k] = hx[7 - k]; sy[k] = hy[7 - k]; }
-  for (int i = 0; t0 + i < n; ++i) {  // (fewer than 8 left: f[i] holds sample t0 + i)
-    double fi = f[0];
-#pragma unroll
-    for (int q = 1; q < 8; ++q) fi = (i == q) ? f[q] : fi;
-    const double op = (fi - prev) * inv_dt;
-    prev = fi;
-    double acc = ca[0] * op;
-#pragma unroll
-    for (int k = 1; k <= 8; ++k) {
-      acc += ca[k] * sx[k - 1];
-      acc += cb[k] * sy[k - 1];
-    }
-#pragma unroll
-    for (int k = 7; k > 0; --k) { sx[k] = sx[k - 1]; sy[k] = sy[k - 1]; }
-    sx[0] = op;
-    sy[0] = acc;
-    double smp = acc * 0.004;
-    smp = smp * (1.0 / 32767);
-    nonfin = nonfin || !isfinite(smp);
-    o[t0 + i] = smp;
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { X[X_OUTF + k] = sx[k]; X[X_OUTF + 8 + k] = sy[k]; }
-  X[X_PREVFLOW] = prev;
-  if (nonfin) X[X_NONFIN] = 1.0;
-}
-#endif
 
 // Hops of at least this many samples run the output filter once per hop (output_filter_run)
 // instead of inside the sample step.

@@ -202,10 +202,17 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   const int hop = a.hop;
   const int64_t n = a.s_end - a.s_begin;
   int k = (int)(a.s_begin / hop) + 1, i = (int)(a.s_begin % hop);
-  // long hops: the output filter runs over each hop's flows once the hop is done (lane 0
-  // re-reads the flows it stored; the filter does not feed back into the tube); a launch
-  // that ends inside a hop filters the part it has
+#if defined(AFS_K1_FILTER)
+  // (A/B variant, the round-2/3 kernel: the output filter in the synthesis kernel -- long hops:
+  // over each hop's flows once the hop is done, lane 0 re-reading the flows it stored; short
+  // hops: inside the sample step)
   const bool defer = hop >= OUT_DEFER_MIN_HOP;
+#else
+  // The output stage (dU/dt, Chebyshev low-pass, scaling) does not feed back into the tube:
+  // the kernel stores the radiated flows and K6 (tree_output_kernel) filters them after the
+  // launch, so none of the filter's state or code is in this kernel's registers.
+  constexpr bool defer = true;
+#endif
   frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
   // hop mode: this hop's record (word gl % 16: its kind and inputs; whether the hop is mixed)
   const PlanHop *hr = HOPS ? a.hops + row * a.hop_stride : nullptr;
@@ -220,6 +227,11 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
     hmixed = h->mixed != 0;
   };
   if constexpr (HOPS) hop_load(hr);
+  // Dense kernel (hops < 32: target sequences play one frame per sample): the fields of the
+  // next right frame are loaded during the last sample of a hop, so that their latency hides
+  // behind that sample's work instead of stalling the frame transition; the new left frame is
+  // the old right one (frame_shift).
+  NextFrame<TW> nf{};
   ex.sync();
   uint64_t next = hmixed ? pl[0] : 0;
   int64_t t0 = 0;
@@ -229,25 +241,33 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
     if constexpr (HOPS) {
       const uint64_t ev = plan_word_fast(hkind, hp, ratio);
       R.planw = hmixed ? next : ev;
-#if defined(AFS_HOP_BRANCH_LOAD)  // (A/B variant: the dense word loaded under a branch)
-      if (hmixed) next = pl[tn * PLAN_WORDS];
-#else
-      // (a hop that is not mixed reads its own record's first word: a cache hit, no branch)
+      // (a hop that is not mixed reads its own record's first word: a cache hit, no branch; the
+      // load under a branch instead measured the same, profiles/r03w_ab.txt)
       next = *(hmixed ? pl + tn * PLAN_WORDS : reinterpret_cast<const uint64_t *>(hr));
-#endif
     } else {
       R.planw = next;
       next = pl[tn * PLAN_WORDS];  // the next sample's word, a sample ahead
     }
+#if !defined(AFS_NO_FRAME_PREFETCH)
+    if constexpr (!HOPS)
+      if (i + 1 == hop && t + 1 < n) nf.load(gl, fu + k + 1);
+#endif
     sample_step<TW, MODEL>(ex, X, a.uni, C, ratio, defer);
     if (valid && gl == 0) o[t] = R.sample;
     if (++i == hop) {
+#if defined(AFS_K1_FILTER)
       if (defer && valid && gl == 0) output_filter_run(X, C, o + t0, (int)(t + 1 - t0));
+#endif
       t0 = t + 1;
       i = 0;
       ++k;
       if (t + 1 < n) {
+#if !defined(AFS_NO_FRAME_PREFETCH)
+        if constexpr (HOPS) frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
+        else frame_shift<TW>(gl, R, X, nf);
+#else
         frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
+#endif
         if constexpr (HOPS) {
           hop_load(++hr);
           if (hmixed) next = pl[(t + 1) * PLAN_WORDS];
@@ -256,7 +276,10 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
       ex.sync();
     }
   }
+#if defined(AFS_K1_FILTER)
   if (defer && valid && gl == 0 && t0 < n) output_filter_run(X, C, o + t0, (int)(n - t0));
+#endif
+  (void)t0;
   ex.sync();
   if (valid) {
     // (the per-sample fields carry nothing to the next launch; zero them so that their
