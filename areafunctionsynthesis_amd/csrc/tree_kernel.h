@@ -20,6 +20,16 @@
 namespace afs {
 namespace tree {
 
+// A DPP lane move whose every lane's source is inside its row (the permutations, rotations and
+// broadcasts used here), or whose out-of-row lanes read 0 (bound_ctrl): the destination's old
+// value is never kept, so the move carries none (update_dpp(0, ...) zeroed it first: ~90 moves
+// per sample).  AFS_DPP_OLD0 restores that form (A/B).
+#if defined(AFS_DPP_OLD0)
+#define AFS_DPP(src, ctrl, rmask, bmask, bc) __builtin_amdgcn_update_dpp(0, (src), (ctrl), (rmask), (bmask), (bc))
+#else
+#define AFS_DPP(src, ctrl, rmask, bmask, bc) __builtin_amdgcn_mov_dpp((src), (ctrl), (rmask), (bmask), (bc))
+#endif
+
 constexpr int TW = TREE_W;
 constexpr int UPW = 64 / TW;          // utterances per wave
 constexpr int WPB = TREE_WPB;         // waves per block (they share one copy of the tables)
@@ -54,7 +64,7 @@ struct GpuExec {
     return (b >> (__lane_id() & ~(TW - 1))) & ((1ull << TW) - 1);
   }
   template <int CTRL> __device__ __forceinline__ static int dpp(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+    return AFS_DPP(v, CTRL, 0xF, 0xF, false);
   }
   template <int CTRL> __device__ __forceinline__ static double dpp(double v) {
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
@@ -113,7 +123,7 @@ struct GpuExec {
   // (bound_ctrl) inside the 16-lane row; for 32 lanes, lane 15 of the first row is added to
   // the second (row_bcast15 into rows 1 and 3).
   template <int CTRL> __device__ __forceinline__ static uint32_t shr(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+    return (uint32_t)AFS_DPP((int)v, CTRL, 0xF, 0xF, true);
   }
   template <int N, class F, class G> __device__ __forceinline__ void scan_add(F f, G g) {
     U4 v = f(gl, *R);
@@ -124,6 +134,7 @@ struct GpuExec {
       x += shr<0x112>(x);
       x += shr<0x114>(x);
       x += shr<0x118>(x);
+      // (rows 1 and 3 only: the other rows keep the old value 0)
       if constexpr (TW == 32) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
       v.v[i] = x;
     }
@@ -134,8 +145,8 @@ struct GpuExec {
     static_assert(K != 0 && K > -16 && K < 16, "row shift");
     constexpr int CTRL = K > 0 ? 0x100 + K : 0x110 - K;
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, true);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, true);
+    const int lo = AFS_DPP((int)(uint32_t)b, CTRL, 0xF, 0xF, true);
+    const int hi = AFS_DPP((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, true);
     return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
   }
   template <int K, int N, class F, class G> __device__ __forceinline__ void pull(F f, G g) {
@@ -149,8 +160,8 @@ struct GpuExec {
   // (R.planw), DPP row_newbcast hands it to the whole row.
   template <int K> __device__ __forceinline__ uint64_t rec() {
     const uint64_t v = R->planw;
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x150 + K, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x150 + K, 0xF, 0xF, false);
+    const int lo = AFS_DPP((int)(uint32_t)v, 0x150 + K, 0xF, 0xF, false);
+    const int hi = AFS_DPP((int)(uint32_t)(v >> 32), 0x150 + K, 0xF, 0xF, false);
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
   }
   __device__ __forceinline__ void mark(int ph) {
