@@ -70,7 +70,12 @@ enum : int {
   X_E = X_P4 + 4, X_D = X_E + NDYP,                      // E: dynamic sections (s-23), D: all
   X_L = X_D + NS + 1, X_R1 = X_L + NDYP, X_R0 = X_R1 + NDYP,  // dynamic, s-23
   X_RAD = X_R0 + NDYP,                                   // 1 / radius sqrt(pi / A) of the dynamic sections
+#if defined(AFS_WALL_REG)
   X_SMP = X_RAD + NDYP,                                  // dipole samples (41)
+#else
+  X_ALPHA = X_RAD + NDYP,                                // wall term alpha of the dynamic sections (update)
+  X_SMP = X_ALPHA + NDYP,                                // dipole samples (41)
+#endif
   X_UNION = X_SMP + NDIP,
   //   sink slots of the phases before the rows (n): stores of lanes / slots with nothing to store
   X_ACT = X_UNION, X_NOISE_END = X_ACT + 16,
@@ -863,8 +868,12 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     }
     Eg[j] = E;
     betag[j] = beta;
+#if defined(AFS_WALL_REG)  // (A/B variant: alpha and beta carried in registers to the update)
     R.al[j] = alpha;
     R.be[j] = beta;
+#else
+    X[X_ALPHA + ks] = alpha;
+#endif
     X[X_E + ks] = E;
     X[X_D + (present ? s : NS)] = R.p[j] + C.h.dtTH1 * R.pr[j] - E * (beta - 0.0);
     X[X_L + ks] = L;
@@ -1258,8 +1267,11 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     const SecRec &q = rec[j];
     const int rc = q.x_rad[0] / 8 - X_U, lc = q.x_rad[1] / 8 - X_U;
     double uR = xat(X, q.x_rad[0]), uL = xat(X, q.x_rad[1]), uRr = xat(X, q.x_rad[2]), uLr = xat(X, q.x_rad[3]);
-    R.rad_u[0] = uR; R.rad_u[1] = uL; R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
+    R.rad_u[0] = uR; R.rad_u[1] = uL;
+#if defined(AFS_RAD_REG)  // (A/B variant: the old d/dt and smoothed flows kept in registers too)
+    R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
     R.rad_un[0] = xat(X, q.x_rad[4]); R.rad_un[1] = xat(X, q.x_rad[5]);
+#endif
     const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
     {
       const double Rrad = dyn ? X[X_RRAD] : C.h.rrad_nose;  // (network phase / tables)
@@ -1573,8 +1585,21 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
     const int s0 = slot_section<W>(j, gl);
     const int s = s0 < 0 ? (j < S::ND ? DYN0 : 0) : s0;
     double alpha, beta;
-    if (j < S::ND) { alpha = R.al[j]; beta = R.be[j]; }
-    else { alpha = C.stat[static_index(s)][ST_ALPHA]; beta = static_beta<W>(R, j, U, C, s); }  // same values as phase_network
+    if (j < S::ND) {
+#if defined(AFS_WALL_REG)
+      alpha = R.al[j];
+      beta = R.be[j];
+#else
+      // alpha from the network phase's LDS slot, beta recomputed from the unchanged wall state
+      // (the network phase's expression): neither is carried in registers through the solver
+      const bool walls = U.opt.soft_walls && !(s == S_GLOT_LO || s == S_GLOT_UP);
+      alpha = X[X_ALPHA + (s - DYN0)];
+      beta = walls ? fma(R.w[j], C.h.wall_k1, fma(R.wr[j], C.h.wall_k2, R.wr2[j] * C.h.wall_k3)) : 0.0;
+#endif
+    } else {
+      alpha = C.stat[static_index(s)][ST_ALPHA];
+      beta = static_beta<W>(R, j, U, C, s);  // same values as phase_network
+    }
     const double un = unew[j];
     const double uold = R.u[j];
     R.u[j] = un;
@@ -1618,9 +1643,16 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
       const SecRec &q = rec[j];
       for (int k = 0; k < 2; ++k) {
         double un = xat(X, q.x_rad[k]);
-        double ur = (un - R.rad_u[k]) * idt - (TH1 / TH) * R.rad_ur[k];
+#if defined(AFS_RAD_REG)
+        const double our = R.rad_ur[k], oun = R.rad_un[k];
+#else
+        // (the previous sample's d/dt and smoothed flow are still in their LDS slots: read before
+        // this update overwrites them, instead of carrying them in registers through the solver)
+        const double our = xat(Xw, q.x_rad[2 + k]), oun = xat(Xw, q.x_rad[4 + k]);
+#endif
+        double ur = (un - R.rad_u[k]) * idt - (TH1 / TH) * our;
         xat(Xw, q.x_rad[2 + k]) = ur;
-        xat(Xw, q.x_rad[4 + k]) = (1.0 - c) * un + c * R.rad_un[k];
+        xat(Xw, q.x_rad[4 + k]) = (1.0 - c) * un + c * oun;
       }
     }
   }
