@@ -70,12 +70,7 @@ enum : int {
   X_E = X_P4 + 4, X_D = X_E + NDYP,                      // E: dynamic sections (s-23), D: all
   X_L = X_D + NS + 1, X_R1 = X_L + NDYP, X_R0 = X_R1 + NDYP,  // dynamic, s-23
   X_RAD = X_R0 + NDYP,                                   // 1 / radius sqrt(pi / A) of the dynamic sections
-#if defined(AFS_WALL_REG)
   X_SMP = X_RAD + NDYP,                                  // dipole samples (41)
-#else
-  X_ALPHA = X_RAD + NDYP,                                // wall term alpha of the dynamic sections (update)
-  X_SMP = X_ALPHA + NDYP,                                // dipole samples (41)
-#endif
   X_UNION = X_SMP + NDIP,
   //   sink slots of the phases before the rows (n): stores of lanes / slots with nothing to store
   X_ACT = X_UNION, X_NOISE_END = X_ACT + 16,
@@ -868,12 +863,10 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     }
     Eg[j] = E;
     betag[j] = beta;
-#if defined(AFS_WALL_REG)  // (A/B variant: alpha and beta carried in registers to the update)
+    // (carried in registers to the update: alpha through an LDS array and beta recomputed there
+    // measured -2.1 %, profiles/r03ab_ab.txt)
     R.al[j] = alpha;
     R.be[j] = beta;
-#else
-    X[X_ALPHA + ks] = alpha;
-#endif
     X[X_E + ks] = E;
     X[X_D + (present ? s : NS)] = R.p[j] + C.h.dtTH1 * R.pr[j] - E * (beta - 0.0);
     X[X_L + ks] = L;
@@ -1585,21 +1578,8 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
     const int s0 = slot_section<W>(j, gl);
     const int s = s0 < 0 ? (j < S::ND ? DYN0 : 0) : s0;
     double alpha, beta;
-    if (j < S::ND) {
-#if defined(AFS_WALL_REG)
-      alpha = R.al[j];
-      beta = R.be[j];
-#else
-      // alpha from the network phase's LDS slot, beta recomputed from the unchanged wall state
-      // (the network phase's expression): neither is carried in registers through the solver
-      const bool walls = U.opt.soft_walls && !(s == S_GLOT_LO || s == S_GLOT_UP);
-      alpha = X[X_ALPHA + (s - DYN0)];
-      beta = walls ? fma(R.w[j], C.h.wall_k1, fma(R.wr[j], C.h.wall_k2, R.wr2[j] * C.h.wall_k3)) : 0.0;
-#endif
-    } else {
-      alpha = C.stat[static_index(s)][ST_ALPHA];
-      beta = static_beta<W>(R, j, U, C, s);  // same values as phase_network
-    }
+    if (j < S::ND) { alpha = R.al[j]; beta = R.be[j]; }
+    else { alpha = C.stat[static_index(s)][ST_ALPHA]; beta = static_beta<W>(R, j, U, C, s); }  // same values as phase_network
     const double un = unew[j];
     const double uold = R.u[j];
     R.u[j] = un;
