@@ -246,11 +246,10 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   ex.sync();
   uint64_t next = hmixed ? pl[0] : 0;
   int64_t t0 = 0;
-  double ratio = (double)i / (double)hop;
   for (int64_t t = 0; t < n; ++t) {
-#if defined(AFS_RATIO_AT_TOP)  // (A/B variant: the sample's ratio divided at the top of its step)
-    ratio = (double)i / (double)hop;
-#endif
+    // (divided at the top of each step: the next sample's ratio computed at the end of the
+    // previous step instead measured -2.5 %, profiles/r03ad_ab.txt)
+    const double ratio = (double)i / (double)hop;
     const int64_t tn = t + 1 < n ? t + 1 : t;
     if constexpr (HOPS) {
       const uint64_t ev = plan_word_fast(hkind, hp, ratio);
@@ -267,11 +266,6 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
       if (i + 1 == hop && t + 1 < n) nf.load(gl, fu + k + 1);
 #endif
     sample_step<TW, MODEL>(ex, X, a.uni, C, ratio, defer);
-#if !defined(AFS_RATIO_AT_TOP)
-    // the next sample's ratio (i / hop, exactly as the reference divides), computed at the end of
-    // this sample's step, where its division overlaps the update, instead of heading the next step
-    ratio = (double)(i + 1 == hop ? 0 : i + 1) / (double)hop;
-#endif
     if (valid && gl == 0) o[t] = R.sample;
     if (++i == hop) {
 #if defined(AFS_K1_FILTER)
