@@ -169,6 +169,12 @@ struct Hot {
   // beta = wall_k1 w + wall_k2 w' + wall_k3 w'' (TdsModel.cpp:805-832); the mouth's radiation
   // elements Rrad = rrad_c / A, Lrad = lrad_c r0 / A (:1874, :1889)
   double wall_invK, wall_k1, wall_k2, wall_k3, rrad_c, lrad_c;
+  // per glottis mass i: mass, stiffness, contact stiffness, damping ratio, sqrt(mass stiffness),
+  // inlet / outlet factor, rest thickness (the constants of TriangularGlottis::incTime for the
+  // mass a lane evaluates when the masses are split over an utterance's lanes, tree_core.h);
+  // 256 B with the padding, so the LDS blocks after the tables keep their bank alignment
+  double gmass[2][8];
+  double gmass_pad[16];
 };
 // Values that steer branches in the time loop: kernel arguments on the device, so the
 // compiler keeps them in scalar registers and branches on them uniformly.

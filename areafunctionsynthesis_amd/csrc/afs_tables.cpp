@@ -375,6 +375,13 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
   h.g_smk0 = std::sqrt(G_MASS0 * G_K0);
   h.g_smk1 = std::sqrt(G_MASS1 * G_K1);
   {
+    const double gm[2][8] = {{G_MASS0, G_K0, G_KC0, G_DAMP0, h.g_smk0, G_INLET, G_REST_THICK0, 0.0},
+                             {G_MASS1, G_K1, G_KC1, G_DAMP1, h.g_smk1, G_OUTLET, G_REST_THICK1, 0.0}};
+    for (int i = 0; i < 2; ++i)
+      for (int k = 0; k < 8; ++k) h.gmass[i][k] = gm[i][k];
+    for (int k = 0; k < 16; ++k) h.gmass_pad[k] = 0.0;
+  }
+  {
     const double Mw = h.Mw_ph0, Bw = h.Bw_ph0, Kw = h.Kw_ph0;
     const double idt = 1.0 / (t->dt * TH), idt2 = 1.0 / (t->dt * t->dt * TH * TH), th = TH1 / TH;
     const double K = Mw * idt2 + Bw * idt + Kw;

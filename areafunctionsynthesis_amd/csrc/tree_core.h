@@ -294,26 +294,26 @@ AFS_HD inline double glottis_q(double f0) {
 
 // getOpenCloseDimensions (TriangularGlottis.cpp:474-576), as selects (the three cases and the
 // apex test are evaluated and chosen; no branch splits the geometry block)
+AFS_HD inline void glottis_open_close_one(double rest, double cord, double rel, double &olen, double &clen,
+                                          double &ow, double &cz) {
+  const double back = rest + rel;
+  const double front = (rest < 0.0) ? back : rel;
+  const bool open = back > 0.0 && front > 0.0;
+  const bool closed = back <= 0.0 && front <= 0.0;
+  double r = rest;
+  if (fabs(r) < 0.000000001) r = 0.000000001;
+  const double apex = cord * (1.0 + fast_div(rel, r));
+  const bool part = !open && !closed && apex >= 0.0 && apex <= cord;
+  const bool pb = part && back > 0.0, pf = part && !(back > 0.0);
+  olen = open ? cord : pb ? apex : pf ? cord - apex : 0.0;
+  ow = open ? back + front : pb ? back : pf ? front : 0.0;
+  clen = open ? 0.0 : pb ? cord - apex : pf ? apex : cord;
+  cz = open ? 0.0 : pb ? 0.5 * (apex + cord) : pf ? 0.5 * apex : 0.5 * cord;
+}
 AFS_HD inline void glottis_open_close(const double *gp, double cord, double rel0, double rel1,
                                       double *olen, double *clen, double *ow, double *cz) {
-  const double rest[2] = {gp[2], gp[3]};
-  const double rel[2] = {rel0, rel1};
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const double back = rest[i] + rel[i];
-    const double front = (rest[i] < 0.0) ? back : rel[i];
-    const bool open = back > 0.0 && front > 0.0;
-    const bool closed = back <= 0.0 && front <= 0.0;
-    double r = rest[i];
-    if (fabs(r) < 0.000000001) r = 0.000000001;
-    const double apex = cord * (1.0 + fast_div(rel[i], r));
-    const bool part = !open && !closed && apex >= 0.0 && apex <= cord;
-    const bool pb = part && back > 0.0, pf = part && !(back > 0.0);
-    olen[i] = open ? cord : pb ? apex : pf ? cord - apex : 0.0;
-    ow[i] = open ? back + front : pb ? back : pf ? front : 0.0;
-    clen[i] = open ? 0.0 : pb ? cord - apex : pf ? apex : cord;
-    cz[i] = open ? 0.0 : pb ? 0.5 * (apex + cord) : pf ? 0.5 * apex : 0.5 * cord;
-  }
+  glottis_open_close_one(gp[2], cord, rel0, olen[0], clen[0], ow[0], cz[0]);
+  glottis_open_close_one(gp[3], cord, rel1, olen[1], clen[1], ow[1], cz[1]);
 }
 
 // Gain of the glottis dipole source, 0.5e-7 * 10^(aspiration dB / 20) (TdsModel.cpp:1546),
@@ -708,6 +708,64 @@ AFS_HD inline GlotRes glottis_eval(const GlotIn &in, const CT &C, double ratio, 
     res.rel[1] = (A * Ff - Ee * Cq) * inv_det;
     return res;
   }
+}
+
+// The triangular glottis with its two masses on the two halves of an utterance's 16 lanes
+// (device, AFS_GLOTTIS_SPLIT): every lane evaluates the shared terms, lanes 0-7 mass 0 and lanes
+// 8-15 mass 1 with the operations glottis_eval applies to that mass (its constants from the
+// tables' gmass row), and each mass's area, A and E terms reach the other half by a row rotation
+// by 8 (xch).  The same values as glottis_eval.
+template <class CT, class XCH>
+AFS_HD inline GlotRes glottis_eval_split(const GlotIn &in, const CT &C, double ratio, const double *p4, int h,
+                                         XCH xch) {
+  const double r1 = 1.0 - ratio;
+  GlotRes res;
+  double *gp = res.gp;
+  {
+#pragma clang fp contract(off)
+    for (int k = 0; k < 6; ++k) gp[k] = r1 * in.fl[k] + ratio * in.fr[k];
+  }
+  const double rel0 = in.rel[0], rel1 = in.rel[1];
+  double chink = gp[4] < 0.0 ? 0.0 : gp[4];
+  double q = glottis_q(gp[0]);
+  double f = fast_sqrt(q);
+  const double inv_f = fast_rcp(f), inv_q = fast_rcp(q);
+  double cord = G_REST_LEN * f;
+  const double inv_cord = fast_rcp(cord);
+  double th0 = G_REST_THICK0 * inv_f, th1 = G_REST_THICK1 * inv_f;
+  const bool m1 = h != 0;
+  const double *K = C.h.gmass[m1 ? 1 : 0];
+  const double rest = m1 ? gp[3] : gp[2], rel = m1 ? rel1 : rel0, relp = m1 ? in.rel[3] : in.rel[2];
+  double olen, clen, ow, cz;
+  glottis_open_close_one(rest, cord, rel, olen, clen, ow, cz);
+  const double area = clampA(olen * ow + chink);
+  const double th = K[6] * inv_f;
+  const double Tt = C.h.Tt;
+  const double p0 = p4[0], p1 = p4[1], p2 = p4[2], p3 = p4[3];
+  double m = K[0] * inv_q;
+  double al = clen * inv_cord;
+  double k = K[1] * q, kc = K[2] * q;
+  double kcp = G_KCOUPLE * q * q;
+  double dr = K[3] + al * 1.0;
+  double rr = 2.0 * dr * K[4];
+  double fo = (m1 ? p2 : p1) * olen * th;
+  fo += 0.5 * 0.5 * ((m1 ? p3 : p0) + (m1 ? p2 : p1)) * K[5] * cord;
+  double rs = (rest >= 0.0) ? rest * (1.0 - cz * inv_cord) : rest;
+  double Am = m + rr * Tt + Tt * Tt * (k + kc * al) + kcp * Tt * Tt;
+  double Em = fo * Tt * Tt + 2.0 * m * rel - m * relp + rr * Tt * rel - Tt * Tt * kc * al * rs;
+  const double oa = xch(area), oA = xch(Am), oE = xch(Em);
+  res.go = GlotOut{m1 ? oa : area, m1 ? area : oa, th0, th1};
+  const double A = m1 ? oA : Am, Dq = m1 ? Am : oA, Ee = m1 ? oE : Em, Ff = m1 ? Em : oE;
+  double B = -kcp * Tt * Tt;
+  double Cq = -kcp * Tt * Tt;
+  double det = A * Dq - B * Cq;
+  if (fabs(det) < 0.000000001) det = 0.000000001;
+  const double inv_det = fast_rcp(det);
+  res.rel[2] = rel0;
+  res.rel[3] = rel1;
+  res.rel[0] = (Ee * Dq - B * Ff) * inv_det;
+  res.rel[1] = (A * Ff - Ee * Cq) * inv_det;
+  return res;
 }
 
 // The glottis state of the sample: new displacements, interpolated controls (X_GP + 1, the lung
@@ -1756,7 +1814,11 @@ AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts
                 [&](Lane<W> &R) {
                   (void)R;
                   const double p4[4] = {X[X_P4 + 0], X[X_P4 + 1], X[X_P4 + 2], X[X_P4 + 3]};
-                  g = glottis_eval<MODEL>(glottis_inputs(X), C, ratio, p4);
+                  if constexpr (Xc::kGlottisSplit && MODEL == AFS_GLOTTIS_TRIANGULAR)
+                    g = glottis_eval_split(glottis_inputs(X), C, ratio, p4, x.half8(),
+                                           [&](double v) { return x.xch8(v); });
+                  else
+                    g = glottis_eval<MODEL>(glottis_inputs(X), C, ratio, p4);
                 });
   x.mark(PH_GEOMETRY);  // (phase marks: cycle accounting of tools/phase_prof, no-ops otherwise)
   x.dyn_neighbors();

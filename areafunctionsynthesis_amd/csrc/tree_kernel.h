@@ -38,6 +38,11 @@ static_assert(TW == 16 || TW == 32, "collectives are written for 16 or 32 lanes 
 
 template <bool PROF>
 struct GpuExec {
+#if defined(AFS_GLOTTIS_SPLIT)
+  static constexpr bool kGlottisSplit = true;   // the glottis' masses on the two lane halves
+#else
+  static constexpr bool kGlottisSplit = false;
+#endif
   int gl;
   Lane<TW> *R;
   uint64_t last = 0;
@@ -156,6 +161,10 @@ struct GpuExec {
     for (int i = 0; i < N; ++i) o.v[i] = shift<K>(v.v[i]);
     g(gl, *R, o);
   }
+  // The lane half (0: lanes 0-7, 1: lanes 8-15 of the utterance) and lane gl ^ 8's value
+  // (row_ror 8 inside the 16-lane row), for glottis_eval_split.
+  __device__ __forceinline__ int half8() const { return (gl >> 3) & 1; }
+  __device__ __forceinline__ static double xch8(double v) { return dpp<0x128>(v); }
   // Word K of this sample's plan (tree_plan.h): lane K of each 16-lane row holds it
   // (R.planw), DPP row_newbcast hands it to the whole row.
   template <int K> __device__ __forceinline__ uint64_t rec() {

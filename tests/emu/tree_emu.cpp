@@ -17,6 +17,7 @@ namespace {
 
 template <int W>
 struct CpuExec {
+  static constexpr bool kGlottisSplit = false;  // (the device's lane split of the glottis masses)
   Lane<W> *R;
   template <class F> void par(F f) { for (int gl = 0; gl < W; ++gl) f(gl, R[gl]); }
   template <class F> void one(F f) { f(R[0]); }
