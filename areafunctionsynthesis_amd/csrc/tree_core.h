@@ -711,10 +711,13 @@ AFS_HD inline GlotRes glottis_eval(const GlotIn &in, const CT &C, double ratio, 
 }
 
 // The triangular glottis with its two masses on the two halves of an utterance's 16 lanes
-// (device, AFS_GLOTTIS_SPLIT): every lane evaluates the shared terms, lanes 0-7 mass 0 and lanes
-// 8-15 mass 1 with the operations glottis_eval applies to that mass (its constants from the
-// tables' gmass row), and each mass's area, A and E terms reach the other half by a row rotation
-// by 8 (xch).  The same values as glottis_eval.
+// (device; AFS_GLOTTIS_UNIFORM keeps glottis_eval): every lane evaluates the shared terms, lanes
+// 0-7 mass 0 and lanes 8-15 mass 1 with the operations glottis_eval applies to that mass (its
+// constants from the tables' gmass row), and each mass's area, A and E terms reach the other
+// half by a row rotation by 8 (xch): ~140 fewer instructions per sample, +1.1 % (A/B,
+// profiles/r03ag_ab.txt).  The same operations as glottis_eval; under the kernel's fma
+// contraction the compiler may fuse a few of them differently than in the uniform form (the
+// parity figures move in their third digit).
 template <class CT, class XCH>
 AFS_HD inline GlotRes glottis_eval_split(const GlotIn &in, const CT &C, double ratio, const double *p4, int h,
                                          XCH xch) {

@@ -38,10 +38,10 @@ static_assert(TW == 16 || TW == 32, "collectives are written for 16 or 32 lanes 
 
 template <bool PROF>
 struct GpuExec {
-#if defined(AFS_GLOTTIS_SPLIT)
-  static constexpr bool kGlottisSplit = true;   // the glottis' masses on the two lane halves
-#else
+#if defined(AFS_GLOTTIS_UNIFORM)  // (A/B variant: every lane evaluates both glottis masses)
   static constexpr bool kGlottisSplit = false;
+#else
+  static constexpr bool kGlottisSplit = true;   // the glottis' masses on the two lane halves
 #endif
   int gl;
   Lane<TW> *R;
