@@ -143,6 +143,10 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       hbuf[0] = (afs::tree::PlanHop *)c->hops[0];
       hbuf[1] = (afs::tree::PlanHop *)c->hops[ov ? 1 : 0];
     }
+    // K6's glottal-tone input (the tree kernel built to leave the tone filter to K6)
+    const bool tone_k6 = !seg(c) && !afs::tree_output_in_kernel() && !afs::tree_tone_in_kernel();
+    if (tone_k6 && (st = ensure(c, &c->p25, &c->p25_bytes, (size_t)B * (size_t)per * sizeof(double))) != AFS_OK)
+      return st;
     hipStream_t ps = ov ? c->plan_stream : c->stream;
     const int two = c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0;
     const afs::SecRec *uo = seg(c) ? c->dev_seg->uo : c->dev_tab->consts.sec;
@@ -174,13 +178,15 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
                       (const uint64_t *)buf[k & 1], per, lanes, (double *)ws, B, c->host_tab.uni,
-                      hbuf[k & 1], hstride};
+                      hbuf[k & 1], hstride, tone_k6 ? (double *)c->p25 : nullptr, per};
       hipEvent_t e1 = prof_event(c);
       if (seg(c)) HIP_TRY(c, afs::launch_seg_synth(afs::SegArgs{a, c->dev_seg}, c->stream));
       else HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
       prof_pair(c, e1, prof_event(c), 0);
       if (!seg(c) && !afs::tree_output_in_kernel())  // K6: the output stage of the launch's samples
-        HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B, c->stream));
+        HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B,
+                                           tone_k6 ? (const double *)c->p25 : nullptr, per,
+                                           c->cfg.options.radiation_from_skin, c->stream));
       if (ov) HIP_TRY(c, hipEventRecord(c->ev_free[k & 1], c->stream));
     }
     return AFS_OK;
@@ -364,6 +370,7 @@ void afs_destroy(afs_ctx *c) {
     if (h) (void)hipFree(h);
   for (void *w : c->plan_work)
     if (w) (void)hipFree(w);
+  if (c->p25) (void)hipFree(c->p25);
   if (c->plan_stream) (void)hipStreamDestroy(c->plan_stream);
   for (hipEvent_t e : {c->ev_go, c->ev_plan[0], c->ev_plan[1], c->ev_free[0], c->ev_free[1]})
     if (e) (void)hipEventDestroy(e);

@@ -39,6 +39,8 @@ struct afs_ctx {
   size_t plan2_bytes = 0;
   void *hops[2] = {nullptr, nullptr};  // tree solver, hops >= PLAN_HOP_MIN: hop records (tree_plan.h PlanHop)
   size_t hops_bytes[2] = {0, 0};
+  void *p25 = nullptr;  // tree solver: section 25's pressure per sample of a launch (K6's tone input)
+  size_t p25_bytes = 0;
   void *plan_work[2] = {nullptr, nullptr};  // hop mode: K5's work lists (the hops decided sample by sample)
   size_t plan_work_bytes[2] = {0, 0};
   bool plan_dense = false;             // AFS_PLAN_DENSE=1: dense records at every hop (A/B, tests)

@@ -30,6 +30,10 @@ struct TreeArgs {
   // samples of mixed hops only
   const tree::PlanHop *hops = nullptr;
   int64_t hop_stride = 0;
+  // section 25's pressure per sample (p25[u * p25_stride + s - s_begin]), K6's glottal-tone
+  // input, unless the kernel filters the tone itself (tree_tone_in_kernel())
+  double *p25 = nullptr;
+  int64_t p25_stride = 0;
 };
 // K5: the noise-source plans of samples [s_begin, s_end) of `rows` frame rows.
 struct PlanArgs {
@@ -73,8 +77,9 @@ hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st);
 // it stored (out[u * out_stride + s - s_begin], replaced by the audio).  Not needed when the
 // synthesis kernel was built to filter itself (tree_output_in_kernel(): the A/B variant).
 hipError_t launch_tree_output(const Tables *tab, double *lds_state, double *out, int64_t out_stride, int64_t n, int B,
-                              hipStream_t st);
+                              const double *p25, int64_t p25_stride, int skin, hipStream_t st);
 bool tree_output_in_kernel();
+bool tree_tone_in_kernel();
 hipError_t launch_tree_nonfinite(const double *lds_state, int B, int32_t *count, uint8_t *flags, hipStream_t st);
 hipError_t launch_tree_draws(const double *lds_state, int B, int64_t *draws, hipStream_t st);
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st);

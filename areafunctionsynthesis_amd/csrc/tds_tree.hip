@@ -21,11 +21,17 @@ __global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_synth_kerne
 // 32767 (Synthesizer.cpp:614-627) -- over the radiated flows the synthesis kernel stored, in
 // place, one thread per utterance; the filter state (X_OUTF, X_PREVFLOW, X_NONFIN) lives in the
 // utterance's saved LDS image, which the synthesis kernel carries through unchanged.
+// With p25 (the synthesis kernel built without the tone filter): first the glottal-tone filter
+// (skin radiation) over section 25's stored pressures, added to the flows (tone_run).
 __global__ void __launch_bounds__(64) tree_output_kernel(const Tables *tab, double *lds_state, double *out,
-                                                         int64_t out_stride, int64_t n, int B) {
+                                                         int64_t out_stride, int64_t n, int B, const double *p25,
+                                                         int64_t p25_stride, int skin) {
   const int u = blockIdx.x * 64 + threadIdx.x;
   if (u >= B) return;
-  output_filter_run(lds_state + (int64_t)u * X_TOTAL, tab->consts, out + (int64_t)u * out_stride, (int)n);
+  double *X = lds_state + (int64_t)u * X_TOTAL;
+  double *o = out + (int64_t)u * out_stride;
+  if (p25 && skin) tone_run(X, tab->consts, p25 + (int64_t)u * p25_stride, o, (int)n);
+  output_filter_run(X, tab->consts, o, (int)n);
 }
 
 // seeds == nullptr: utterance u is seeded u + 1 (afs.h)
@@ -97,10 +103,13 @@ bool tree_output_in_kernel() {
 #endif
 }
 
+bool tree_tone_in_kernel() { return !GpuExec<false>::kToneOut; }
+
 hipError_t launch_tree_output(const Tables *tab, double *lds_state, double *out, int64_t out_stride, int64_t n, int B,
-                              hipStream_t st) {
+                              const double *p25, int64_t p25_stride, int skin, hipStream_t st) {
   if (B <= 0 || n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(tree_output_kernel, dim3((B + 63) / 64), dim3(64), 0, st, tab, lds_state, out, out_stride, n, B);
+  hipLaunchKernelGGL(tree_output_kernel, dim3((B + 63) / 64), dim3(64), 0, st, tab, lds_state, out, out_stride, n, B,
+                     p25, p25_stride, skin);
   return hipGetLastError();
 }
 

@@ -1790,6 +1790,45 @@ constexpr int OUT_DEFER_MIN_HOP = 32;
 // Phase O (lane-uniform): radiated flow and glottal tone (TdsModel.cpp:687-705); with
 // defer == false also the output filter.  Returns the audio sample, or with defer the flow.
 // p25 = the new pressure of section 25 (section_pressure), the glottal tone filter's input.
+// The radiated flow alone (the device kernel: the glottal-tone filter runs in K6 from the
+// stored p[25], tone_run).
+AFS_HD inline double phase_output_flow(const double *X) {
+  double flow = 0.0;
+  flow += X[X_U + 93];
+  flow += X[X_U + 94];
+  flow += X[X_U + 95];
+  flow += X[X_U + 96];
+  return flow;
+}
+
+// The glottal-tone filter (skin radiation, TdsModel.cpp:687-705) over n samples: p25[i] is
+// section 25's new pressure of sample i, o[i] its radiated flow, to which the tone is added.
+// The state (X_TONE) in registers over the run; uncontracted (as output_filter_run: the result
+// does not depend on where a run starts).
+AFS_HD inline void tone_run(double *X, const Consts &C, const double *p25, double *o, int n) {
+#pragma clang fp contract(off)
+  double sx[4], sy[4], ca[5], cb[5];
+  for (int k = 0; k < 4; ++k) { sx[k] = X[X_TONE + k]; sy[k] = X[X_TONE + 4 + k]; }
+  for (int k = 0; k <= 4; ++k) { ca[k] = C.h.tone_a[k]; cb[k] = C.h.tone_b[k]; }
+  for (int i = 0; i < n; ++i) {
+    const double x = p25[i];
+    double acc = ca[0] * x;
+#pragma unroll
+    for (int k = 1; k <= 4; ++k) {
+      acc += ca[k] * sx[k - 1];
+      acc += cb[k] * sy[k - 1];
+    }
+#pragma unroll
+    for (int k = 3; k > 0; --k) { sx[k] = sx[k - 1]; sy[k] = sy[k - 1]; }
+    sx[0] = x;
+    sy[0] = acc;
+    double flow = o[i];
+    flow += acc;
+    o[i] = flow;
+  }
+  for (int k = 0; k < 4; ++k) { X[X_TONE + k] = sx[k]; X[X_TONE + 4 + k] = sy[k]; }
+}
+
 AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, double p25, bool defer) {
   double flow = 0.0;
   flow += X[X_U + 93];
@@ -1865,7 +1904,10 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   rng_ahead<W>(x, X);
   // the state update and the output stage (lane-uniform: radiated flow, filters) in one phase
   x.par_uniform([&](int gl, Lane<W> &R) { phase_update<W>(gl, R, X, X, U, C); },
-                [&](Lane<W> &R) { R.sample = phase_output(X, U, C, section_pressure(X, C, S_PHARYNX0), defer_out); });
+                [&](Lane<W> &R) {
+                  if constexpr (Xc::kToneOut) R.sample = phase_output_flow(X);
+                  else R.sample = phase_output(X, U, C, section_pressure(X, C, S_PHARYNX0), defer_out);
+                });
   x.sync();
   x.mark(PH_UPDATE);
   x.mark(PH_OUTPUT);

@@ -38,6 +38,11 @@ static_assert(TW == 16 || TW == 32, "collectives are written for 16 or 32 lanes 
 
 template <bool PROF>
 struct GpuExec {
+#if defined(AFS_TONE_IN_KERNEL) || defined(AFS_K1_FILTER)  // (A/B variant: the glottal-tone filter in the step)
+  static constexpr bool kToneOut = false;
+#else
+  static constexpr bool kToneOut = true;        // the tone filter in K6 from the stored p[25]
+#endif
 #if defined(AFS_GLOTTIS_UNIFORM)  // (A/B variant: every lane evaluates both glottis masses)
   static constexpr bool kGlottisSplit = false;
 #else
@@ -217,6 +222,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   const int64_t row = a.frame_row ? a.frame_row[ue] : ue;
   const afs_frame *fu = a.frames + row * a.frame_stride;
   double *o = a.out + (int64_t)ue * a.out_stride;
+  double *p25o = a.p25 ? a.p25 + (int64_t)ue * a.p25_stride : nullptr;
   // this utterance's plan records, word gl % 16 of each (tree_plan.h)
   const uint64_t *pl = a.plan + row * a.plan_stride * PLAN_WORDS + (gl & (PLAN_WORDS - 1));
   const int hop = a.hop;
@@ -276,6 +282,9 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
 #endif
     sample_step<TW, MODEL>(ex, X, a.uni, C, ratio, defer);
     if (valid && gl == 0) o[t] = R.sample;
+    // section 25's new pressure (lane 2's slot 0), the glottal-tone filter's input in K6
+    if constexpr (GpuExec<PROF>::kToneOut)
+      if (valid && gl == 2 && p25o) p25o[t] = R.p[0];
     if (++i == hop) {
 #if defined(AFS_K1_FILTER)
       if (defer && valid && gl == 0) output_filter_run(X, C, o + t0, (int)(t + 1 - t0));

@@ -18,6 +18,7 @@ namespace {
 template <int W>
 struct CpuExec {
   static constexpr bool kGlottisSplit = false;  // (the device's lane split of the glottis masses)
+  static constexpr bool kToneOut = false;       // (the device's tone filter in K6)
   Lane<W> *R;
   template <class F> void par(F f) { for (int gl = 0; gl < W; ++gl) f(gl, R[gl]); }
   template <class F> void one(F f) { f(R[0]); }
