@@ -15,10 +15,10 @@ using namespace afs::tree;
 
 namespace {
 
-template <int W>
+template <int W, bool TONE = false>
 struct CpuExec {
   static constexpr bool kGlottisSplit = false;  // (the device's lane split of the glottis masses)
-  static constexpr bool kToneOut = false;       // (the device's tone filter in K6)
+  static constexpr bool kToneOut = TONE;        // the device's tone filter in K6 (emu_tree_set_tone_k6)
   Lane<W> *R;
   template <class F> void par(F f) { for (int gl = 0; gl < W; ++gl) f(gl, R[gl]); }
   template <class F> void one(F f) { f(R[0]); }
@@ -80,9 +80,13 @@ struct CpuExec {
 // kernel), mixed hops from the dense records.  Off by default (dense records at every hop).
 int g_hop_mode = 0;
 long g_hops = 0, g_mixed_hops = 0;
+// Tone-in-K6 mode (the device default): the sample step leaves out the glottal-tone filter, lane
+// 2's slot 0 (section 25's new pressure) is stored per sample, and tone_run adds the tone to the
+// hop's flows before the output filter -- as tree_kernel.h + tree_output_kernel.  Off by default.
+int g_tone_k6 = 0;
 
-template <int W>
-long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, const afs_options &opt,
+template <int W, bool TONE>
+long run_impl(const afs_frame *frames, int F, int hop, unsigned seed, double fs, const afs_options &opt,
          double *out, double *dump_p, double *dump_u, int ndump) {
   static Tables T;
   build_tables(&T, fs, opt);
@@ -91,9 +95,11 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
   std::vector<double> X(X_TOTAL);
   for (int gl = 0; gl < W; ++gl) reset_lane<W>(gl, R[gl]);
   reset_lds(X.data(), seed);
-  CpuExec<W> ex{R.data()};
+  CpuExec<W, TONE> ex{R.data()};
   long t = 0;
-  const bool defer = hop >= OUT_DEFER_MIN_HOP;  // as the GPU kernel (tree_kernel.h)
+  // as the GPU kernel (tree_kernel.h): the tone-in-K6 build always defers the output filter
+  const bool defer = TONE || hop >= OUT_DEFER_MIN_HOP;
+  std::vector<double> p25(TONE ? hop : 0);
   const bool two = opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
   const bool hops = g_hop_mode && hop >= PLAN_HOP_MIN;
   for (int k = 1; k < F; ++k) {
@@ -118,6 +124,7 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
       else
         sample_step<W, AFS_GLOTTIS_TRIANGULAR>(ex, X.data(), T.uni, T.consts, ratio, defer);
       out[t] = R[0].sample;
+      if constexpr (TONE) p25[i] = R[2].p[0];
       if (t < ndump) {
         for (int gl = 0; gl < W; ++gl)
           for (int j = 0; j < Shape<W>::NSL; ++j) {
@@ -128,9 +135,18 @@ long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, cons
       }
       ++t;
     }
+    if constexpr (TONE)
+      if (opt.radiation_from_skin) tone_run(X.data(), T.consts, p25.data(), out + t0, hop);
     if (defer) output_filter_run(X.data(), T.consts, out + t0, hop);
   }
   return t;
+}
+
+template <int W>
+long run(const afs_frame *frames, int F, int hop, unsigned seed, double fs, const afs_options &opt,
+         double *out, double *dump_p, double *dump_u, int ndump) {
+  return g_tone_k6 ? run_impl<W, true>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump)
+                   : run_impl<W, false>(frames, F, hop, seed, fs, opt, out, dump_p, dump_u, ndump);
 }
 
 }  // namespace
@@ -165,6 +181,7 @@ extern "C" long emu_tree_utterance_opt(const afs_frame *frames, int F, int hop, 
 }
 
 extern "C" void emu_tree_set_hop_mode(int on) { g_hop_mode = on; }
+extern "C" void emu_tree_set_tone_k6(int on) { g_tone_k6 = on; }
 // hops run in hop mode since the last call, and how many of them were mixed
 extern "C" void emu_tree_hop_counts(long *hops, long *mixed) {
   *hops = g_hops;

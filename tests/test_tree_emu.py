@@ -207,3 +207,36 @@ def test_hop_mode_every_shape_vs_oracle(emu, oracle, hop_mode):
         assert np.abs(x - y).max() <= TOL, seq
     hops, mixed = hop_mode()
     assert 0 < mixed < hops, (hops, mixed)
+
+
+@pytest.mark.parametrize("hop", [7, 97, 441])
+@pytest.mark.parametrize("skin", [1, 0])
+def test_tone_in_k6_vs_in_step(emu, oracle, hop, skin):
+    """The device default leaves the glottal-tone (skin radiation) filter out of the sample step:
+    the synthesis kernel stores section 25's new pressure (lane 2, slot 0) per sample and K6 runs
+    the filter over the hop (tree_core.h tone_run) before the output filter (TdsModel.cpp:687-705).
+    Emulated that way, deferred hops give bitwise the audio of the in-step filter, and every hop
+    length matches the oracle."""
+    from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS
+    from areafunctionsynthesis_amd.params import default_shapes
+    lib = emu.lib
+    lib.emu_tree_set_tone_k6.argtypes = [ctypes.c_int]
+    sh = default_shapes()
+    frames = []
+    for name, f0 in (("a:", 120.0), ("s", 125.0), ("i:", 130.0)):
+        f = oracle.af_to_frame(sh[name])
+        f["glottis"] = DEFAULT_GLOTTIS
+        f["glottis"][0] = f0
+        frames.append(f)
+    frames = np.stack(frames * 3)
+    opt = {"radiation_from_skin": skin}
+    lib.emu_tree_set_tone_k6(1)
+    try:
+        x = emu.opt(frames, hop, 7, 22050.0, opt)
+    finally:
+        lib.emu_tree_set_tone_k6(0)
+    y = emu.opt(frames, hop, 7, 22050.0, opt)
+    if hop >= 32:  # OUT_DEFER_MIN_HOP: both defer the output filter
+        assert np.array_equal(x, y)
+    z = oracle.utterance(frames, hop, 7, 22050.0, opt=opt)
+    assert np.abs(x - z).max() <= TOL
