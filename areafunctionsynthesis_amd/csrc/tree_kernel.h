@@ -38,10 +38,10 @@ static_assert(TW == 16 || TW == 32, "collectives are written for 16 or 32 lanes 
 
 template <bool PROF>
 struct GpuExec {
-#if defined(AFS_TONE_K6) && !defined(AFS_K1_FILTER)  // (A/B variant: the tone filter in K6 from the stored p[25])
-  static constexpr bool kToneOut = true;
+#if defined(AFS_TONE_IN_KERNEL) || defined(AFS_K1_FILTER)  // (A/B variant: the glottal-tone filter in the step)
+  static constexpr bool kToneOut = false;
 #else
-  static constexpr bool kToneOut = false;       // the glottal-tone filter in the sample step
+  static constexpr bool kToneOut = true;        // the tone filter in K6 from the stored p[25]
 #endif
 #if defined(AFS_GLOTTIS_UNIFORM)  // (A/B variant: every lane evaluates both glottis masses)
   static constexpr bool kGlottisSplit = false;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-3 session ai: the glottal-tone filter in K6 from a stored p[25] per sample (tonek6,
-# -DAFS_TONE_K6) against the filter inside the sample step (tonein, the default build); config 4 and
+# the default build since) against the filter inside the sample step (tonein, -DAFS_TONE_IN_KERNEL); config 4 and
 # config 3; then the tree GPU tests on tonek6
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
