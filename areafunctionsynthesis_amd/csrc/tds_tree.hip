@@ -22,7 +22,8 @@ __global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_synth_kerne
 // place, one thread per utterance; the filter state (X_OUTF, X_PREVFLOW, X_NONFIN) lives in the
 // utterance's saved LDS image, which the synthesis kernel carries through unchanged.
 // With p25 (the synthesis kernel built without the tone filter): first the glottal-tone filter
-// (skin radiation) over section 25's stored pressures, added to the flows (tone_run).
+// (skin radiation) over section 25's stored pressures, added to the flows, in the output filter's
+// loop (tone_output_run).
 __global__ void __launch_bounds__(64) tree_output_kernel(const Tables *tab, double *lds_state, double *out,
                                                          int64_t out_stride, int64_t n, int B, const double *p25,
                                                          int64_t p25_stride, int skin) {
@@ -30,8 +31,8 @@ __global__ void __launch_bounds__(64) tree_output_kernel(const Tables *tab, doub
   if (u >= B) return;
   double *X = lds_state + (int64_t)u * X_TOTAL;
   double *o = out + (int64_t)u * out_stride;
-  if (p25 && skin) tone_run(X, tab->consts, p25 + (int64_t)u * p25_stride, o, (int)n);
-  output_filter_run(X, tab->consts, o, (int)n);
+  if (p25 && skin) tone_output_run(X, tab->consts, p25 + (int64_t)u * p25_stride, o, (int)n);
+  else output_filter_run(X, tab->consts, o, (int)n);
 }
 
 // seeds == nullptr: utterance u is seeded u + 1 (afs.h)

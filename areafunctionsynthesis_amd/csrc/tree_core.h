@@ -1733,7 +1733,12 @@ AFS_HD inline double output_filter_one(double *X, const Consts &C, double flow) 
 // (A 16-entry window moved once per 8-sample block instead of the per-sample shift -- the same
 // operations, 16 instead of 128 register moves per block -- measured 2 % slower end to end: the
 // window's 64 registers push persistent state into AGPRs, profiles/r03w_ab.txt.)
-AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int n) {
+// TONE: first the glottal-tone filter (skin radiation, TdsModel.cpp:687-705) over p25[i], section
+// 25's new pressure of sample i, its output added to the flow o[i] (the same operations as
+// phase_output, so bitwise the same audio): one loop, so that the tone chain of sample i + 1 and
+// the output filter's chain of sample i (independent) overlap, instead of two runs back to back.
+template <bool TONE>
+AFS_HD inline void output_filter_run_t(double *X, const Consts &C, double *o, int n, const double *p25) {
   // (not contracted into fmas: each product and sum rounds as in the reference, so the result does
   // not depend on where a run starts -- a session's per-call runs equal one run over the whole
   // trajectory bit for bit; with contraction the compiler may pair the terms differently in
@@ -1747,18 +1752,46 @@ AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int 
   const double inv_dt = C.h.inv_dt;
   double prev = X[X_PREVFLOW];
   bool nonfin = false;
-  double f[8];
+  double tx[4], ty[4], ta[5], tb[5];
+  if constexpr (TONE) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) f[i] = (i < n) ? o[i] : 0.0;
+    for (int k = 0; k < 4; ++k) { tx[k] = X[X_TONE + k]; ty[k] = X[X_TONE + 4 + k]; }
+#pragma unroll
+    for (int k = 0; k <= 4; ++k) { ta[k] = C.h.tone_a[k]; tb[k] = C.h.tone_b[k]; }
+  }
+  double f[8], fp[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    f[i] = (i < n) ? o[i] : 0.0;
+    if constexpr (TONE) fp[i] = (i < n) ? p25[i] : 0.0;
+  }
   for (int t0 = 0; t0 < n; t0 += 8) {
-    double g[8];
+    double g[8], gp[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) g[i] = (t0 + 8 + i < n) ? o[t0 + 8 + i] : 0.0;
+    for (int i = 0; i < 8; ++i) {
+      g[i] = (t0 + 8 + i < n) ? o[t0 + 8 + i] : 0.0;
+      if constexpr (TONE) gp[i] = (t0 + 8 + i < n) ? p25[t0 + 8 + i] : 0.0;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if (t0 + i >= n) break;
-      const double op = (f[i] - prev) * inv_dt;
-      prev = f[i];
+      double flow = f[i];
+      if constexpr (TONE) {
+        const double x = fp[i];
+        double tacc = ta[0] * x;
+#pragma unroll
+        for (int k = 1; k <= 4; ++k) {
+          tacc += ta[k] * tx[k - 1];
+          tacc += tb[k] * ty[k - 1];
+        }
+#pragma unroll
+        for (int k = 3; k > 0; --k) { tx[k] = tx[k - 1]; ty[k] = ty[k - 1]; }
+        tx[0] = x;
+        ty[0] = tacc;
+        flow += tacc;
+      }
+      const double op = (flow - prev) * inv_dt;
+      prev = flow;
       double acc = ca[0] * op;
 #pragma unroll
       for (int k = 1; k <= 8; ++k) {
@@ -1775,12 +1808,27 @@ AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int 
       o[t0 + i] = smp;
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = g[i];
+    for (int i = 0; i < 8; ++i) {
+      f[i] = g[i];
+      if constexpr (TONE) fp[i] = gp[i];
+    }
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) { X[X_OUTF + k] = sx[k]; X[X_OUTF + 8 + k] = sy[k]; }
   X[X_PREVFLOW] = prev;
   if (nonfin) X[X_NONFIN] = 1.0;
+  if constexpr (TONE) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { X[X_TONE + k] = tx[k]; X[X_TONE + 4 + k] = ty[k]; }
+  }
+}
+
+AFS_HD inline void output_filter_run(double *X, const Consts &C, double *o, int n) {
+  output_filter_run_t<false>(X, C, o, n, nullptr);
+}
+// the glottal-tone filter and the output stage over n samples in one loop (K6 of the tone-in-K6 build)
+AFS_HD inline void tone_output_run(double *X, const Consts &C, const double *p25, double *o, int n) {
+  output_filter_run_t<true>(X, C, o, n, p25);
 }
 
 // Hops of at least this many samples run the output filter once per hop (output_filter_run)
@@ -1791,7 +1839,7 @@ constexpr int OUT_DEFER_MIN_HOP = 32;
 // defer == false also the output filter.  Returns the audio sample, or with defer the flow.
 // p25 = the new pressure of section 25 (section_pressure), the glottal tone filter's input.
 // The radiated flow alone (the device kernel: the glottal-tone filter runs in K6 from the
-// stored p[25], tone_run).
+// stored p[25], tone_output_run).
 AFS_HD inline double phase_output_flow(const double *X) {
   double flow = 0.0;
   flow += X[X_U + 93];
@@ -1799,34 +1847,6 @@ AFS_HD inline double phase_output_flow(const double *X) {
   flow += X[X_U + 95];
   flow += X[X_U + 96];
   return flow;
-}
-
-// The glottal-tone filter (skin radiation, TdsModel.cpp:687-705) over n samples: p25[i] is
-// section 25's new pressure of sample i, o[i] its radiated flow, to which the tone is added.
-// The state (X_TONE) in registers over the run; uncontracted (as output_filter_run: the result
-// does not depend on where a run starts).
-AFS_HD inline void tone_run(double *X, const Consts &C, const double *p25, double *o, int n) {
-#pragma clang fp contract(off)
-  double sx[4], sy[4], ca[5], cb[5];
-  for (int k = 0; k < 4; ++k) { sx[k] = X[X_TONE + k]; sy[k] = X[X_TONE + 4 + k]; }
-  for (int k = 0; k <= 4; ++k) { ca[k] = C.h.tone_a[k]; cb[k] = C.h.tone_b[k]; }
-  for (int i = 0; i < n; ++i) {
-    const double x = p25[i];
-    double acc = ca[0] * x;
-#pragma unroll
-    for (int k = 1; k <= 4; ++k) {
-      acc += ca[k] * sx[k - 1];
-      acc += cb[k] * sy[k - 1];
-    }
-#pragma unroll
-    for (int k = 3; k > 0; --k) { sx[k] = sx[k - 1]; sy[k] = sy[k - 1]; }
-    sx[0] = x;
-    sy[0] = acc;
-    double flow = o[i];
-    flow += acc;
-    o[i] = flow;
-  }
-  for (int k = 0; k < 4; ++k) { X[X_TONE + k] = sx[k]; X[X_TONE + 4 + k] = sy[k]; }
 }
 
 AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, double p25, bool defer) {

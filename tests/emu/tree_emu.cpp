@@ -81,7 +81,7 @@ struct CpuExec {
 int g_hop_mode = 0;
 long g_hops = 0, g_mixed_hops = 0;
 // Tone-in-K6 mode (the device default): the sample step leaves out the glottal-tone filter, lane
-// 2's slot 0 (section 25's new pressure) is stored per sample, and tone_run adds the tone to the
+// 2's slot 0 (section 25's new pressure) is stored per sample, and tone_output_run adds the tone to the
 // hop's flows before the output filter -- as tree_kernel.h + tree_output_kernel.  Off by default.
 int g_tone_k6 = 0;
 
@@ -135,9 +135,8 @@ long run_impl(const afs_frame *frames, int F, int hop, unsigned seed, double fs,
       }
       ++t;
     }
-    if constexpr (TONE)
-      if (opt.radiation_from_skin) tone_run(X.data(), T.consts, p25.data(), out + t0, hop);
-    if (defer) output_filter_run(X.data(), T.consts, out + t0, hop);
+    if (TONE && opt.radiation_from_skin) tone_output_run(X.data(), T.consts, p25.data(), out + t0, hop);
+    else if (defer) output_filter_run(X.data(), T.consts, out + t0, hop);
   }
   return t;
 }

@@ -214,7 +214,7 @@ def test_hop_mode_every_shape_vs_oracle(emu, oracle, hop_mode):
 def test_tone_in_k6_vs_in_step(emu, oracle, hop, skin):
     """The device default leaves the glottal-tone (skin radiation) filter out of the sample step:
     the synthesis kernel stores section 25's new pressure (lane 2, slot 0) per sample and K6 runs
-    the filter over the hop (tree_core.h tone_run) before the output filter (TdsModel.cpp:687-705).
+    the filter in the output filter's loop (tree_core.h tone_output_run, TdsModel.cpp:687-705).
     Emulated that way, deferred hops give bitwise the audio of the in-step filter, and every hop
     length matches the oracle."""
     from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS
