@@ -18,7 +18,6 @@ STATUS = {0: "ok", 1: "invalid argument", 2: "no HIP device", 3: "HIP runtime er
 AFS_SOLVER_CHOLESKY = 0
 AFS_SOLVER_TREE = 1
 AFS_SOLVER_SOR = 2
-AFS_SOLVER_SEG = 3
 AFS_PLAN_WORDS = 16  # afs.h
 AFS_PLAN_HOP_BYTES = 544  # afs.h
 AFS_PLAN_HOP_MIN = 32  # afs.h
@@ -33,9 +32,10 @@ EXPORTED = (
     "afs_last_error", "afs_set_stream", "afs_synchronize", "afs_synthesize",
     "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_session_destroy",
     "afs_af_to_frames", "afs_to_int16", "afs_target_sequence_default", "afs_target_sequence_samples",
-    "afs_play_target_sequences", "afs_rng_draws", "afs_noise_plans", "afs_noise_plan_hops", "afs_tube_interpolate", "afs_session_rng_draws", "afs_kernel_times",
+    "afs_play_target_sequences", "afs_rng_draws", "afs_noise_plans", "afs_noise_plan_hops", "afs_plan_hop_words", "afs_tube_interpolate", "afs_session_rng_draws", "afs_kernel_times",
+    "afs_kernel_times_ex",
     "afs_shard_range", "afs_comm_unique_id", "afs_comm_create", "afs_comm_create_all", "afs_comm_destroy",
-    "afs_gather_pcm", "afs_comm_fence", "afs_comm_synchronize", "afs_multi_synthesize",
+    "afs_gather_pcm", "afs_comm_fence", "afs_comm_synchronize", "afs_comm_gather_times", "afs_multi_synthesize",
 )
 
 
@@ -62,6 +62,12 @@ class AfsConfig(ctypes.Structure):
 class AfsReport(ctypes.Structure):
     _fields_ = [("device_ms", ctypes.c_double), ("samples", ctypes.c_int64),
                 ("nonfinite_utterances", ctypes.c_int32), ("kernel", ctypes.c_int32)]
+
+
+class AfsKernelTiming(ctypes.Structure):
+    _fields_ = [("synth_ms", ctypes.c_double), ("synth_launches", ctypes.c_int32),
+                ("plan_ms", ctypes.c_double), ("plan_launches", ctypes.c_int32),
+                ("output_ms", ctypes.c_double), ("output_launches", ctypes.c_int32)]
 
 
 class AfsError(RuntimeError):
@@ -101,6 +107,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                                     ctypes.c_int64, vp]
     lib.afs_noise_plan_hops.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                         ctypes.c_int64, vp, vp]
+    lib.afs_plan_hop_words.argtypes = [vp, vp, vp, ctypes.c_int32, vp]
     lib.afs_session_rng_draws.argtypes = [vp, vp]
     lib.afs_session_create.argtypes = [vp, ctypes.c_int32, vp, ctypes.POINTER(vp)]
     lib.afs_session_synthesize.argtypes = [vp, vp, ctypes.c_int32, vp, vp, ctypes.POINTER(ctypes.c_int32),
@@ -117,6 +124,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                                               ctypes.c_int32, vp, vp, ctypes.POINTER(AfsReport)]
     i32p, i64p, dp = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)
     lib.afs_kernel_times.argtypes = [vp, dp, i32p, dp, i32p]
+    lib.afs_kernel_times_ex.argtypes = [vp, ctypes.POINTER(AfsKernelTiming)]
     lib.afs_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, i64p, i64p]
     lib.afs_shard_range.restype = None
     lib.afs_comm_unique_id.argtypes = [vp]
@@ -127,13 +135,15 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.afs_gather_pcm.argtypes = [vp, vp, ctypes.c_int64, vp, vp]
     lib.afs_comm_fence.argtypes = [vp]
     lib.afs_comm_synchronize.argtypes = [vp]
+    lib.afs_comm_gather_times.argtypes = [vp, dp, i32p]
     lib.afs_multi_synthesize.argtypes = [vp, vp, ctypes.c_int32, vp, vp, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, vp, vp, ctypes.POINTER(AfsReport)]
     for name in ("afs_create", "afs_set_stream", "afs_synchronize", "afs_synthesize",
                  "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_af_to_frames",
-                 "afs_to_int16", "afs_play_target_sequences", "afs_rng_draws", "afs_session_rng_draws",
-                 "afs_kernel_times", "afs_comm_unique_id", "afs_comm_create", "afs_comm_create_all",
-                 "afs_gather_pcm", "afs_comm_fence", "afs_comm_synchronize", "afs_multi_synthesize"):
+                 "afs_to_int16", "afs_play_target_sequences", "afs_rng_draws", "afs_session_rng_draws", "afs_plan_hop_words",
+                 "afs_kernel_times", "afs_kernel_times_ex", "afs_comm_unique_id", "afs_comm_create", "afs_comm_create_all",
+                 "afs_gather_pcm", "afs_comm_fence", "afs_comm_synchronize", "afs_comm_gather_times",
+                 "afs_multi_synthesize"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib

@@ -14,10 +14,9 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libafs.so")
 ARCH = os.environ.get("AFS_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["afs_capi.cpp", "afs_comm.cpp", "afs_tables.cpp", "seg_tables.cpp", "tds_lane.hip", "tds_tree.hip", "tds_seg.hip",
-           "tds_plan.hip", "af_kernels.hip", "audio_kernels.hip"]
+SOURCES = ["afs_capi.cpp", "afs_comm.cpp", "afs_tables.cpp", "tds_lane.hip", "tds_tree.hip", "tds_plan.hip",
+           "af_kernels.hip", "audio_kernels.hip"]
 HEADERS = ["afs_model.h", "afs_ctx.h", "afs_gather.h", "afs_af.h", "afs_lane.h", "afs_tree.h", "afs_audio.h", "tree_core.h", "tree_plan.h", "tree_kernel.h",
-           "seg_model.h", "seg_core.h", "seg_kernel.h", "afs_seg.h",
            os.path.join("..", "..", "include", "afs.h")]
 # Per-source extra flags.
 # The tree kernel contracts a*b+c into fma (-ffp-contract=fast-honor-pragmas after COMMON's
@@ -38,7 +37,7 @@ HEADERS = ["afs_model.h", "afs_ctx.h", "afs_gather.h", "afs_af.h", "afs_lane.h",
 # scheduler / no machine sinking / no memop clustering neutral or slower).  Instruction order
 # only: the results are bit-identical.
 TREE_FLAGS = ["-mllvm", "-disable-machine-licm", "-ffp-contract=fast-honor-pragmas", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
-PER_SOURCE: dict = {"tds_tree.hip": list(TREE_FLAGS), "tds_seg.hip": list(TREE_FLAGS)}
+PER_SOURCE: dict = {"tds_tree.hip": list(TREE_FLAGS)}
 # (AFS_TREE_FLAGS: extra compiler flags for the tree kernel, for A/B builds of scheduler options)
 if os.environ.get("AFS_TREE_FLAGS"):
     PER_SOURCE["tds_tree.hip"] = TREE_FLAGS + os.environ["AFS_TREE_FLAGS"].split()
@@ -94,8 +93,6 @@ def build(force: bool = False, verbose: bool = True) -> str:
 # the headers the synthesis kernels' objects are compiled from (host-only headers excluded)
 KERNEL_HEADERS = {"tds_tree.hip": ["afs_model.h", "afs_tree.h", "tree_core.h", "tree_plan.h", "tree_kernel.h",
                                    os.path.join("..", "..", "include", "afs.h")],
-                  "tds_seg.hip": ["afs_model.h", "afs_tree.h", "tree_core.h", "tree_plan.h", "seg_model.h",
-                                  "seg_core.h", "seg_kernel.h", "afs_seg.h", os.path.join("..", "..", "include", "afs.h")],
                   "tds_plan.hip": ["afs_model.h", "afs_tree.h", "tree_plan.h", os.path.join("..", "..", "include", "afs.h")]}
 
 

@@ -21,7 +21,6 @@
 #include "afs_audio.h"
 #include "afs_ctx.h"
 #include "afs_model.h"
-#include "afs_seg.h"
 #include "afs_tree.h"
 
 static_assert(sizeof(afs_frame) == 1072, "afs_frame layout");
@@ -69,13 +68,10 @@ namespace {
 
 int64_t pad64(int64_t b) { return (b + 63) / 64 * 64; }
 
-bool solver_ok(int32_t s) {
-  return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_TREE || s == AFS_SOLVER_SOR || s == AFS_SOLVER_SEG;
-}
+bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_TREE || s == AFS_SOLVER_SOR; }
 
-// the cooperative kernels (16 lanes per utterance, noise-source plans from K5): tree and seg
-bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE || c->cfg.solver == AFS_SOLVER_SEG; }
-bool seg(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_SEG; }
+// the cooperative kernel (16 lanes per utterance, noise-source plans from K5)
+bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE; }
 
 // Bytes of noise-source plans one tree launch may use (afs_ctx::plan_budget: 4 GiB, or
 // AFS_PLAN_BUDGET_MB); a launch covers at most plan_budget / (rows * 128 B) samples and at most
@@ -130,7 +126,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     void *buf[2] = {c->plan, ov ? c->plan2 : c->plan};
     // hop mode (tree solver, hops >= PLAN_HOP_MIN): K5 writes one record per (row, hop) and the
     // dense records of mixed hops only; K1 evaluates the words from the hop records
-    const bool hops = !seg(c) && !c->plan_dense && hop >= afs::tree::PLAN_HOP_MIN;
+    const bool hops = !c->plan_dense && hop >= afs::tree::PLAN_HOP_MIN;
     const int64_t hstride = afs::plan_hop_slots(0, per, hop) + 1;  // (a chunk may start inside a hop)
     afs::tree::PlanHop *hbuf[2] = {nullptr, nullptr};
     if (hops) {
@@ -143,13 +139,11 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       hbuf[0] = (afs::tree::PlanHop *)c->hops[0];
       hbuf[1] = (afs::tree::PlanHop *)c->hops[ov ? 1 : 0];
     }
-    // K6's glottal-tone input (the tree kernel built to leave the tone filter to K6)
-    const bool tone_k6 = !seg(c) && !afs::tree_output_in_kernel() && !afs::tree_tone_in_kernel();
-    if (tone_k6 && (st = ensure(c, &c->p25, &c->p25_bytes, (size_t)B * (size_t)per * sizeof(double))) != AFS_OK)
-      return st;
+    // K6's glottal-tone input: section 25's pressure per sample of the launch
+    if ((st = ensure(c, &c->p25, &c->p25_bytes, (size_t)B * (size_t)per * sizeof(double))) != AFS_OK) return st;
     hipStream_t ps = ov ? c->plan_stream : c->stream;
     const int two = c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0;
-    const afs::SecRec *uo = seg(c) ? c->dev_seg->uo : c->dev_tab->consts.sec;
+    const afs::SecRec *uo = c->dev_tab->consts.sec;
     auto plan_chunk = [&](int64_t k) -> afs_status {
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)buf[k & 1], per, two, uo,
@@ -178,15 +172,15 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
                       (const uint64_t *)buf[k & 1], per, lanes, (double *)ws, B, c->host_tab.uni,
-                      hbuf[k & 1], hstride, tone_k6 ? (double *)c->p25 : nullptr, per};
+                      hbuf[k & 1], hstride, (double *)c->p25, per};
       hipEvent_t e1 = prof_event(c);
-      if (seg(c)) HIP_TRY(c, afs::launch_seg_synth(afs::SegArgs{a, c->dev_seg}, c->stream));
-      else HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
-      prof_pair(c, e1, prof_event(c), 0);
-      if (!seg(c) && !afs::tree_output_in_kernel())  // K6: the output stage of the launch's samples
-        HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B,
-                                           tone_k6 ? (const double *)c->p25 : nullptr, per,
-                                           c->cfg.options.radiation_from_skin, c->stream));
+      HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
+      hipEvent_t e2 = prof_event(c);
+      prof_pair(c, e1, e2, 0);
+      // K6: the glottal-tone filter and the output stage of the launch's samples
+      HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B,
+                                         (const double *)c->p25, per, c->cfg.options.radiation_from_skin, c->stream));
+      prof_pair(c, e2, prof_event(c), 2);
       if (ov) HIP_TRY(c, hipEventRecord(c->ev_free[k & 1], c->stream));
     }
     return AFS_OK;
@@ -206,19 +200,15 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
 
 // bytes of the state buffers for B utterances
 size_t ws_bytes_for(const afs_ctx *c, int64_t bp) {
-  if (seg(c)) return (size_t)bp * afs::seg_lds_doubles() * sizeof(double);
   if (tree(c)) return (size_t)bp * afs::tree_lds_doubles() * sizeof(double);
   return (size_t)(afs::lane_ws_rows(c->host_tab) * bp) * sizeof(double);
 }
 size_t lanes_bytes_for(const afs_ctx *c, int64_t bp) {
-  if (seg(c)) return (size_t)bp * afs::seg::SW * afs::seg_lane_bytes();
   return tree(c) ? (size_t)bp * afs::TREE_W * afs::tree_lane_bytes() : 0;
 }
 
 afs_status reset_state(afs_ctx *c, void *ws, int32_t *rng, void *lanes, int64_t bp, int B, const uint32_t *seeds_dev) {
-  if (seg(c))
-    HIP_TRY(c, afs::launch_seg_reset(lanes, (double *)ws, B, seeds_dev, c->stream));
-  else if (tree(c))
+  if (tree(c))
     HIP_TRY(c, afs::launch_tree_reset(lanes, (double *)ws, B, seeds_dev, c->stream));
   else
     HIP_TRY(c, afs::launch_lane_reset((double *)ws, rng, bp, B, seeds_dev, c->stream));
@@ -240,9 +230,7 @@ afs_status nonfinite_report(afs_ctx *c, void *ws, int64_t bp, int B, uint8_t *fl
     *host_sync = true;
   }
   HIP_TRY(c, hipMemsetAsync(c->dcount, 0, sizeof(int32_t), c->stream));
-  if (seg(c))
-    HIP_TRY(c, afs::launch_seg_nonfinite((const double *)ws, B, c->dcount, dflags, c->stream));
-  else if (tree(c))
+  if (tree(c))
     HIP_TRY(c, afs::launch_tree_nonfinite((const double *)ws, B, c->dcount, dflags, c->stream));
   else
     HIP_TRY(c, afs::launch_lane_nonfinite((const double *)ws, bp, B, c->dcount, dflags, c->stream));
@@ -252,15 +240,14 @@ afs_status nonfinite_report(afs_ctx *c, void *ws, int64_t bp, int B, uint8_t *fl
 }
 
 afs_status draws_of(afs_ctx *c, const void *ws, int B, int64_t *draws) {
-  if (!tree(c)) return fail(c, AFS_ERR_UNSUPPORTED, "rand() call counts are kept by the tree and seg solvers only");
+  if (!tree(c)) return fail(c, AFS_ERR_UNSUPPORTED, "rand() call counts are kept by the tree solver only");
   int64_t *d = draws;
   void *tmp = nullptr;
   if (!is_device_ptr(draws)) {
     HIP_TRY(c, hipMalloc(&tmp, (size_t)B * sizeof(int64_t)));
     d = (int64_t *)tmp;
   }
-  hipError_t e = seg(c) ? afs::launch_seg_draws((const double *)ws, B, d, c->stream)
-                        : afs::launch_tree_draws((const double *)ws, B, d, c->stream);
+  hipError_t e = afs::launch_tree_draws((const double *)ws, B, d, c->stream);
   if (e == hipSuccess && tmp) e = hipMemcpyAsync(draws, d, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (tmp) (void)hipFree(tmp);
@@ -279,7 +266,7 @@ void afs_config_default(afs_config *cfg) {
   std::memset(cfg, 0, sizeof *cfg);
   cfg->sampling_rate_hz = 22050.0;
   cfg->precision = AFS_FP64;
-  cfg->solver = AFS_SOLVER_TREE;  // (the fastest measured: DESIGN.md 4, K1 and the seg kernel)
+  cfg->solver = AFS_SOLVER_TREE;  // (the fastest kernel: DESIGN.md 4)
   cfg->device = 0;
   cfg->flags = 0;
   cfg->options = afs::default_options();
@@ -320,15 +307,6 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   if (hipMalloc((void **)&ctx->dev_tab, sizeof(afs::Tables)) != hipSuccess) return bail(AFS_ERR_OUT_OF_MEMORY);
   if (hipMemcpy(ctx->dev_tab, &ctx->host_tab, sizeof(afs::Tables), hipMemcpyHostToDevice) != hipSuccess)
     return bail(AFS_ERR_HIP);
-  if (c.solver == AFS_SOLVER_SEG) {
-    std::vector<char> buf(sizeof(afs::seg::SegTables));
-    auto *st = reinterpret_cast<afs::seg::SegTables *>(buf.data());
-    afs::seg::build_seg_tables(ctx->host_tab, st);
-    if (!st->ok) return bail(AFS_ERR_UNSUPPORTED);
-    if (hipMalloc((void **)&ctx->dev_seg, sizeof(afs::seg::SegTables)) != hipSuccess) return bail(AFS_ERR_OUT_OF_MEMORY);
-    if (hipMemcpy(ctx->dev_seg, st, sizeof(afs::seg::SegTables), hipMemcpyHostToDevice) != hipSuccess)
-      return bail(AFS_ERR_HIP);
-  }
   if (hipMalloc((void **)&ctx->dcount, sizeof(int32_t)) != hipSuccess) return bail(AFS_ERR_OUT_OF_MEMORY);
   if (hipHostMalloc((void **)&ctx->hcount, sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
     return bail(AFS_ERR_OUT_OF_MEMORY);
@@ -355,7 +333,6 @@ void afs_destroy(afs_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
   if (c->dev_tab) (void)hipFree(c->dev_tab);
-  if (c->dev_seg) (void)hipFree(c->dev_seg);
   if (c->ws) (void)hipFree(c->ws);
   if (c->rng) (void)hipFree(c->rng);
   if (c->tree_lanes) (void)hipFree(c->tree_lanes);
@@ -471,30 +448,42 @@ afs_status afs_synthesize(afs_ctx *c, const afs_frame *frames, const uint32_t *s
   return synth_core(c, frames, seeds, B, F, hop, out, nonfinite, rep, false);
 }
 
-afs_status afs_kernel_times(afs_ctx *c, double *synth_ms, int32_t *synth_launches, double *plan_ms,
-                            int32_t *plan_launches) {
-  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+afs_status afs_kernel_times_ex(afs_ctx *c, afs_kernel_timing *t) {
+  if (!c || !t) return AFS_ERR_INVALID_ARGUMENT;
   if (!(c->cfg.flags & AFS_PROFILE)) return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_kernel_times: AFS_PROFILE is off");
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  double ms[2] = {0.0, 0.0};
-  int32_t n[2] = {0, 0};
-  for (const auto &t : c->timed) {
+  double ms[3] = {0.0, 0.0, 0.0};
+  int32_t n[3] = {0, 0, 0};
+  for (const auto &e : c->timed) {
     float x = 0.f;
-    HIP_TRY(c, hipEventElapsedTime(&x, t.a, t.b));
-    ms[t.kind] += x;
-    ++n[t.kind];
+    HIP_TRY(c, hipEventElapsedTime(&x, e.a, e.b));
+    ms[e.kind] += x;
+    ++n[e.kind];
   }
   const bool overflow = c->timed_overflow;
   c->timed.clear();
   c->pev_used = 0;
   c->timed_overflow = false;
-  if (synth_ms) *synth_ms = ms[0];
-  if (synth_launches) *synth_launches = n[0];
-  if (plan_ms) *plan_ms = ms[1];
-  if (plan_launches) *plan_launches = n[1];
+  t->synth_ms = ms[0];
+  t->synth_launches = n[0];
+  t->plan_ms = ms[1];
+  t->plan_launches = n[1];
+  t->output_ms = ms[2];
+  t->output_launches = n[2];
   if (overflow) return fail(c, AFS_ERR_UNSUPPORTED, "afs_kernel_times: more launches than the event pool holds");
   return AFS_OK;
+}
+
+afs_status afs_kernel_times(afs_ctx *c, double *synth_ms, int32_t *synth_launches, double *plan_ms,
+                            int32_t *plan_launches) {
+  afs_kernel_timing t{};
+  const afs_status s = afs_kernel_times_ex(c, &t);
+  if (synth_ms) *synth_ms = t.synth_ms;
+  if (synth_launches) *synth_launches = t.synth_launches;
+  if (plan_ms) *plan_ms = t.plan_ms;
+  if (plan_launches) *plan_launches = t.plan_launches;
+  return s;
 }
 
 afs_status afs_rng_draws(afs_ctx *c, int32_t B, int64_t *draws) {
@@ -509,7 +498,7 @@ afs_status afs_noise_plans(afs_ctx *c, const afs_frame *frames, int32_t rows, in
                            int64_t s1, uint64_t *plans) {
   static_assert(AFS_PLAN_WORDS * 8 == afs::PLAN_RECORD_BYTES, "afs.h / tree_plan.h record size");
   if (!c) return AFS_ERR_INVALID_ARGUMENT;
-  if (!tree(c)) return fail(c, AFS_ERR_UNSUPPORTED, "afs_noise_plans: tree / seg solvers only");
+  if (!tree(c)) return fail(c, AFS_ERR_UNSUPPORTED, "afs_noise_plans: tree solver only");
   if (!frames || !plans || rows <= 0 || F < 2 || hop < 1 || s0 < 0 || s1 <= s0 || s1 > (int64_t)(F - 1) * hop)
     return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_noise_plans: need frames, plans, rows>0, num_frames>=2, hop>=1, "
                                              "0 <= s_begin < s_end <= (num_frames-1)*hop");
@@ -532,7 +521,7 @@ afs_status afs_noise_plans(afs_ctx *c, const afs_frame *frames, int32_t rows, in
   }
   afs::PlanArgs pa{c->dev_tab, dframes, F, rows, hop, s0, s1, dplans, n,
                    c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0,
-                   seg(c) ? c->dev_seg->uo : c->dev_tab->consts.sec};
+                   c->dev_tab->consts.sec};
   HIP_TRY(c, afs::launch_plan(pa, c->stream));
   if (host_out) HIP_TRY(c, hipMemcpyAsync(plans, dplans, bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -582,6 +571,27 @@ afs_status afs_noise_plan_hops(afs_ctx *c, const afs_frame *frames, int32_t rows
   if (host_plans) HIP_TRY(c, hipMemcpyAsync(plans, dplans, pbytes, hipMemcpyDeviceToHost, c->stream));
   if (host_hops) HIP_TRY(c, hipMemcpyAsync(hops, dhops, hbytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return AFS_OK;
+}
+
+afs_status afs_plan_hop_words(afs_ctx *c, const uint8_t *hops, const double *ratio, int32_t n, uint64_t *words) {
+  if (!c) return AFS_ERR_INVALID_ARGUMENT;
+  if (c->cfg.solver != AFS_SOLVER_TREE) return fail(c, AFS_ERR_UNSUPPORTED, "afs_plan_hop_words: tree solver only");
+  if (!hops || !ratio || !words || n <= 0)
+    return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_plan_hop_words: need hops, ratio, words, n>0");
+  HIP_TRY(c, hipSetDevice(c->cfg.device));
+  const size_t hb = (size_t)n * sizeof(afs::tree::PlanHop), rb = (size_t)n * 8, wb = (size_t)n * AFS_PLAN_WORDS * 8;
+  char *d = nullptr;
+  HIP_TRY(c, hipMalloc((void **)&d, hb + rb + wb));
+  hipError_t e = hipMemcpyAsync(d, hops, hb, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d + hb, ratio, rb, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess)
+    e = afs::launch_tree_hop_words((const afs::tree::PlanHop *)d, (const double *)(d + hb), n, (uint64_t *)(d + hb + rb),
+                                   c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(words, d + hb + rb, wb, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d);
+  HIP_TRY(c, e);
   return AFS_OK;
 }
 

@@ -27,6 +27,13 @@ struct afs_comm {
   hipEvent_t ready = nullptr, done = nullptr;
   bool pending = false;      // a gather was queued since the last fence
   bool aborted = false;      // the communicator was aborted after a failed group (comm_abort)
+  // a timing event pair on the comm stream around every gather (afs_comm_gather_times): the
+  // pool grows to the gathers in flight between two reads
+  std::vector<hipEvent_t> tev;
+  size_t tev_used = 0;
+  hipEvent_t t_open = nullptr;  // the gather being queued: its start event
+  double gather_ms = 0.0;       // summed over the gathers read so far
+  int32_t gathers = 0;
 };
 
 namespace {
@@ -110,12 +117,25 @@ afs_status comm_setup(afs_comm *m) {
 // can run every fallible HIP step before the group opens: gather_prepare makes the comm's
 // stream wait for the work queued so far on the context's stream; gather_post queues only the
 // RCCL sends / receives (and rank 0's local copy).
+// the next timing event of the pool, recorded on the comm stream
+afs_status timing_event(afs_comm *m, hipEvent_t *out) {
+  afs_ctx *c = m->ctx;
+  if (m->tev_used == m->tev.size()) {
+    hipEvent_t e = nullptr;
+    HIP_TRY(c, hipEventCreate(&e));
+    m->tev.push_back(e);
+  }
+  *out = m->tev[m->tev_used++];
+  HIP_TRY(c, hipEventRecord(*out, m->cs));
+  return AFS_OK;
+}
+
 afs_status gather_prepare(afs_comm *m) {
   afs_ctx *c = m->ctx;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   HIP_TRY(c, hipEventRecord(m->ready, c->stream));
   HIP_TRY(c, hipStreamWaitEvent(m->cs, m->ready, 0));
-  return AFS_OK;
+  return timing_event(m, &m->t_open);  // (after the wait: the gather's own time, not its queueing)
 }
 
 afs_status gather_post(afs_comm *m, const int16_t *local, int64_t count, int16_t *root_out,
@@ -160,8 +180,25 @@ void comm_abort(afs_comm *m) {
 afs_status gather_finish(afs_comm *m) {
   afs_ctx *c = m->ctx;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
+  hipEvent_t t_close = nullptr;
+  afs_status s = timing_event(m, &t_close);
+  if (s != AFS_OK) return s;
+  (void)t_close;  // (pairs are read in order: tev[2i], tev[2i + 1])
   HIP_TRY(c, hipEventRecord(m->done, m->cs));
   m->pending = true;
+  return AFS_OK;
+}
+
+// Sum the finished gathers' event pairs into gather_ms (the comm stream has drained).
+afs_status read_gather_times(afs_comm *m) {
+  afs_ctx *c = m->ctx;
+  for (size_t i = 0; i + 1 < m->tev_used; i += 2) {
+    float x = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&x, m->tev[i], m->tev[i + 1]));
+    m->gather_ms += x;
+    ++m->gathers;
+  }
+  m->tev_used = 0;
   return AFS_OK;
 }
 
@@ -245,6 +282,7 @@ void afs_comm_destroy(afs_comm *m) {
   (void)hipSetDevice(m->ctx->cfg.device);
   if (m->cs && !m->aborted) (void)hipStreamSynchronize(m->cs);
   if (m->nc) (void)rccl().CommDestroy(m->nc);
+  for (hipEvent_t e : m->tev) (void)hipEventDestroy(e);
   if (m->ready) (void)hipEventDestroy(m->ready);
   if (m->done) (void)hipEventDestroy(m->done);
   if (m->cs) (void)hipStreamDestroy(m->cs);
@@ -267,6 +305,8 @@ afs_status afs_gather_pcm(afs_comm *m, const int16_t *local, int64_t count, int1
 
 afs_status afs_comm_fence(afs_comm *m) {
   if (!m) return AFS_ERR_INVALID_ARGUMENT;
+  // (an aborted communicator's stream may never drain: do not make the context's stream wait on it)
+  if (m->aborted) return afs::fail(m->ctx, AFS_ERR_HIP, "afs_comm_fence: the communicator was aborted");
   if (!m->pending) return AFS_OK;
   afs_ctx *c = m->ctx;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
@@ -276,10 +316,22 @@ afs_status afs_comm_fence(afs_comm *m) {
 
 afs_status afs_comm_synchronize(afs_comm *m) {
   if (!m) return AFS_ERR_INVALID_ARGUMENT;
+  if (m->aborted) return afs::fail(m->ctx, AFS_ERR_HIP, "afs_comm_synchronize: the communicator was aborted");
   afs_ctx *c = m->ctx;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   HIP_TRY(c, hipStreamSynchronize(m->cs));
   m->pending = false;
+  return read_gather_times(m);
+}
+
+afs_status afs_comm_gather_times(afs_comm *m, double *ms, int32_t *count) {
+  if (!m) return AFS_ERR_INVALID_ARGUMENT;
+  afs_status s = afs_comm_synchronize(m);
+  if (s != AFS_OK) return s;
+  if (ms) *ms = m->gather_ms;
+  if (count) *count = m->gathers;
+  m->gather_ms = 0.0;
+  m->gathers = 0;
   return AFS_OK;
 }
 

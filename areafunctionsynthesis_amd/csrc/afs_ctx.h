@@ -9,21 +9,19 @@
 #include <hip/hip_runtime.h>
 
 #include "afs_model.h"
-#include "seg_model.h"
 
 struct afs_ctx {
   afs_config cfg{};
   hipStream_t stream = nullptr;
   afs::Tables host_tab{};
   afs::Tables *dev_tab = nullptr;
-  afs::seg::SegTables *dev_seg = nullptr;  // AFS_SOLVER_SEG: the lane records (device copy)
   std::string err;
   // reusable device buffers for whole-trajectory calls
   void *ws = nullptr;
   size_t ws_bytes = 0;
   int32_t *rng = nullptr;
   size_t rng_bytes = 0;
-  void *tree_lanes = nullptr;  // tree / seg solver: per-lane register state
+  void *tree_lanes = nullptr;  // tree solver: per-lane register state
   size_t tree_lanes_bytes = 0;
   void *stage_in = nullptr;
   size_t stage_in_bytes = 0;
@@ -59,7 +57,8 @@ struct afs_ctx {
   int32_t *hcount = nullptr;  // pinned host copy of dcount
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // AFS_PROFILE: an event pair around every kernel launch of the synthesis calls
-  struct Timed { hipEvent_t a, b; int kind; };  // kind 0: synthesis kernel, 1: noise-source plan (K5)
+  struct Timed { hipEvent_t a, b; int kind; };  // kind 0: synthesis kernel (K1), 1: noise-source plan (K5),
+                                                // 2: output stage (K6)
   std::vector<hipEvent_t> pev;  // pool
   size_t pev_used = 0;
   std::vector<Timed> timed;
@@ -72,7 +71,7 @@ struct afs_session {
   int64_t bp = 0;
   void *ws = nullptr;          // lane solver: SoA workspace; tree solver: per-utterance LDS blocks
   int32_t *rng = nullptr;      // lane solver: generator state; tree solver: unused
-  void *tree_lanes = nullptr;  // tree / seg solver: per-lane register state
+  void *tree_lanes = nullptr;  // tree solver: per-lane register state
   afs_frame *pair = nullptr;   // [B][2]: previous frame, new frame
   uint32_t *seeds = nullptr;   // device copy
   bool latched = false;

@@ -30,8 +30,7 @@ struct TreeArgs {
   // samples of mixed hops only
   const tree::PlanHop *hops = nullptr;
   int64_t hop_stride = 0;
-  // section 25's pressure per sample (p25[u * p25_stride + s - s_begin]), K6's glottal-tone
-  // input, unless the kernel filters the tone itself (tree_tone_in_kernel())
+  // section 25's pressure per sample (p25[u * p25_stride + s - s_begin]), K6's glottal-tone input
   double *p25 = nullptr;
   int64_t p25_stride = 0;
 };
@@ -46,7 +45,7 @@ struct PlanArgs {
   int64_t plan_stride;
   int two_mass;
   const SecRec *uo;         // the synthesis kernel's LDS offsets of the section outputs' noise-
-                            // smoothed flows (tree: tab->consts.sec; seg: SegTables::uo)
+                            // smoothed flows (tab->consts.sec)
   tree::PlanHop *hops = nullptr;  // hop mode (launch_plan_hops): as TreeArgs::hops
   int64_t hop_stride = 0;
   uint32_t *work = nullptr;  // hop mode: a counter and rows * hop slots entries (the hops decided
@@ -73,18 +72,18 @@ int64_t tree_lane_bytes();
 int64_t tree_lds_doubles();
 hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const uint32_t *seeds, hipStream_t st);
 hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st);
-// K6, after each tree_synth launch of samples [s_begin, s_end): the output stage over the flows
-// it stored (out[u * out_stride + s - s_begin], replaced by the audio).  Not needed when the
-// synthesis kernel was built to filter itself (tree_output_in_kernel(): the A/B variant).
+// K6, after each tree_synth launch of samples [s_begin, s_end): the glottal-tone filter over the
+// section-25 pressures (p25, skin != 0) and the output stage over the flows the launch stored
+// (out[u * out_stride + s - s_begin], replaced by the audio).
 hipError_t launch_tree_output(const Tables *tab, double *lds_state, double *out, int64_t out_stride, int64_t n, int B,
                               const double *p25, int64_t p25_stride, int skin, hipStream_t st);
-bool tree_output_in_kernel();
-bool tree_tone_in_kernel();
 hipError_t launch_tree_nonfinite(const double *lds_state, int B, int32_t *count, uint8_t *flags, hipStream_t st);
 hipError_t launch_tree_draws(const double *lds_state, int B, int64_t *draws, hipStream_t st);
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st);
 // K5 in hop mode: the hop records of the launch's hops, the dense records of its mixed hops
 hipError_t launch_plan_hops(const PlanArgs &a, hipStream_t st);
+// diagnostics: the tree kernel's per-sample plan words from hop records (afs_plan_hop_words)
+hipError_t launch_tree_hop_words(const tree::PlanHop *h, const double *ratio, int n, uint64_t *out, hipStream_t st);
 // diagnostics: the tree kernel's tube interpolation (afs_tube_interpolate)
 hipError_t launch_tree_interp(const Tables *tab, const afs_frame *fl, const afs_frame *fr, const double *ratio, int n,
                               double *area, double *len, hipStream_t st);

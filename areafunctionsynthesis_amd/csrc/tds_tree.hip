@@ -19,11 +19,10 @@ __global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_synth_kerne
 
 // K6: the output stage of a launch's samples -- dU/dt, the 8-pole Chebyshev low-pass, x 0.004 /
 // 32767 (Synthesizer.cpp:614-627) -- over the radiated flows the synthesis kernel stored, in
-// place, one thread per utterance; the filter state (X_OUTF, X_PREVFLOW, X_NONFIN) lives in the
-// utterance's saved LDS image, which the synthesis kernel carries through unchanged.
-// With p25 (the synthesis kernel built without the tone filter): first the glottal-tone filter
-// (skin radiation) over section 25's stored pressures, added to the flows, in the output filter's
-// loop (tone_output_run).
+// place, one thread per utterance; the filter state (X_OUTF, X_PREVFLOW, X_NONFIN, X_TONE) lives in
+// the utterance's saved LDS image, which the synthesis kernel carries through unchanged.  With skin
+// radiation (TdsModel::Options.radiationFromSkin): first the glottal-tone filter over section 25's
+// stored pressures, added to the flows, in the output filter's loop (tone_output_run).
 __global__ void __launch_bounds__(64) tree_output_kernel(const Tables *tab, double *lds_state, double *out,
                                                          int64_t out_stride, int64_t n, int B, const double *p25,
                                                          int64_t p25_stride, int skin) {
@@ -85,7 +84,23 @@ __global__ void tree_interp_kernel(const Tables *tab, const afs_frame *fl, const
   }
 }
 
+// Diagnostics (afs_plan_hop_words): the synthesis kernel's per-sample plan words, plan_word_fast
+// compiled here with its flags, for n (hop record, ratio) pairs: thread (i, w) writes word w.
+__global__ void tree_hop_words_kernel(const tree::PlanHop *h, const double *ratio, int n, uint64_t *out) {
+  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (int64_t)n * PLAN_WORDS) return;
+  const int i = (int)(id / PLAN_WORDS), w = (int)(id % PLAN_WORDS);
+  out[id] = plan_word_fast(h[i].kind[w], h[i].p[w], ratio[i]);
+}
+
 }  // namespace
+
+hipError_t launch_tree_hop_words(const tree::PlanHop *h, const double *ratio, int n, uint64_t *out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t t = (int64_t)n * PLAN_WORDS;
+  hipLaunchKernelGGL(tree_hop_words_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, h, ratio, n, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_tree_interp(const Tables *tab, const afs_frame *fl, const afs_frame *fr, const double *ratio, int n,
                               double *area, double *len, hipStream_t st) {
@@ -95,16 +110,6 @@ hipError_t launch_tree_interp(const Tables *tab, const afs_frame *fl, const afs_
                      area, len);
   return hipGetLastError();
 }
-
-bool tree_output_in_kernel() {
-#if defined(AFS_K1_FILTER)
-  return true;
-#else
-  return false;
-#endif
-}
-
-bool tree_tone_in_kernel() { return !GpuExec<false>::kToneOut; }
 
 hipError_t launch_tree_output(const Tables *tab, double *lds_state, double *out, int64_t out_stride, int64_t n, int B,
                               const double *p25, int64_t p25_stride, int skin, hipStream_t st) {

@@ -154,16 +154,10 @@ struct D4 { double v[4]; };
 // dropping it measured +2.3 % end to end (profiles/r03s_rcp_rows_ab.txt) with the parity
 // figures still 5-6 orders inside the bounds and 0 rand() count differences.
 // Plain division in the CPU emulator.
-#ifndef AFS_RCP_NEWTON
-#define AFS_RCP_NEWTON 1
-#endif
 AFS_HD inline double pivot_recip(double d) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  double r = __builtin_amdgcn_rcp(d);
-  double e = fma(-d, r, 1.0);
-  r = fma(r, e, r);
-  if constexpr (AFS_RCP_NEWTON == 1) return r;
-  e = fma(-d, r, 1.0);
+  const double r = __builtin_amdgcn_rcp(d);
+  const double e = fma(-d, r, 1.0);
   return fma(r, e, r);
 #else
   return 1.0 / d;
@@ -192,8 +186,10 @@ AFS_HD inline double fast_sqrt(double x) {
 }
 
 // Reciprocal and quotient of positive, normal operands (areas, surfaces, capacitances) without
-// the scaling/fixup steps of IEEE division: v_rcp_f64 + two Newton steps, and for the quotient
-// one residual correction (within 1 ulp of a / b).  Host builds (the CPU emulator) divide.
+// the scaling/fixup steps of IEEE division: v_rcp_f64 + one Newton step (pivot_recip: within 11
+// ulps of 1 / b), and for the quotient one residual correction (within 1 ulp of a / b for the
+// operands here, measured on 3 M inputs by tools/microbench/f64_ops.hip).  Host builds (the CPU
+// emulator) divide.
 AFS_HD inline double fast_rcp(double d) { return pivot_recip(d); }
 AFS_HD inline double fast_div(double a, double b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -207,8 +203,12 @@ AFS_HD inline double fast_div(double a, double b) {
 
 // Word `kind` of a hop record at `ratio` (tree_plan.h plan_word_eval), branch-free on the
 // device: every lane evaluates one square root and one quotient and keeps its kind's value.
-// The interpolation is K5's and phase_interpolate's (uncontracted); the square roots are exact
-// (fast_sqrt), the quotients within an ulp of K5's divisions (fast_div).
+// The interpolation is K5's and phase_interpolate's (uncontracted), so the area A is bit-identical.
+// The words are NOT bit-identical with K5's dense records: PK_SQRT (sqrt A) is exact (fast_sqrt);
+// PK_INVA (1 / A), PK_INVD (1 / sqrt(4 A / pi), here sqrt((4 A) * (1 / pi)): one rounding more)
+// and PK_FDN (N / D) come from fast_div (v_rcp_f64, one Newton step, one residual correction)
+// instead of IEEE divisions.  tests/test_plan_gpu.py::test_hop_words_vs_dense_records measures the
+// device words against the dense records (within a few ulps, 1e-15 relative).
 AFS_HD inline uint64_t plan_word_fast(uint32_t kind, const double *p, double ratio) {
 #if defined(__HIP_DEVICE_COMPILE__)
   double x, y;
@@ -248,7 +248,7 @@ struct Lane {
   double aL[S::ND], aR[S::ND], lL[S::ND], lR[S::ND];                 // frame cache
   double al[S::ND], be[S::ND];                                        // dynamic wall terms
   double damp[S::NDP], dout[S::NDP], dcut[S::NDP];                   // dipoles gl + k W
-  double rad_u[2], rad_ur[2], rad_un[2];                             // owner of 64 / 83
+  double rad_u[2];                                                    // owner of 64 / 83: radiation currents' old u
   double sample;                                                     // lane 0
   uint64_t planw;                                                    // word gl of this sample's plan (tree_plan.h)
   uint32_t racc[S::NDP];                                             // rand() sums of owned dipoles
@@ -502,7 +502,7 @@ AFS_HD inline void reset_lane(int gl, Lane<W> &R) {
   R.planw = 0;
 #pragma unroll
   for (int k = 0; k < S::NDP; ++k) { R.damp[k] = 0.0; R.dout[k] = 0.0; R.dcut[k] = 3000.0; }
-  for (int k = 0; k < 2; ++k) R.rad_u[k] = R.rad_ur[k] = R.rad_un[k] = 0.0;
+  for (int k = 0; k < 2; ++k) R.rad_u[k] = 0.0;
   R.sample = 0.0;
 #pragma unroll
   for (int k = 0; k < S::NDP; ++k) R.racc[k] = 0u;
@@ -658,12 +658,6 @@ AFS_HD inline GlotRes glottis_eval(const GlotIn &in, const CT &C, double ratio, 
     gp[5] = GLOTTIS_DEFAULT_ASPIRATION_DB;  // X_GP + 5 is read as the aspiration strength
     return res;
   } else {
-#if defined(AFS_EXP_NO_GLOTTIS)  // timing experiment only (tools/phase_prof): no glottis work
-    (void)r1;
-    res.go = GlotOut{0.1 + 1e-3 * ratio, 0.1, 0.3, 0.3};
-    for (int k = 0; k < 4; ++k) res.rel[k] = in.rel[k];
-    return res;
-#endif
     const double rel0 = in.rel[0], rel1 = in.rel[1];
     // calcGeometry + getTubeData + Tube::setGlottisGeometry (TriangularGlottis.cpp:338-411)
     // (divisions sharing a denominator use one reciprocal; sqrt(m k) is a constant since
@@ -711,7 +705,7 @@ AFS_HD inline GlotRes glottis_eval(const GlotIn &in, const CT &C, double ratio, 
 }
 
 // The triangular glottis with its two masses on the two halves of an utterance's 16 lanes
-// (device; AFS_GLOTTIS_UNIFORM keeps glottis_eval): every lane evaluates the shared terms, lanes
+// (device; the CPU emulator runs glottis_eval): every lane evaluates the shared terms, lanes
 // 0-7 mass 0 and lanes 8-15 mass 1 with the operations glottis_eval applies to that mass (its
 // constants from the tables' gmass row), and each mass's area, A and E terms reach the other
 // half by a row rotation by 8 (xch): ~140 fewer instructions per sample, +1.1 % (A/B,
@@ -847,12 +841,6 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     const double len = glot ? (s == S_GLOT_LO ? go.l0 : go.l1) : R.lcur[j];
     // prepareTimeStep's section quantities (TdsModel.cpp:732-834), with the repeated
     // divisions folded into one reciprocal of the area and one of the wall surface.
-#if defined(AFS_EXP_NO_NETGEO)  // timing experiment only (tools/phase_prof): no geometric chains
-    const double inv_area = area, r0 = area * 0.5641895835, Rr = len * 1e-3, L = len * area, alw = 1e-3 * area,
-                 E = 1e-3 * len, c1 = 1e-3, c2 = 2e-3, c3 = 3e-3, ia2 = inv_area * inv_area;
-    const double bew = alw * (R.w[j] * c1 + R.wr[j] * c2 + R.wr2[j] * c3);
-    (void)idt; (void)idt2;
-#else
     // (the divisions rewritten around one reciprocal of the area: the Poiseuille resistance of
     // the circular and the elliptic section (:741-760) as polynomials in 1/A, the wall terms with
     // the wall surface cancelled (alpha = surf / K, beta = k1 w + k2 w' + k3 w''); the decisions
@@ -875,12 +863,6 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     const double beta = walls ? fma(R.w[j], C.h.wall_k1, fma(R.wr[j], C.h.wall_k2, R.wr2[j] * C.h.wall_k3)) : 0.0;
     const double E = fast_div(dt * TH, Cc + alpha);
     (void)idt; (void)idt2;
-#endif
-#if defined(AFS_EXP_NO_NETGEO)
-    const bool walls = opt.soft_walls && !glot;
-    const double alpha = walls ? alw : 0.0, beta = walls ? bew : 0.0;
-    (void)dt;
-#endif
     double R0 = Rr, R1 = Rr;
     // Bernoulli losses between pharynx/mouth sections (TdsModel.cpp:850-877)
     const bool turb = opt.turbulence_losses && pm;
@@ -1322,10 +1304,6 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     const int rc = q.x_rad[0] / 8 - X_U, lc = q.x_rad[1] / 8 - X_U;
     double uR = xat(X, q.x_rad[0]), uL = xat(X, q.x_rad[1]), uRr = xat(X, q.x_rad[2]), uLr = xat(X, q.x_rad[3]);
     R.rad_u[0] = uR; R.rad_u[1] = uL;
-#if defined(AFS_RAD_REG)  // (A/B variant: the old d/dt and smoothed flows kept in registers too)
-    R.rad_ur[0] = uRr; R.rad_ur[1] = uLr;
-    R.rad_un[0] = xat(X, q.x_rad[4]); R.rad_un[1] = xat(X, q.x_rad[5]);
-#endif
     const double LA2 = LB, RA2 = R1B, Sr = -X[X_SMP + DIP_LIPS];
     {
       const double Rrad = dyn ? X[X_RRAD] : C.h.rrad_nose;  // (network phase / tables)
@@ -1684,13 +1662,10 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
       const SecRec &q = rec[j];
       for (int k = 0; k < 2; ++k) {
         double un = xat(X, q.x_rad[k]);
-#if defined(AFS_RAD_REG)
-        const double our = R.rad_ur[k], oun = R.rad_un[k];
-#else
         // (the previous sample's d/dt and smoothed flow are still in their LDS slots: read before
-        // this update overwrites them, instead of carrying them in registers through the solver)
+        // this update overwrites them, instead of carrying them in registers through the solver:
+        // +0.2 %, profiles/r03ab_ab.txt)
         const double our = xat(Xw, q.x_rad[2 + k]), oun = xat(Xw, q.x_rad[4 + k]);
-#endif
         double ur = (un - R.rad_u[k]) * idt - (TH1 / TH) * our;
         xat(Xw, q.x_rad[2 + k]) = ur;
         xat(Xw, q.x_rad[4 + k]) = (1.0 - c) * un + c * oun;

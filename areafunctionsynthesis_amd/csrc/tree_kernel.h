@@ -23,12 +23,8 @@ namespace tree {
 // A DPP lane move whose every lane's source is inside its row (the permutations, rotations and
 // broadcasts used here), or whose out-of-row lanes read 0 (bound_ctrl): the destination's old
 // value is never kept, so the move carries none (update_dpp(0, ...) zeroed it first: ~90 moves
-// per sample).  AFS_DPP_OLD0 restores that form (A/B).
-#if defined(AFS_DPP_OLD0)
-#define AFS_DPP(src, ctrl, rmask, bmask, bc) __builtin_amdgcn_update_dpp(0, (src), (ctrl), (rmask), (bmask), (bc))
-#else
+// per sample, +0.3 % without them, profiles/r03z_ab.txt).
 #define AFS_DPP(src, ctrl, rmask, bmask, bc) __builtin_amdgcn_mov_dpp((src), (ctrl), (rmask), (bmask), (bc))
-#endif
 
 constexpr int TW = TREE_W;
 constexpr int UPW = 64 / TW;          // utterances per wave
@@ -38,16 +34,8 @@ static_assert(TW == 16 || TW == 32, "collectives are written for 16 or 32 lanes 
 
 template <bool PROF>
 struct GpuExec {
-#if defined(AFS_TONE_IN_KERNEL) || defined(AFS_K1_FILTER)  // (A/B variant: the glottal-tone filter in the step)
-  static constexpr bool kToneOut = false;
-#else
-  static constexpr bool kToneOut = true;        // the tone filter in K6 from the stored p[25]
-#endif
-#if defined(AFS_GLOTTIS_UNIFORM)  // (A/B variant: every lane evaluates both glottis masses)
-  static constexpr bool kGlottisSplit = false;
-#else
-  static constexpr bool kGlottisSplit = true;   // the glottis' masses on the two lane halves
-#endif
+  static constexpr bool kToneOut = true;        // the tone filter in K6 from the stored p[25] (+0.5 %, r03ai_ab.txt)
+  static constexpr bool kGlottisSplit = true;   // the glottis' masses on the two lane halves (+1.1 %, r03ag_ab.txt)
   int gl;
   Lane<TW> *R;
   uint64_t last = 0;
@@ -222,23 +210,16 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   const int64_t row = a.frame_row ? a.frame_row[ue] : ue;
   const afs_frame *fu = a.frames + row * a.frame_stride;
   double *o = a.out + (int64_t)ue * a.out_stride;
-  double *p25o = a.p25 ? a.p25 + (int64_t)ue * a.p25_stride : nullptr;
+  double *p25o = a.p25 + (int64_t)ue * a.p25_stride;
   // this utterance's plan records, word gl % 16 of each (tree_plan.h)
   const uint64_t *pl = a.plan + row * a.plan_stride * PLAN_WORDS + (gl & (PLAN_WORDS - 1));
   const int hop = a.hop;
   const int64_t n = a.s_end - a.s_begin;
   int k = (int)(a.s_begin / hop) + 1, i = (int)(a.s_begin % hop);
-#if defined(AFS_K1_FILTER)
-  // (A/B variant, the round-2/3 kernel: the output filter in the synthesis kernel -- long hops:
-  // over each hop's flows once the hop is done, lane 0 re-reading the flows it stored; short
-  // hops: inside the sample step)
-  const bool defer = hop >= OUT_DEFER_MIN_HOP;
-#else
-  // The output stage (dU/dt, Chebyshev low-pass, scaling) does not feed back into the tube:
-  // the kernel stores the radiated flows and K6 (tree_output_kernel) filters them after the
-  // launch, so none of the filter's state or code is in this kernel's registers.
-  constexpr bool defer = true;
-#endif
+  // The output stage (dU/dt, Chebyshev low-pass, scaling) and the glottal-tone filter do not feed
+  // back into the tube: the kernel stores the radiated flows and section 25's pressures, and K6
+  // (tree_output_kernel) filters them after the launch, so none of the filters' state or code is
+  // in this kernel's registers.
   frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
   // hop mode: this hop's record (word gl % 16: its kind and inputs; whether the hop is mixed)
   const PlanHop *hr = HOPS ? a.hops + row * a.hop_stride : nullptr;
@@ -260,7 +241,6 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   NextFrame<TW> nf{};
   ex.sync();
   uint64_t next = hmixed ? pl[0] : 0;
-  int64_t t0 = 0;
   for (int64_t t = 0; t < n; ++t) {
     // (divided at the top of each step: the next sample's ratio computed at the end of the
     // previous step instead measured -2.5 %, profiles/r03ad_ab.txt)
@@ -275,42 +255,27 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
     } else {
       R.planw = next;
       next = pl[tn * PLAN_WORDS];  // the next sample's word, a sample ahead
-    }
-#if !defined(AFS_NO_FRAME_PREFETCH)
-    if constexpr (!HOPS)
       if (i + 1 == hop && t + 1 < n) nf.load(gl, fu + k + 1);
-#endif
-    sample_step<TW, MODEL>(ex, X, a.uni, C, ratio, defer);
+    }
+    sample_step<TW, MODEL>(ex, X, a.uni, C, ratio, true);
     if (valid && gl == 0) o[t] = R.sample;
     // section 25's new pressure (lane 2's slot 0), the glottal-tone filter's input in K6
-    if constexpr (GpuExec<PROF>::kToneOut)
-      if (valid && gl == 2 && p25o) p25o[t] = R.p[0];
+    if (valid && gl == 2) p25o[t] = R.p[0];
     if (++i == hop) {
-#if defined(AFS_K1_FILTER)
-      if (defer && valid && gl == 0) output_filter_run(X, C, o + t0, (int)(t + 1 - t0));
-#endif
-      t0 = t + 1;
       i = 0;
       ++k;
       if (t + 1 < n) {
-#if !defined(AFS_NO_FRAME_PREFETCH)
-        if constexpr (HOPS) frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
-        else frame_shift<TW>(gl, R, X, nf);
-#else
-        frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
-#endif
         if constexpr (HOPS) {
+          frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
           hop_load(++hr);
           if (hmixed) next = pl[(t + 1) * PLAN_WORDS];
+        } else {
+          frame_shift<TW>(gl, R, X, nf);
         }
       }
       ex.sync();
     }
   }
-#if defined(AFS_K1_FILTER)
-  if (defer && valid && gl == 0 && t0 < n) output_filter_run(X, C, o + t0, (int)(n - t0));
-#endif
-  (void)t0;
   ex.sync();
   if (valid) {
     // (the per-sample fields carry nothing to the next launch; zero them so that their

@@ -10,7 +10,7 @@ code over either.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 
 def shard_range(rank: int, world: int, per_rank: int) -> Tuple[int, int]:
@@ -105,3 +105,33 @@ class PcmGather:
 
     def drain(self):
         self.transport.drain()
+
+
+def edge_utterances(world: int, per_rank: int) -> List[Tuple[int, int, int]]:
+    """(rank, row in the rank's block, global utterance index) of the first and the last utterance
+    of every rank's block: the rows :func:`check_gathered` verifies."""
+    rows = sorted({0, per_rank - 1}) if per_rank > 0 else []
+    return [(r, j, r * per_rank + j) for r in range(world) for j in rows]
+
+
+def check_gathered(rows, world: int, per_rank: int, reference: Callable[[Sequence[int]], "object"]) -> dict:
+    """Rank 0: the gathered int16 audio against the same utterances synthesized on rank 0 alone.
+
+    ``rows[i]`` is the gathered row of the i-th entry of :func:`edge_utterances` (``[n, T]``
+    int16, any array type with ``numpy()`` or an ndarray); ``reference(us)`` synthesizes the
+    global utterances ``us`` (frames of index u, seed u + 1) in one call on rank 0 and returns their
+    int16 audio ``[len(us), T]``.  Bit-for-bit comparison: the shards' audio does not depend on
+    the GPU count, so any difference is a gather (or sharding) fault."""
+    import numpy as np
+    edges = edge_utterances(world, per_rank)
+    got = rows.numpy() if hasattr(rows, "numpy") else np.asarray(rows)
+    ref = np.asarray(reference([u for _, _, u in edges]))
+    bad = []
+    for i, (r, j, u) in enumerate(edges):
+        d = int(np.count_nonzero(got[i] != ref[i])) if got[i].shape == ref[i].shape else -1
+        if d != 0:
+            bad.append({"utterance": u, "rank": r, "row": j, "differing_samples": d})
+    return {"utterances_checked": [u for _, _, u in edges], "bitwise_equal": not bad and len(edges) > 0,
+            "mismatches": bad,
+            "method": "rank 0 re-synthesizes the first and last utterance of every rank's block alone "
+                      "(global frames and seeds u + 1) and compares the int16 rows it received bit for bit"}

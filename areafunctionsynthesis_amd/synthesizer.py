@@ -25,8 +25,7 @@ from .frames import FRAME_DTYPE
 
 _vp = ctypes.c_void_p
 
-SOLVERS = {"cholesky": _native.AFS_SOLVER_CHOLESKY, "tree": _native.AFS_SOLVER_TREE, "sor": _native.AFS_SOLVER_SOR,
-           "seg": _native.AFS_SOLVER_SEG}
+SOLVERS = {"cholesky": _native.AFS_SOLVER_CHOLESKY, "tree": _native.AFS_SOLVER_TREE, "sor": _native.AFS_SOLVER_SOR}
 
 
 def _addr(x) -> int:
@@ -136,7 +135,7 @@ class Context:
         return out
 
     def noise_plans(self, frames: np.ndarray, hop: int, s_begin: int = 0, s_end: Optional[int] = None) -> np.ndarray:
-        """Diagnostics (tree / seg solvers): the noise-source plan records K5 computes for samples
+        """Diagnostics (tree solver): the noise-source plan records K5 computes for samples
         [s_begin, s_end) of frames[rows, F] -> uint64[rows, s_end - s_begin, AFS_PLAN_WORDS]."""
         if frames.dtype != FRAME_DTYPE or frames.ndim != 2:
             raise ValueError("frames must be a 2-D FRAME_DTYPE array [rows, F]")
@@ -167,6 +166,19 @@ class Context:
         _native.check(st, self._h, "afs_noise_plan_hops")
         return hops, plans
 
+    def plan_hop_words(self, hops: np.ndarray, ratio: np.ndarray) -> np.ndarray:
+        """Diagnostics (tree solver): the plan words the synthesis kernel evaluates per sample from
+        hop records hops[n, AFS_PLAN_HOP_BYTES] (uint8) at ratio[n] -> uint64[n, AFS_PLAN_WORDS]."""
+        hops = np.ascontiguousarray(hops, dtype=np.uint8)
+        ratio = np.ascontiguousarray(ratio, dtype=np.float64)
+        n = ratio.shape[0]
+        if hops.shape != (n, _native.AFS_PLAN_HOP_BYTES):
+            raise ValueError("hops must be uint8[n, AFS_PLAN_HOP_BYTES]")
+        out = np.zeros((n, _native.AFS_PLAN_WORDS), dtype=np.uint64)
+        st = self._lib.afs_plan_hop_words(self._h, _vp(_addr(hops)), _vp(_addr(ratio)), n, _vp(_addr(out)))
+        _native.check(st, self._h, "afs_plan_hop_words")
+        return out
+
     def tube_interpolate(self, left: np.ndarray, right: np.ndarray, ratio: np.ndarray):
         """Diagnostics (tree solver): the synthesis kernel's interpolated pharynx/mouth areas and
         lengths for frames left[n], right[n] at ratio[n] -> (area[n, 40], length[n, 40])."""
@@ -184,13 +196,13 @@ class Context:
         return area, length
 
     def kernel_times(self) -> dict:
-        """(profile=True contexts) summed device time and count of the synthesis-kernel and
-        noise-source-plan launches since the previous call (waits for the stream)."""
-        sm, pm = ctypes.c_double(), ctypes.c_double()
-        sn, pn = ctypes.c_int32(), ctypes.c_int32()
-        _native.check(self._lib.afs_kernel_times(self._h, ctypes.byref(sm), ctypes.byref(sn), ctypes.byref(pm),
-                                                 ctypes.byref(pn)), self._h, "afs_kernel_times")
-        return {"synth_ms": sm.value, "synth_launches": sn.value, "plan_ms": pm.value, "plan_launches": pn.value}
+        """(profile=True contexts) summed device time and count of the synthesis-kernel (K1),
+        noise-source-plan (K5) and output-stage (K6) launches since the previous call (waits for
+        the stream)."""
+        t = _native.AfsKernelTiming()
+        _native.check(self._lib.afs_kernel_times_ex(self._h, ctypes.byref(t)), self._h, "afs_kernel_times_ex")
+        return {"synth_ms": t.synth_ms, "synth_launches": t.synth_launches, "plan_ms": t.plan_ms,
+                "plan_launches": t.plan_launches, "output_ms": t.output_ms, "output_launches": t.output_launches}
 
     def rng_draws(self, batch: int) -> np.ndarray:
         """rand() calls per utterance of the last synthesize / play_target_sequences call
@@ -313,6 +325,14 @@ class Comm:
 
     def synchronize(self) -> None:
         _native.check(self._lib.afs_comm_synchronize(self._h), self.ctx.handle, "afs_comm_synchronize")
+
+    def gather_times(self) -> dict:
+        """afs_comm_gather_times: device time and count of this rank's gathers since the last call
+        (HIP events on the comm's stream; waits for it)."""
+        ms, n = ctypes.c_double(), ctypes.c_int32()
+        _native.check(self._lib.afs_comm_gather_times(self._h, ctypes.byref(ms), ctypes.byref(n)), self.ctx.handle,
+                      "afs_comm_gather_times")
+        return {"gather_ms": ms.value, "gathers": n.value}
 
     def close(self) -> None:
         if self._h:

@@ -209,6 +209,8 @@ def measure(args, ctx, dev, stream, workload: str, B: int, first: int, world: in
     pcm.drain()
     torch.cuda.synchronize(dev)
     ctx.kernel_times()  # drop the warm-up launches
+    if comm is not None:
+        comm.gather_times()  # (and the warm-up gathers)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     if world > 1:
@@ -231,7 +233,43 @@ def measure(args, ctx, dev, stream, workload: str, B: int, first: int, world: in
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     m.elapsed = float(t.item())
+    m.multi = None
+    if world > 1:
+        # the slowest rank's kernel and gather times (HIP events; the gathers on the comm's stream)
+        gt = comm.gather_times()
+        launches = max(1, m.kt["synth_launches"])
+        mx = torch.tensor([m.kt["synth_ms"] / launches, gt["gather_ms"] / steps], dtype=torch.float64)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        m.multi = {"avg_launch_ms_max_over_ranks": float(mx[0]), "gather_ms_per_step_max_over_ranks": float(mx[1]),
+                   "gathers_per_step_rank0": gt["gathers"] / steps,
+                   "gather_timing": "HIP events on the comm's stream around each afs_gather_pcm "
+                                    "(afs_comm_gather_times); the gather overlaps the next step's synthesis"}
+        # self-check of the exchange: rank 0 compares the int16 rows it received (the last step's
+        # slot) with the same utterances synthesized on rank 0 alone
+        if rank == 0:
+            edges = sharding.edge_utterances(world, B)
+            root = pcm.result((pcm.k - 1) % len(pcm.bufs))
+            rows = torch.stack([root[r, j] for r, j, _ in edges]).cpu()
+            m.gather_check = sharding.check_gathered(rows, world, B, lambda us: _resynth(ctx, m, us, args))
+        dist.barrier()
     return m
+
+
+def _resynth(ctx, m, us, args):
+    """int16 audio [len(us), T] of global utterances `us` synthesized on this GPU in one call
+    (the frames / targets and seeds u + 1 the full batch gives them)."""
+    from areafunctionsynthesis_amd.workloads import build_frames, fricatives, static_vowels, vcv_targets
+    seeds = np.array([u + 1 for u in us], dtype=np.uint32)
+    if m.workload in ("static", "fricatives"):
+        gen = static_vowels if m.workload == "static" else fricatives
+        frames = np.concatenate([build_frames(gen(1, seconds=args.seconds, fs=args.fs, first_utterance=u),
+                                              ctx.af_to_frames) for u in us])
+        y = ctx.synthesize(frames, m.hop, seeds=seeds)
+    else:
+        shapes, _, _ = vcv_targets(1)
+        targets = np.concatenate([vcv_targets(1, first_utterance=u)[1] for u in us])
+        y = ctx.play_target_sequences(shapes, targets, seeds=seeds)
+    return ctx.to_int16(y)
 
 
 def describe(args, m: Measured, world: int, digest: str) -> dict:
@@ -239,8 +277,7 @@ def describe(args, m: Measured, world: int, digest: str) -> dict:
     B, T, hop = m.B, m.T, m.hop
     total_samples = float(world) * B * T * m.steps
     value = total_samples / m.elapsed
-    kname = {"cholesky": "lane_synth_kernel", "sor": "lane_synth_kernel", "seg": "seg_synth_kernel"}.get(
-        args.solver, "tree_synth_kernel")
+    kname = {"cholesky": "lane_synth_kernel", "sor": "lane_synth_kernel"}.get(args.solver, "tree_synth_kernel")
     launches = max(1, m.kt["synth_launches"])
     avg_launch_s = m.kt["synth_ms"] / launches / 1e3
     samples_per_launch = B * T * m.steps / launches
@@ -404,6 +441,9 @@ def main() -> None:
             "roofline": d["roofline"],
             "fp64": d["fp64"],
         }
+        if world > 1:
+            result["multi_gpu"] = m.multi
+            result["gather_check"] = m.gather_check
         if world == 1 and not args.no_cpu_baseline:
             cb, max_abs, max_rms = cpu_leg(args, m, min(args.cpu_utterances, B))
             result["cpu_baseline"] = cb

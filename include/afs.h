@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define AFS_ABI_VERSION 4
+#define AFS_ABI_VERSION 5
 #define AFS_NUM_TUBE_SECTIONS 40   /* Tube::NUM_PHARYNX_MOUTH_SECTIONS (Tube.h:56-58) */
 #define AFS_NUM_GLOTTIS_PARAMS 6   /* TriangularGlottis::NUM_CONTROL_PARAMS (TriangularGlottis.h:26-35) */
 #define AFS_NUM_AF_PARAMS 16       /* OneDimAreaFunction::NUM_AF_PARAMS (OneDimAreaFunction.h:34-43) */
@@ -68,11 +68,14 @@ typedef enum afs_status {
 
 /* Linear solver for the per-sample 97x97 SPD system. */
 typedef enum afs_solver {
-  AFS_SOLVER_CHOLESKY = 0, /* TdsModel::CHOLESKY_FACTORIZATION, same operation order (TdsModel.cpp:2231-2314) */
-  AFS_SOLVER_TREE = 1,     /* nested-dissection LDL^T on the tube tree (same system, fewer flops) */
-  AFS_SOLVER_SOR = 2,      /* TdsModel::SOR_GAUSS_SEIDEL, same sweep order (TdsModel.cpp:2105-2180) */
-  AFS_SOLVER_SEG = 3       /* the same LDL^T with lanes owning the same currents in every phase and the
-                              static subtrees condensed (the default: the fastest kernel) */
+  AFS_SOLVER_CHOLESKY = 0, /* TdsModel::CHOLESKY_FACTORIZATION, same operation order (TdsModel.cpp:2231-2314):
+                              one lane per utterance, the reference-order kernel (slow; for checks) */
+  AFS_SOLVER_TREE = 1,     /* the default and the fastest: 16 lanes per utterance, the same system solved by an
+                              LDL^T in arm order (tube tree, fewer flops), noise-source plans computed ahead */
+  AFS_SOLVER_SOR = 2       /* TdsModel::SOR_GAUSS_SEIDEL, same sweep order (TdsModel.cpp:2105-2180), one lane
+                              per utterance */
+  /* 3 was AFS_SOLVER_SEG (a segment-aligned cooperative kernel, measured 42 % slower than TREE and
+     withdrawn in ABI 5): afs_create rejects it with AFS_ERR_INVALID_ARGUMENT */
 } afs_solver;
 
 /* Glottis model driven by the synthesizer: the reference's Synthesizer uses TriangularGlottis
@@ -168,7 +171,7 @@ afs_status afs_synthesize(afs_ctx *ctx, const afs_frame *frames, const uint32_t 
  * count that differs from the reference's means a noise source switched on or off at a
  * different sample (TdsModel.cpp:1647-1666).  Tree solver only (else AFS_ERR_UNSUPPORTED). */
 afs_status afs_rng_draws(afs_ctx *ctx, int32_t batch, int64_t *draws);
-/* Diagnostics: the noise-source plan records the tree / seg solvers compute ahead of the time
+/* Diagnostics: the noise-source plan records the tree solver computes ahead of the time
  * loop (kernel K5; AFS_PLAN_WORDS u64 words per sample, layout in csrc/tree_plan.h) for samples
  * [s_begin, s_end) of frames[rows][num_frames] at this hop: plans[rows][s_end - s_begin]
  * [AFS_PLAN_WORDS] (host or device).  Everything calcNoiseSources decides from the geometry
@@ -194,6 +197,17 @@ afs_status afs_noise_plans(afs_ctx *ctx, const afs_frame *frames, int32_t rows, 
 #define AFS_PLAN_HOP_MIN 32
 afs_status afs_noise_plan_hops(afs_ctx *ctx, const afs_frame *frames, int32_t rows, int32_t num_frames, int32_t hop,
                                int64_t s_begin, int64_t s_end, uint8_t *hops, uint64_t *plans);
+/* Diagnostics: the plan words the tree solver's synthesis kernel evaluates per sample from a hop
+ * record (kernel K1's own evaluation, compiled with its flags) for n (record, ratio) pairs:
+ * hops[n][AFS_PLAN_HOP_BYTES], ratio[n] -> words[n][AFS_PLAN_WORDS] (host pointers).  Outside
+ * mixed hops, these words replace K5's dense records: the discrete words and sqrt(A) are the same
+ * bits, the quotient words (1/A, 1/sqrt(4A/pi), the downstream factors N/D) come from a reciprocal
+ * with one Newton step and a residual correction instead of an IEEE division -- within a few ulps
+ * of the dense records (tests/test_plan_gpu.py measures it) -- and the downstream factors and the
+ * glottis gain are hop-constant forms within 1e-12 / 1e-13 relative of the per-sample ones
+ * (tests/test_plan_hops.py).  AFS_PLAN_DENSE=1 in the environment makes every hop read its dense
+ * records (the per-sample plan bit for bit). */
+afs_status afs_plan_hop_words(afs_ctx *ctx, const uint8_t *hops, const double *ratio, int32_t n, uint64_t *words);
 
 /* Stateful sessions: B independent Synthesizer instances living on the device. */
 afs_status afs_session_create(afs_ctx *ctx, int32_t batch, const uint32_t *seeds, afs_session **s);
@@ -246,9 +260,20 @@ afs_status afs_play_target_sequences(afs_ctx *ctx, const double *shapes, int32_t
                                      const uint32_t *seeds, int32_t B, double *out, uint8_t *nonfinite,
                                      afs_report *report);
 
-/* AFS_PROFILE contexts: summed device time and count of the synthesis-kernel launches and of
- * the noise-source plan launches (tree solver, K5) since the previous call (waits for the
- * stream).  Any pointer may be NULL. */
+/* AFS_PROFILE contexts: summed device time and count of the synthesis-kernel launches (K1), of
+ * the noise-source plan launches (tree solver, K5) and of the output-stage launches (tree solver,
+ * K6: glottal-tone filter, dU/dt, Chebyshev low-pass) since the previous call (waits for the
+ * stream; the next call starts from zero).  afs_kernel_times is the same without K6; any pointer
+ * may be NULL. */
+typedef struct afs_kernel_timing {
+  double synth_ms;
+  int32_t synth_launches;
+  double plan_ms;
+  int32_t plan_launches;
+  double output_ms;
+  int32_t output_launches;
+} afs_kernel_timing;
+afs_status afs_kernel_times_ex(afs_ctx *ctx, afs_kernel_timing *timing);
 afs_status afs_kernel_times(afs_ctx *ctx, double *synth_ms, int32_t *synth_launches, double *plan_ms,
                             int32_t *plan_launches);
 
@@ -280,6 +305,10 @@ afs_status afs_gather_pcm(afs_comm *comm, const int16_t *local, int64_t count, i
                           const int64_t *root_counts);
 afs_status afs_comm_fence(afs_comm *comm);
 afs_status afs_comm_synchronize(afs_comm *comm);
+/* Device time of this rank's gathers since the previous call (HIP events on the comm's stream
+ * around each afs_gather_pcm, from the moment its input is ready to the end of its sends /
+ * receives) and their count; waits for the comm's stream.  Either pointer may be NULL. */
+afs_status afs_comm_gather_times(afs_comm *comm, double *ms, int32_t *count);
 /* The whole node from one host thread: `batch` utterances sharded over the n contexts of comms
  * (afs_comm_create_all) with afs_shard_range; each shard runs afs_synthesize on its GPU (seeds
  * keep the global index: NULL = u + 1), is converted to int16 on its GPU (afs_to_int16) and

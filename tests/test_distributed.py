@@ -57,6 +57,33 @@ def _to_int16(x: torch.Tensor, out: torch.Tensor) -> None:
     out.copy_(torch.from_numpy(Oracle().to_int16(x.numpy())).reshape(out.shape))
 
 
+def _resynth_int16(us):
+    """The global utterances `us` synthesized alone (one-utterance workloads at index u, seed u + 1)
+    and converted to int16: what bench.py's rank 0 recomputes for the gather check."""
+    ws = [workloads.static_vowels(1, seconds=SECONDS, fs=FS, first_utterance=u) for u in us]
+    x = torch.cat([_synth(w) for w in ws])
+    o = torch.empty(x.shape, dtype=torch.int16)
+    _to_int16(x, o)
+    return o.numpy()
+
+
+def test_gather_check_reports_a_corrupt_row():
+    """check_gathered flags a gathered row that differs from the re-synthesized utterance (the
+    check has teeth), and names it."""
+    world, n, T = 3, 4, 50
+    rng = np.random.default_rng(1)
+    full = rng.integers(-32768, 32767, size=(world * n, T)).astype(np.int16)
+    edges = sharding.edge_utterances(world, n)
+    assert [u for _, _, u in edges] == [0, 3, 4, 7, 8, 11]
+    rows = np.stack([full[u] for _, _, u in edges])
+    ok = sharding.check_gathered(rows, world, n, lambda us: full[list(us)])
+    assert ok["bitwise_equal"] and not ok["mismatches"]
+    rows[3, 17] ^= 1  # rank 1's last row
+    bad = sharding.check_gathered(rows, world, n, lambda us: full[list(us)])
+    assert not bad["bitwise_equal"]
+    assert bad["mismatches"] == [{"utterance": 7, "rank": 1, "row": 3, "differing_samples": 1}]
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -79,10 +106,19 @@ def _worker(rank, world, port, q):
             pg.drain()
             if rank == 0:
                 pcm.append(pg.result(slot).reshape(-1, out.shape[1]).numpy().copy())
+    # bench.py's self-check of the exchange: the synthesized audio itself through the gather, then
+    # rank 0 re-synthesizes the edge utterances of every block alone and compares bit for bit
+    slot = pg.submit(out)
+    pg.drain()
+    check = None
+    if rank == 0:
+        root = pg.result(slot)
+        rows = torch.stack([root[r, j] for r, j, _ in sharding.edge_utterances(world, n)])
+        check = sharding.check_gathered(rows, world, n, _resynth_int16)
     t = torch.tensor([float(out.numel())], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks timing reduction
     if rank == 0:
-        q.put((torch.cat(got).numpy(), w.seeds.copy(), float(t.item()), pcm))
+        q.put((torch.cat(got).numpy(), w.seeds.copy(), float(t.item()), pcm, check))
     else:
         q.put(("seeds", w.seeds.copy()))
     dist.barrier()
@@ -110,7 +146,9 @@ def test_gloo_world2_gather_matches_single_process():
         p.join(timeout=60)
         assert p.exitcode == 0
     gathered = next(r for r in res if not isinstance(r[0], str))
-    audio, seeds0, numel, pcm = gathered
+    audio, seeds0, numel, pcm, check = gathered
+    assert check["bitwise_equal"], check
+    assert check["utterances_checked"] == [0, B - 1, B, 2 * B - 1]
     seeds1 = next(r[1] for r in res if isinstance(r[0], str))
     full = workloads.static_vowels(world * B, seconds=SECONDS, fs=FS)
     ref = _synth(full).numpy()

@@ -23,7 +23,8 @@ pytestmark = pytest.mark.gpu
 
 GOLD_TOL = 1e-9
 RMS_TOL = 1e-4
-SOLVERS = ("cholesky", "tree", "seg")
+TREE_SOLVERS = ("tree",)           # the cooperative kernel (K1)
+SOLVERS = ("cholesky",) + TREE_SOLVERS
 
 
 @pytest.fixture(scope="module")
@@ -265,7 +266,7 @@ def _full_length_check(ctx, w, frames, stride, parity_report, label, solver):
     rms = np.sqrt(np.mean(err ** 2, axis=1))
     mx = np.abs(err).max(axis=1)
     flips = None
-    if solver in ("tree", "seg"):
+    if solver in TREE_SOLVERS:
         gd = ctx.rng_draws(B)[idx]
         flips = int(np.count_nonzero(gd != draws))
     parity_report.append(
@@ -294,7 +295,7 @@ def test_full_second_static_vowels_rms(contexts, solver, parity_report):
     assert np.array_equal(y, y2)
 
 
-@pytest.mark.parametrize("solver", ("tree", "seg"))
+@pytest.mark.parametrize("solver", TREE_SOLVERS)
 def test_full_second_fricatives_config5(contexts, parity_report, solver):
     """Config 5 at its defined length: fricatives s f z S Z x C R v (Default.params:44-52) with the
     velum open 1.0 cm^2 (MainPage.cpp:127-131), 1 s @ 44.1 kHz, noise sources active; 512
@@ -335,7 +336,7 @@ def test_frame_rate_vcv_hop_records(contexts, parity_report, monkeypatch):
     assert diff < 1e-7
 
 
-@pytest.mark.parametrize("solver", ("tree", "seg"))
+@pytest.mark.parametrize("solver", TREE_SOLVERS)
 def test_full_length_vcv_config3(contexts, parity_report, solver):
     """Config 3 at the reference's playTargetSequence timing (stationary 0.2/0.05/0.2/0.1 s,
     transitions 0.05 s: 30870 samples @ 44.1 kHz): 512 VCV utterances (V, (V)C(V):, V, V over

@@ -27,13 +27,13 @@ PW_FDN, PW_GAIN_G = 3, 15
 @pytest.fixture(scope="module")
 def lib():
     subprocess.check_call(["make", "-s", "-C", EMU])
-    lib = ctypes.CDLL(os.path.join(EMU, "libseg_emu.so"))
+    lib = ctypes.CDLL(os.path.join(EMU, "libplan_emu.so"))
     vp = ctypes.c_void_p
     lib.emu_plan_iv_check.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_long, vp]
     lib.emu_plan_hops.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_long,
                                   ctypes.c_double, ctypes.c_int, vp]
     lib.emu_plan_records.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_long,
-                                     ctypes.c_double, ctypes.c_int, ctypes.c_int, vp]
+                                     ctypes.c_double, ctypes.c_int, vp]
     lib.emu_plan_hop_words.argtypes = [vp, ctypes.c_double, vp]
     return lib
 
@@ -92,7 +92,7 @@ def test_hop_record_words_equal_dense_records(lib, oracle):
         hops = np.zeros((rows, F - 1), dtype=HOP_DTYPE)
         assert lib.emu_plan_hops(frames.ctypes.data, rows, F, hop, 0, n, 44100.0, 0, hops.ctypes.data) == 0
         dense = np.zeros((rows, n, PLAN_WORDS), dtype=np.uint64)
-        assert lib.emu_plan_records(frames.ctypes.data, rows, F, hop, 0, n, 44100.0, 0, 0, dense.ctypes.data) == 0
+        assert lib.emu_plan_records(frames.ctypes.data, rows, F, hop, 0, n, 44100.0, 0, dense.ctypes.data) == 0
         checked = 0
         for r in range(rows):
             for q in range(F - 1):

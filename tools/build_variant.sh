@@ -13,10 +13,10 @@ mkdir -p $O
 TREE_BASE=${TREE_BASE:-"-mllvm -disable-machine-licm -ffp-contract=fast-honor-pragmas -mllvm -amdgpu-sched-strategy=iterative-ilp"}
 COMMON="-O3 -std=c++17 -fPIC -Wall -Wno-unused-function -ffp-contract=off -fno-strict-aliasing -Wno-unknown-pragmas --offload-arch=gfx950 $FLAGS"
 objs=""
-for s in afs_capi.cpp afs_comm.cpp afs_tables.cpp seg_tables.cpp tds_lane.hip tds_tree.hip tds_seg.hip tds_plan.hip af_kernels.hip audio_kernels.hip; do
+for s in afs_capi.cpp afs_comm.cpp afs_tables.cpp tds_lane.hip tds_tree.hip tds_plan.hip af_kernels.hip audio_kernels.hip; do
   o=$O/${s%.*}.o
   extra=""
-  { [ $s = tds_tree.hip ] || [ $s = tds_seg.hip ]; } && extra="$TREE_BASE ${TREE_EXTRA:-}"  # (as build.py)
+  [ $s = tds_tree.hip ] && extra="$TREE_BASE ${TREE_EXTRA:-}"  # (as build.py)
   [ $s = tds_plan.hip ] && extra="${PLAN_EXTRA:-}"
   /opt/rocm/bin/hipcc -c -x hip $C/$s -o $o $COMMON $extra &
   objs="$objs $o"

@@ -45,6 +45,7 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   double *dout, *dlds;
   void *dlanes;
   uint64_t *dprof;
+  double *dp25;  // section 25's pressures (K6's tone input; the kernel stores them every sample)
   const int blocks = (B + UPB - 1) / UPB, waves = blocks * WPB;
   CK(hipMalloc(&dt, sizeof(Tables)));
   CK(hipMemcpy(dt, ht, sizeof(Tables), hipMemcpyHostToDevice));
@@ -56,13 +57,14 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   CK(hipMalloc(&dlds, sizeof(double) * (size_t)B * tree_lds_doubles()));
   CK(hipMalloc(&dlanes, (size_t)B * TW * tree_lane_bytes()));
   CK(hipMalloc(&dprof, sizeof(uint64_t) * waves * PH_COUNT));
+  CK(hipMalloc(&dp25, sizeof(double) * (size_t)B * (F - 1) * hop));
   CK(launch_tree_reset(dlanes, dlds, B, ds, nullptr));
   const int64_t T = (int64_t)(F - 1) * hop;
   uint64_t *dplan;
   CK(hipMalloc(&dplan, (size_t)B * T * PLAN_RECORD_BYTES));
   PlanArgs pa{dt, df, F, B, hop, 0, T, dplan, T, 0, &dt->consts.sec[0]};
   CK(launch_plan(pa, nullptr));
-  TreeArgs a{dt, df, F, nullptr, hop, 0, T, dout, T, dplan, T, dlanes, dlds, B, ht->uni};
+  TreeArgs a{dt, df, F, nullptr, hop, 0, T, dout, T, dplan, T, dlanes, dlds, B, ht->uni, nullptr, 0, dp25, T};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -84,7 +86,7 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
       g_wave[w] += h[(size_t)w * PH_COUNT + p];
     }
   (void)hipFree(dt); (void)hipFree(df); (void)hipFree(ds); (void)hipFree(dout);
-  (void)hipFree(dlds); (void)hipFree(dlanes); (void)hipFree(dprof); (void)hipFree(dplan);
+  (void)hipFree(dlds); (void)hipFree(dlanes); (void)hipFree(dprof); (void)hipFree(dplan); (void)hipFree(dp25);
   delete ht;
   return waves;
 }
