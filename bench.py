@@ -332,6 +332,8 @@ def describe(args, m: Measured, world: int, digest: str) -> dict:
         "launches_per_step": m.kt["synth_launches"] / m.steps,
         "launch_timing": "HIP events around every launch on the library's stream (afs_kernel_times)",
         "plan_kernel_ms_per_step": m.kt["plan_ms"] / m.steps,
+        "output_kernel_ms_per_launch": m.kt["output_ms"] / max(1, m.kt["output_launches"]),
+        "output_kernel": "tree_output_kernel (K6: glottal-tone filter + dU/dt + Chebyshev low-pass after each K1 launch)",
         "binding_resource": "neither HBM nor MFMA: the latency of the per-sample fp64 recurrence "
                             "(SURVEY.md 8(d)); see fp64",
     }
@@ -444,6 +446,12 @@ def main() -> None:
         if world > 1:
             result["multi_gpu"] = m.multi
             result["gather_check"] = m.gather_check
+        if world > 1 and not args.no_cpu_baseline:
+            # (no CPU timing at N > 1: the error of rank 0's first utterances against the reference build)
+            _, max_abs, max_rms = cpu_leg(args, m, min(8, B))
+            result["max_abs_err_vs_cpu_ref"] = max_abs
+            result["max_rms_err_vs_cpu_ref"] = max_rms
+            result["cpu_ref_utterances"] = min(8, B)
         if world == 1 and not args.no_cpu_baseline:
             cb, max_abs, max_rms = cpu_leg(args, m, min(args.cpu_utterances, B))
             result["cpu_baseline"] = cb
