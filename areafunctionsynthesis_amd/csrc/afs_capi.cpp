@@ -70,8 +70,18 @@ int64_t pad64(int64_t b) { return (b + 63) / 64 * 64; }
 
 bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_TREE || s == AFS_SOLVER_SOR; }
 
-// the cooperative kernel (16 lanes per utterance, noise-source plans from K5)
+// the cooperative kernel (noise-source plans from K5)
 bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE; }
+
+// Lanes per utterance of the tree kernel for a batch of B: forced by AFS_LANES_16 / AFS_LANES_64,
+// else the voice kernel (64 lanes, one utterance per wave: fewer instructions per sample on the
+// chain) while the batch leaves SIMDs idle with 16 lanes per utterance (B <= the GPU's SIMDs), the
+// throughput kernel (16 lanes, four utterances per wave) above.
+int lanes_for(const afs_ctx *c, int64_t B) {
+  if (c->cfg.flags & AFS_LANES_16) return afs::TREE_W;
+  if (c->cfg.flags & AFS_LANES_64) return afs::TREE_VOICE_W;
+  return B <= c->simds ? afs::TREE_VOICE_W : afs::TREE_W;
+}
 
 // Bytes of noise-source plans one tree launch may use (afs_ctx::plan_budget: 4 GiB, or
 // AFS_PLAN_BUDGET_MB); a launch covers at most plan_budget / (rows * 128 B) samples and at most
@@ -107,7 +117,7 @@ void prof_pair(afs_ctx *c, hipEvent_t a, hipEvent_t b, int kind) {
 
 afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int rows, int ntrans, int hop,
                       double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B,
-                      const int32_t *frame_row = nullptr) {
+                      int width, const int32_t *frame_row = nullptr) {
   if (tree(c)) {
     // Launch chunks of `per` samples: K5 (the chunk's noise-source plans), then K1.  With
     // AFS_PLAN_OVERLAP=1 in the environment (afs_ctx::overlap), K5 of chunk k + 1 runs on the
@@ -174,7 +184,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
                       (const uint64_t *)buf[k & 1], per, lanes, (double *)ws, B, c->host_tab.uni,
                       hbuf[k & 1], hstride, (double *)c->p25, per};
       hipEvent_t e1 = prof_event(c);
-      HIP_TRY(c, afs::launch_tree_synth(a, c->stream));
+      HIP_TRY(c, afs::launch_tree_synth(a, width, c->stream));
       hipEvent_t e2 = prof_event(c);
       prof_pair(c, e1, e2, 0);
       // K6: the glottal-tone filter and the output stage of the launch's samples
@@ -203,13 +213,14 @@ size_t ws_bytes_for(const afs_ctx *c, int64_t bp) {
   if (tree(c)) return (size_t)bp * afs::tree_lds_doubles() * sizeof(double);
   return (size_t)(afs::lane_ws_rows(c->host_tab) * bp) * sizeof(double);
 }
-size_t lanes_bytes_for(const afs_ctx *c, int64_t bp) {
-  return tree(c) ? (size_t)bp * afs::TREE_W * afs::tree_lane_bytes() : 0;
+size_t lanes_bytes_for(const afs_ctx *c, int64_t bp, int width) {
+  return tree(c) ? (size_t)bp * (size_t)width * (size_t)afs::tree_lane_bytes(width) : 0;
 }
 
-afs_status reset_state(afs_ctx *c, void *ws, int32_t *rng, void *lanes, int64_t bp, int B, const uint32_t *seeds_dev) {
+afs_status reset_state(afs_ctx *c, void *ws, int32_t *rng, void *lanes, int64_t bp, int B, const uint32_t *seeds_dev,
+                       int width) {
   if (tree(c))
-    HIP_TRY(c, afs::launch_tree_reset(lanes, (double *)ws, B, seeds_dev, c->stream));
+    HIP_TRY(c, afs::launch_tree_reset(lanes, (double *)ws, B, seeds_dev, width, c->stream));
   else
     HIP_TRY(c, afs::launch_lane_reset((double *)ws, rng, bp, B, seeds_dev, c->stream));
   return AFS_OK;
@@ -289,7 +300,8 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   *out = nullptr;
   afs_config c;
   if (cfg) c = *cfg; else afs_config_default(&c);
-  if (!(c.sampling_rate_hz > 0.0) || c.precision != AFS_FP64 || !solver_ok(c.solver))
+  if (!(c.sampling_rate_hz > 0.0) || c.precision != AFS_FP64 || !solver_ok(c.solver) ||
+      ((c.flags & AFS_LANES_16) && (c.flags & AFS_LANES_64)))
     return AFS_ERR_INVALID_ARGUMENT;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
@@ -300,6 +312,11 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   if (hipSetDevice(c.device) != hipSuccess) return AFS_ERR_NO_DEVICE;
   afs_ctx *ctx = new afs_ctx();
   ctx->cfg = c;
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus <= 0) cus = 256;
+    ctx->simds = 4 * cus;  // (4 SIMDs per CU on CDNA)
+  }
   afs::build_tables(&ctx->host_tab, c.sampling_rate_hz, c.options);
   if (ctx->host_tab.n_rounds <= 0) { afs_destroy(ctx); return AFS_ERR_UNSUPPORTED; }
   afs_status st = AFS_OK;
@@ -408,12 +425,14 @@ static afs_status synth_core(afs_ctx *c, const afs_frame *frames, const uint32_t
     dout = (double *)c->stage_out;
   }
   // state
+  const int width = lanes_for(c, B);
   if ((s = ensure(c, &c->ws, &c->ws_bytes, ws_bytes_for(c, bp))) != AFS_OK) return s;
   if ((s = ensure(c, (void **)&c->rng, &c->rng_bytes, (size_t)(32 * bp) * sizeof(int32_t))) != AFS_OK) return s;
-  if (tree(c) && (s = ensure(c, &c->tree_lanes, &c->tree_lanes_bytes, lanes_bytes_for(c, bp))) != AFS_OK) return s;
-  if ((s = reset_state(c, c->ws, c->rng, c->tree_lanes, bp, B, dseeds)) != AFS_OK) return s;
+  if (tree(c) && (s = ensure(c, &c->tree_lanes, &c->tree_lanes_bytes, lanes_bytes_for(c, bp, width))) != AFS_OK)
+    return s;
+  if ((s = reset_state(c, c->ws, c->rng, c->tree_lanes, bp, B, dseeds, width)) != AFS_OK) return s;
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-  if ((s = run_chunks(c, dframes, F, B, F - 1, hop, dout, T, c->ws, c->rng, c->tree_lanes, bp, B)) != AFS_OK)
+  if ((s = run_chunks(c, dframes, F, B, F - 1, hop, dout, T, c->ws, c->rng, c->tree_lanes, bp, B, width)) != AFS_OK)
     return s;
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   c->last_B = B;
@@ -446,6 +465,11 @@ afs_status afs_synthesize(afs_ctx *c, const afs_frame *frames, const uint32_t *s
   if (!frames || !out || B <= 0 || F < 2 || hop < 1)
     return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_synthesize: need frames, out, batch>0, num_frames>=2, hop>=1");
   return synth_core(c, frames, seeds, B, F, hop, out, nonfinite, rep, false);
+}
+
+int32_t afs_lanes_per_utterance(const afs_ctx *c, int32_t batch) {
+  if (!c || c->cfg.solver != AFS_SOLVER_TREE || batch <= 0) return 1;
+  return lanes_for(c, batch);
 }
 
 afs_status afs_kernel_times_ex(afs_ctx *c, afs_kernel_timing *t) {
@@ -627,6 +651,7 @@ afs_status afs_session_create(afs_ctx *c, int32_t B, const uint32_t *seeds, afs_
   s->ctx = c;
   s->B = B;
   s->bp = pad64(B);
+  s->lanes = lanes_for(c, B);  // (fixed for the session: the per-lane state layout depends on it)
   auto bail = [&](hipError_t e) {
     afs_session_destroy(s);
     return fail(c, e == hipErrorOutOfMemory ? AFS_ERR_OUT_OF_MEMORY : AFS_ERR_HIP, "session alloc: %s", hipGetErrorString(e));
@@ -634,7 +659,7 @@ afs_status afs_session_create(afs_ctx *c, int32_t B, const uint32_t *seeds, afs_
   hipError_t e;
   if ((e = hipMalloc(&s->ws, ws_bytes_for(c, s->bp))) != hipSuccess) return bail(e);
   if ((e = hipMalloc((void **)&s->rng, (size_t)(32 * s->bp) * sizeof(int32_t))) != hipSuccess) return bail(e);
-  if (tree(c) && (e = hipMalloc(&s->tree_lanes, lanes_bytes_for(c, s->bp))) != hipSuccess) return bail(e);
+  if (tree(c) && (e = hipMalloc(&s->tree_lanes, lanes_bytes_for(c, s->bp, s->lanes))) != hipSuccess) return bail(e);
   if ((e = hipMalloc((void **)&s->pair, (size_t)B * 2 * sizeof(afs_frame))) != hipSuccess) return bail(e);
   if ((e = hipMalloc((void **)&s->seeds, (size_t)B * sizeof(uint32_t))) != hipSuccess) return bail(e);
   *out = s;
@@ -655,7 +680,7 @@ afs_status afs_session_reset(afs_session *s, const uint32_t *seeds) {
     HIP_TRY(c, hipMemcpyAsync(s->seeds, seeds, (size_t)s->B * 4, k, c->stream));
   }
   // (no seeds: the reset kernels seed voice u with u + 1)
-  afs_status st = reset_state(c, s->ws, s->rng, s->tree_lanes, s->bp, s->B, seeds ? s->seeds : nullptr);
+  afs_status st = reset_state(c, s->ws, s->rng, s->tree_lanes, s->bp, s->B, seeds ? s->seeds : nullptr, s->lanes);
   if (st != AFS_OK) return st;
   s->latched = false;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -700,7 +725,8 @@ afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32
     dout = (double *)c->stage_out;
   }
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-  if ((st = run_chunks(c, s->pair, 2, B, 1, n, dout, n, s->ws, s->rng, s->tree_lanes, s->bp, B)) != AFS_OK) return st;
+  if ((st = run_chunks(c, s->pair, 2, B, 1, n, dout, n, s->ws, s->rng, s->tree_lanes, s->bp, B, s->lanes)) != AFS_OK)
+    return st;
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   // prevTube = *newTube (Synthesizer.cpp:633-637)
   HIP_TRY(c, hipMemcpy2DAsync(s->pair, 2 * sizeof(afs_frame), s->pair + 1, 2 * sizeof(afs_frame),
@@ -887,10 +913,12 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
     dout = (double *)c->stage_out;
   }
   const int64_t bp = pad64(B);
+  const int width = lanes_for(c, B);
   if ((s = ensure(c, &c->ws, &c->ws_bytes, ws_bytes_for(c, bp))) != AFS_OK) return s;
   if ((s = ensure(c, (void **)&c->rng, &c->rng_bytes, (size_t)(32 * bp) * sizeof(int32_t))) != AFS_OK) return s;
-  if (tree(c) && (s = ensure(c, &c->tree_lanes, &c->tree_lanes_bytes, lanes_bytes_for(c, bp))) != AFS_OK) return s;
-  if ((s = reset_state(c, c->ws, c->rng, c->tree_lanes, bp, B, dseeds)) != AFS_OK) return s;
+  if (tree(c) && (s = ensure(c, &c->tree_lanes, &c->tree_lanes_bytes, lanes_bytes_for(c, bp, width))) != AFS_OK)
+    return s;
+  if ((s = reset_state(c, c->ws, c->rng, c->tree_lanes, bp, B, dseeds, width)) != AFS_OK) return s;
   // time chunks of Tc samples: Tc + 1 frames per sequence (the first repeats the previous
   // chunk's last), at most 1 GiB of frames
   const int64_t budget = (int64_t)1 << 30;
@@ -902,8 +930,8 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
   for (int64_t k0 = 0; k0 < T; k0 += Tc) {
     const int nk = (int)std::min<int64_t>(Tc, T - k0);
     HIP_TRY(c, afs::launch_target_frames(dseq, Q, plan, k0, nk + 1, Tc + 1, dframes, c->stream));
-    if ((s = run_chunks(c, dframes, Tc + 1, Q, nk, 1, dout + k0, T, c->ws, c->rng, c->tree_lanes, bp, B, drow)) !=
-        AFS_OK)
+    if ((s = run_chunks(c, dframes, Tc + 1, Q, nk, 1, dout + k0, T, c->ws, c->rng, c->tree_lanes, bp, B, width,
+                        drow)) != AFS_OK)
       return s;
   }
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));

@@ -12,6 +12,7 @@
 
 struct afs_ctx {
   afs_config cfg{};
+  int simds = 1024;  // SIMDs of the device (the voice kernel's batch limit, afs_capi.cpp lanes_for)
   hipStream_t stream = nullptr;
   afs::Tables host_tab{};
   afs::Tables *dev_tab = nullptr;
@@ -72,6 +73,7 @@ struct afs_session {
   void *ws = nullptr;          // lane solver: SoA workspace; tree solver: per-utterance LDS blocks
   int32_t *rng = nullptr;      // lane solver: generator state; tree solver: unused
   void *tree_lanes = nullptr;  // tree solver: per-lane register state
+  int lanes = 16;              // tree solver: lanes per utterance (fixed at creation)
   afs_frame *pair = nullptr;   // [B][2]: previous frame, new frame
   uint32_t *seeds = nullptr;   // device copy
   bool latched = false;

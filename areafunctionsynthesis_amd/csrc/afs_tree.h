@@ -21,7 +21,7 @@ struct TreeArgs {
   int64_t out_stride;
   const uint64_t *plan;     // plan[(row(u) * plan_stride + s - s_begin) * 16 + w] (tree_plan.h)
   int64_t plan_stride;
-  void *lane_state;         // per-lane register state, B * TREE_W entries
+  void *lane_state;         // per-lane register state, B * lanes entries (Lane<lanes>)
   double *lds_state;        // per-utterance LDS block, B * tree_lds_doubles()
   int B;
   Uni uni;                  // copy of tab->uni: scalar kernel arguments
@@ -66,12 +66,15 @@ inline int64_t plan_work_bytes(int64_t rows, int64_t slots) { return (rows * slo
 #ifndef AFS_TREE_MIN_WAVES
 #define AFS_TREE_MIN_WAVES 1  // waves per SIMD the register allocation must allow
 #endif
-constexpr int TREE_W = AFS_TREE_W;      // lanes per utterance (16 or 32)
-constexpr int TREE_WPB = AFS_TREE_WPB;  // waves per block
-int64_t tree_lane_bytes();
+constexpr int TREE_W = AFS_TREE_W;      // lanes per utterance of the throughput kernel (16)
+constexpr int TREE_WPB = AFS_TREE_WPB;  // its waves per block
+constexpr int TREE_VOICE_W = 64;        // lanes per utterance of the voice kernel (one utterance per wave)
+// Lanes per utterance: TREE_W or TREE_VOICE_W (the per-lane state layout, Lane<lanes>, differs).
+int64_t tree_lane_bytes(int lanes);
 int64_t tree_lds_doubles();
-hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const uint32_t *seeds, hipStream_t st);
-hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st);
+hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const uint32_t *seeds, int lanes,
+                             hipStream_t st);
+hipError_t launch_tree_synth(const TreeArgs &a, int lanes, hipStream_t st);
 // K6, after each tree_synth launch of samples [s_begin, s_end): the glottal-tone filter over the
 // section-25 pressures (p25, skin != 0) and the output stage over the flows the launch stored
 // (out[u * out_stride + s - s_begin], replaced by the audio).

@@ -9,12 +9,13 @@ using namespace tree;
 
 namespace {
 
-// one kernel per glottis model (TriangularGlottis, the reference's; TwoMassModel) and plan mode
-// (HOPS: hop records, hops >= PLAN_HOP_MIN; dense records otherwise)
-template <int MODEL, bool HOPS>
-__global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_synth_kernel(TreeArgs a) {
-  __shared__ WaveLds lds;
-  tree_synth_body<false, MODEL, HOPS>(a, lds, nullptr);
+// one kernel per glottis model (TriangularGlottis, the reference's; TwoMassModel), plan mode
+// (HOPS: hop records, hops >= PLAN_HOP_MIN; dense records otherwise) and lanes per utterance W
+// (16: the throughput kernel; 64: the voice kernel, tree_kernel.h)
+template <int MODEL, bool HOPS, int W>
+__global__ void __launch_bounds__(64 * Geom<W>::WPB, AFS_TREE_MIN_WAVES) tree_synth_kernel(TreeArgs a) {
+  __shared__ WaveLdsT<W> lds;
+  tree_synth_body<false, MODEL, HOPS, W>(a, lds, nullptr);
 }
 
 // K6: the output stage of a launch's samples -- dU/dt, the 8-pole Chebyshev low-pass, x 0.004 /
@@ -35,12 +36,13 @@ __global__ void __launch_bounds__(64) tree_output_kernel(const Tables *tab, doub
 }
 
 // seeds == nullptr: utterance u is seeded u + 1 (afs.h)
-__global__ void tree_reset_kernel(Lane<TW> *lanes, double *lds, int B, const uint32_t *seeds) {
+template <int W>
+__global__ void tree_reset_kernel(Lane<W> *lanes, double *lds, int B, const uint32_t *seeds) {
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= (int64_t)B * TW) return;
-  const int u = (int)(id / TW), gl = (int)(id % TW);
-  Lane<TW> R;
-  reset_lane<TW>(gl, R);
+  if (id >= (int64_t)B * W) return;
+  const int u = (int)(id / W), gl = (int)(id % W);
+  Lane<W> R;
+  reset_lane<W>(gl, R);
   lanes[id] = R;
   if (gl == 0) reset_lds(lds + (int64_t)u * X_TOTAL, seeds ? seeds[u] : (uint32_t)u + 1u);
 }
@@ -119,28 +121,39 @@ hipError_t launch_tree_output(const Tables *tab, double *lds_state, double *out,
   return hipGetLastError();
 }
 
-int64_t tree_lane_bytes() { return (int64_t)sizeof(Lane<TW>); }
+int64_t tree_lane_bytes(int lanes) { return lanes == 64 ? (int64_t)sizeof(Lane<64>) : (int64_t)sizeof(Lane<TW>); }
 int64_t tree_lds_doubles() { return X_TOTAL; }
 
-hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const uint32_t *seeds, hipStream_t st) {
+hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const uint32_t *seeds, int lanes,
+                             hipStream_t st) {
   if (B <= 0) return hipSuccess;
-  int64_t n = (int64_t)B * TW;
-  hipLaunchKernelGGL(tree_reset_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                     (Lane<TW> *)lane_state, lds_state, B, seeds);
+  const int64_t n = (int64_t)B * lanes;
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  if (lanes == 64)
+    hipLaunchKernelGGL(tree_reset_kernel<64>, grid, block, 0, st, (Lane<64> *)lane_state, lds_state, B, seeds);
+  else
+    hipLaunchKernelGGL(tree_reset_kernel<TW>, grid, block, 0, st, (Lane<TW> *)lane_state, lds_state, B, seeds);
   return hipGetLastError();
 }
 
-hipError_t launch_tree_synth(const TreeArgs &a, hipStream_t st) {
-  if (a.B <= 0 || a.s_end <= a.s_begin) return hipSuccess;
-  const dim3 grid((a.B + UPB - 1) / UPB), block(64 * WPB);
+template <int W>
+static void launch_synth_w(const TreeArgs &a, hipStream_t st) {
+  constexpr int UPB_ = Geom<W>::UPB;
+  const dim3 grid((a.B + UPB_ - 1) / UPB_), block(64 * Geom<W>::WPB);
   const bool two = a.uni.opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
   if (a.hops) {
-    if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true>), grid, block, 0, st, a);
+    if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true, W>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, W>), grid, block, 0, st, a);
   } else {
-    if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, false>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false>), grid, block, 0, st, a);
+    if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, false, W>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false, W>), grid, block, 0, st, a);
   }
+}
+
+hipError_t launch_tree_synth(const TreeArgs &a, int lanes, hipStream_t st) {
+  if (a.B <= 0 || a.s_end <= a.s_begin) return hipSuccess;
+  if (lanes == 64) launch_synth_w<64>(a, st);
+  else launch_synth_w<TW>(a, st);
   return hipGetLastError();
 }
 

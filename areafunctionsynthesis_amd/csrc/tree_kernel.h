@@ -26,18 +26,28 @@ namespace tree {
 // per sample, +0.3 % without them, profiles/r03z_ab.txt).
 #define AFS_DPP(src, ctrl, rmask, bmask, bc) __builtin_amdgcn_mov_dpp((src), (ctrl), (rmask), (bmask), (bc))
 
+// Lanes per utterance: W = 16 (TREE_W, the throughput kernel: four utterances per wave64, six
+// sections per lane) or W = 64 (the voice kernel: one utterance per wave, two sections per lane --
+// fewer instructions per sample on the chain, for batches that leave SIMDs idle and for
+// real-time voices).  The solver always runs on the utterance's first 16 lanes.
 constexpr int TW = TREE_W;
-constexpr int UPW = 64 / TW;          // utterances per wave
-constexpr int WPB = TREE_WPB;         // waves per block (they share one copy of the tables)
-constexpr int UPB = UPW * WPB;        // utterances per block
-static_assert(TW == 16 || TW == 32, "collectives are written for 16 or 32 lanes per utterance");
+template <int W>
+struct Geom {
+  static_assert(W == 16 || W == 32 || W == 64, "collectives are written for 16, 32 or 64 lanes per utterance");
+  static constexpr int UPW = 64 / W;                 // utterances per wave
+  static constexpr int WPB = W == 64 ? 1 : TREE_WPB;  // waves per block (they share one copy of the tables)
+  static constexpr int UPB = UPW * WPB;              // utterances per block
+};
+constexpr int UPW = Geom<TW>::UPW;
+constexpr int WPB = Geom<TW>::WPB;
+constexpr int UPB = Geom<TW>::UPB;
 
-template <bool PROF>
+template <bool PROF, int W = TW>
 struct GpuExec {
   static constexpr bool kToneOut = true;        // the tone filter in K6 from the stored p[25] (+0.5 %, r03ai_ab.txt)
   static constexpr bool kGlottisSplit = true;   // the glottis' masses on the two lane halves (+1.1 %, r03ag_ab.txt)
   int gl;
-  Lane<TW> *R;
+  Lane<W> *R;
   uint64_t last = 0;
   uint64_t acc[PROF ? PH_COUNT : 1] = {};
   template <class F> __device__ __forceinline__ void par(F f) { f(gl, *R); }
@@ -46,20 +56,19 @@ struct GpuExec {
   // part (same inputs, same values, same stores), so the two interleave without a branch.
   template <class F, class G> __device__ __forceinline__ void par_uniform(F f, G g) { f(gl, *R); g(*R); }
   template <class F> __device__ __forceinline__ void lanes(int n, F f) {
-    if (n >= TW || gl < n) f(gl, *R);  // (no branch when every lane takes part)
+    if (n >= W || gl < n) f(gl, *R);  // (no branch when every lane takes part)
   }
   __device__ __forceinline__ void sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  // Collectives over the lanes of this utterance.  16 lanes = one DPP row: quad_perm xor 1
-  // and xor 2, then row_half_mirror and row_mirror combine quads and halves (all lanes of
-  // the row end with the same result); 32 lanes add a swap of the two rows (lane ^ 16).
+  // Bit gl of the result: f(gl, R) of this utterance's lane gl.
   template <class F> __device__ __forceinline__ uint64_t ballot(F f) {
     const bool p = f(gl, *R);
     const uint64_t b = __ballot(p);
-    return (b >> (__lane_id() & ~(TW - 1))) & ((1ull << TW) - 1);
+    if constexpr (W == 64) return b;
+    else return (b >> (__lane_id() & ~(W - 1))) & ((1ull << W) - 1);
   }
   template <int CTRL> __device__ __forceinline__ static int dpp(int v) {
     return AFS_DPP(v, CTRL, 0xF, 0xF, false);
@@ -69,57 +78,39 @@ struct GpuExec {
     const int lo = dpp<CTRL>((int)(uint32_t)b), hi = dpp<CTRL>((int)(uint32_t)(b >> 32));
     return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
   }
-  template <int CTRL> __device__ __forceinline__ static MinIdx min_step(MinIdx a) {
-    return min_idx_combine(a, MinIdx{dpp<CTRL>(a.v), dpp<CTRL>(a.i)});
-  }
-  __device__ __forceinline__ static double xor16(double v) { return __shfl_xor(v, 16, 64); }
-  __device__ __forceinline__ static int xor16(int v) { return __shfl_xor(v, 16, 64); }
-  template <class F> __device__ __forceinline__ MinIdx min_index(F f) {
-    MinIdx b = f(gl, *R);
-    b = min_step<0xB1>(b);   // quad_perm [1,0,3,2]
-    b = min_step<0x4E>(b);   // quad_perm [2,3,0,1]
-    b = min_step<0x141>(b);  // row_half_mirror
-    b = min_step<0x140>(b);  // row_mirror
-    if constexpr (TW == 32) b = min_idx_combine(b, MinIdx{xor16(b.v), xor16(b.i)});
-    return b;
-  }
-  template <class F> __device__ __forceinline__ double max_value(F f) {
-    double b = f(gl, *R);
-    b = max_combine(b, dpp<0xB1>(b));
-    b = max_combine(b, dpp<0x4E>(b));
-    b = max_combine(b, dpp<0x141>(b));
-    b = max_combine(b, dpp<0x140>(b));
-    if constexpr (TW == 32) b = max_combine(b, xor16(b));
-    return b;
-  }
   // Areas of the neighbouring dynamic sections: section s = 23 + jW + gl, so s+1 is slot j
   // of lane gl+1 (slot j+1 of lane 0 for the last lane) and s-1 slot j of lane gl-1 (slot
   // j-1 of the last lane for lane 0).  16 lanes: row rotations (row_ror 15 / 1) of the
   // utterance's DPP row; 32 lanes: ds_bpermute.
   __device__ __forceinline__ void dyn_neighbors() {
-    using S = Shape<TW>;
+    using S = Shape<W>;
 #pragma unroll
     for (int j = 0; j < S::ND; ++j) {
       const double up = (j + 1 < S::ND) ? R->acur[j + 1 < S::ND ? j + 1 : j] : 0.0;
       const double dn = (j >= 1) ? R->acur[j >= 1 ? j - 1 : j] : 0.0;
-      if constexpr (TW == 16) {
+      if constexpr (W == 16) {
         const double a = dpp<0x12F>(R->acur[j]), b = dpp<0x12F>(up);  // from lane gl+1 (mod 16)
         const double c = dpp<0x121>(R->acur[j]), d = dpp<0x121>(dn);  // from lane gl-1 (mod 16)
-        R->anx[j] = gl == TW - 1 ? b : a;
+        R->anx[j] = gl == W - 1 ? b : a;
         R->apv[j] = gl == 0 ? d : c;
+      } else if constexpr (S::ND == 1) {  // (64 lanes: one dynamic slot, no wrap into another slot)
+        const int base = (int)(__lane_id() & ~(W - 1));
+        R->anx[j] = __shfl(R->acur[j], base + (gl + 1) % W, 64);
+        R->apv[j] = __shfl(R->acur[j], base + (gl + W - 1) % W, 64);
       } else {
-        const int base = (int)(__lane_id() & ~(TW - 1));
-        const int nl = base + (gl + 1) % TW, pl = base + (gl + TW - 1) % TW;
+        const int base = (int)(__lane_id() & ~(W - 1));
+        const int nl = base + (gl + 1) % W, pl = base + (gl + W - 1) % W;
         const double a = __shfl(R->acur[j], nl, 64), b = __shfl(up, nl, 64);
         const double c = __shfl(R->acur[j], pl, 64), d = __shfl(dn, pl, 64);
-        R->anx[j] = gl == TW - 1 ? b : a;
+        R->anx[j] = gl == W - 1 ? b : a;
         R->apv[j] = gl == 0 ? d : c;
       }
     }
   }
   // Inclusive prefix sums over the utterance's lanes: row_shr 1, 2, 4, 8 with zero fill
   // (bound_ctrl) inside the 16-lane row; for 32 lanes, lane 15 of the first row is added to
-  // the second (row_bcast15 into rows 1 and 3).
+  // the second (row_bcast15 into rows 1 and 3).  64 lanes: the sums of lanes 16-63 stay row-local
+  // -- the only caller (rng_block) consumes lanes < rng_lanes() = 10 alone.
   template <int CTRL> __device__ __forceinline__ static uint32_t shr(uint32_t v) {
     return (uint32_t)AFS_DPP((int)v, CTRL, 0xF, 0xF, true);
   }
@@ -133,7 +124,7 @@ struct GpuExec {
       x += shr<0x114>(x);
       x += shr<0x118>(x);
       // (rows 1 and 3 only: the other rows keep the old value 0)
-      if constexpr (TW == 32) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+      if constexpr (W == 32) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
       v.v[i] = x;
     }
     g(gl, *R, v);
@@ -177,20 +168,23 @@ struct GpuExec {
 
 // LDS of one block: the packed hot tables (shared by all its utterances) and one block per
 // utterance.
-struct WaveLds {
+template <int W>
+struct WaveLdsT {
   Consts C;
-  double X[UPB][X_STRIDE];
+  double X[Geom<W>::UPB][X_STRIDE];
 };
+using WaveLds = WaveLdsT<TW>;
 
 // prof (PROF only): per wave, PH_COUNT cycle sums (s_memtime) over the launch.
 // HOPS: the plan words come from hop records (a.hops, tree_plan.h PlanHop): lane gl keeps word
 // gl's kind and inputs for the hop and evaluates the word at every sample; a mixed hop's samples
 // read their dense records as without HOPS.
-template <bool PROF, int MODEL, bool HOPS = false>
-__device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds, uint64_t *prof) {
+template <bool PROF, int MODEL, bool HOPS = false, int W = TW>
+__device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &lds, uint64_t *prof) {
+  constexpr int UPB_ = Geom<W>::UPB, WPB_ = Geom<W>::WPB;
   const int lane = threadIdx.x;  // 0 .. 64 WPB - 1
-  const int g = lane / TW, gl = lane % TW;
-  const int u = blockIdx.x * UPB + g;
+  const int g = lane / W, gl = lane % W;
+  const int u = blockIdx.x * UPB_ + g;
   const bool valid = u < a.B;
   const int ue = valid ? u : 0;
   double *X = lds.X[g];
@@ -198,14 +192,14 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   {  // stage the hot tables (8-byte words; Consts is a multiple of 8 bytes)
     const uint64_t *src = (const uint64_t *)&T.consts;
     uint64_t *dst = (uint64_t *)&lds.C;
-    for (int k = lane; k < (int)(sizeof(Consts) / 8); k += 64 * WPB) dst[k] = src[k];
+    for (int k = lane; k < (int)(sizeof(Consts) / 8); k += 64 * WPB_) dst[k] = src[k];
   }
-  Lane<TW> R = ((const Lane<TW> *)a.lane_state)[(int64_t)ue * TW + gl];
+  Lane<W> R = ((const Lane<W> *)a.lane_state)[(int64_t)ue * W + gl];
   const double *ls = a.lds_state + (int64_t)ue * X_TOTAL;
-  for (int k = gl; k < X_TOTAL; k += TW) X[k] = ls[k];
+  for (int k = gl; k < X_TOTAL; k += W) X[k] = ls[k];
   __syncthreads();
   const Consts &C = lds.C;
-  GpuExec<PROF> ex{gl, &R};
+  GpuExec<PROF, W> ex{gl, &R};
   if constexpr (PROF) ex.last = __builtin_amdgcn_s_memtime();
   const int64_t row = a.frame_row ? a.frame_row[ue] : ue;
   const afs_frame *fu = a.frames + row * a.frame_stride;
@@ -220,7 +214,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   // back into the tube: the kernel stores the radiated flows and section 25's pressures, and K6
   // (tree_output_kernel) filters them after the launch, so none of the filters' state or code is
   // in this kernel's registers.
-  frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
+  frame_load<W>(gl, R, X, fu + (k - 1), fu + k);
   // hop mode: this hop's record (word gl % 16: its kind and inputs; whether the hop is mixed)
   const PlanHop *hr = HOPS ? a.hops + row * a.hop_stride : nullptr;
   double hp[4] = {0.0, 0.0, 0.0, 0.0};
@@ -238,7 +232,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
   // next right frame are loaded during the last sample of a hop, so that their latency hides
   // behind that sample's work instead of stalling the frame transition; the new left frame is
   // the old right one (frame_shift).
-  NextFrame<TW> nf{};
+  NextFrame<W> nf{};
   ex.sync();
   uint64_t next = hmixed ? pl[0] : 0;
   for (int64_t t = 0; t < n; ++t) {
@@ -257,7 +251,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
       next = pl[tn * PLAN_WORDS];  // the next sample's word, a sample ahead
       if (i + 1 == hop && t + 1 < n) nf.load(gl, fu + k + 1);
     }
-    sample_step<TW, MODEL>(ex, X, a.uni, C, ratio, true);
+    sample_step<W, MODEL>(ex, X, a.uni, C, ratio, true);
     if (valid && gl == 0) o[t] = R.sample;
     // section 25's new pressure (lane 2's slot 0), the glottal-tone filter's input in K6
     if (valid && gl == 2) p25o[t] = R.p[0];
@@ -266,11 +260,11 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
       ++k;
       if (t + 1 < n) {
         if constexpr (HOPS) {
-          frame_load<TW>(gl, R, X, fu + (k - 1), fu + k);
+          frame_load<W>(gl, R, X, fu + (k - 1), fu + k);
           hop_load(++hr);
           if (hmixed) next = pl[(t + 1) * PLAN_WORDS];
         } else {
-          frame_shift<TW>(gl, R, X, nf);
+          frame_shift<W>(gl, R, X, nf);
         }
       }
       ex.sync();
@@ -281,16 +275,16 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLds &lds,
     // (the per-sample fields carry nothing to the next launch; zero them so that their
     // last values are not kept alive through the time loop for this store)
 #pragma unroll
-    for (int j = 0; j < Shape<TW>::ND; ++j) R.acur[j] = R.lcur[j] = R.anx[j] = R.apv[j] = 0.0;
+    for (int j = 0; j < Shape<W>::ND; ++j) R.acur[j] = R.lcur[j] = R.anx[j] = R.apv[j] = 0.0;
     R.ac = ArmCarry{};
-    ((Lane<TW> *)a.lane_state)[(int64_t)u * TW + gl] = R;
+    ((Lane<W> *)a.lane_state)[(int64_t)u * W + gl] = R;
     double *ws = a.lds_state + (int64_t)u * X_TOTAL;
-    for (int k = gl; k < X_TOTAL; k += TW) ws[k] = X[k];
+    for (int k = gl; k < X_TOTAL; k += W) ws[k] = X[k];
   }
   if constexpr (PROF) {
     if (lane % 64 == 0)
       for (int p = 0; p < PH_COUNT; ++p)
-        prof[((int64_t)blockIdx.x * WPB + lane / 64) * PH_COUNT + p] = ex.acc[p];
+        prof[((int64_t)blockIdx.x * WPB_ + lane / 64) * PH_COUNT + p] = ex.acc[p];
   }
 }
 

@@ -50,7 +50,9 @@ class Context:
     """An afs_ctx: device + sampling rate + solver + options (TdsModel::Options)."""
 
     def __init__(self, sampling_rate_hz: float = 22050.0, solver: str = "tree", device: int = 0,
-                 async_calls: bool = False, profile: bool = False, **options):
+                 async_calls: bool = False, profile: bool = False, lanes: Optional[int] = None, **options):
+        """``lanes``: tree solver, lanes per utterance (16: the throughput kernel, 64: the voice
+        kernel); None lets the library pick per batch (AFS_LANES_16 / AFS_LANES_64, afs.h)."""
         lib = _native.load()
         cfg = _native.AfsConfig()
         lib.afs_config_default(ctypes.byref(cfg))
@@ -58,6 +60,8 @@ class Context:
         cfg.solver = SOLVERS[solver]
         cfg.device = int(device)
         cfg.flags = (_native.AFS_ASYNC if async_calls else 0) | (_native.AFS_PROFILE if profile else 0)
+        if lanes is not None:
+            cfg.flags |= {16: _native.AFS_LANES_16, 64: _native.AFS_LANES_64}[int(lanes)]
         for k, v in options.items():
             if not hasattr(cfg.options, k):
                 raise TypeError(f"unknown option {k}")
@@ -89,6 +93,10 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def lanes_per_utterance(self, batch: int) -> int:
+        """Lanes per utterance the tree solver uses for a batch of this size."""
+        return int(self._lib.afs_lanes_per_utterance(self._h, int(batch)))
 
     def set_stream(self, stream_handle: int) -> None:
         """Issue all work on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""

@@ -250,7 +250,16 @@ def measure(args, ctx, dev, stream, workload: str, B: int, first: int, world: in
             edges = sharding.edge_utterances(world, B)
             root = pcm.result((pcm.k - 1) % len(pcm.bufs))
             rows = torch.stack([root[r, j] for r, j, _ in edges]).cpu()
-            m.gather_check = sharding.check_gathered(rows, world, B, lambda us: _resynth(ctx, m, us, args))
+            # (the re-synthesis uses the kernel the shards ran: the lane width chosen for B, not for
+            # the few utterances re-synthesized)
+            from areafunctionsynthesis_amd.synthesizer import Context
+            lanes = ctx.lanes_per_utterance(B) if args.solver == "tree" else None
+            chk = Context(args.fs, solver=args.solver, device=ctx.device, lanes=lanes)
+            try:
+                m.gather_check = sharding.check_gathered(rows, world, B, lambda us: _resynth(chk, m, us, args))
+            finally:
+                chk.close()
+            m.gather_check["lanes_per_utterance"] = lanes
         dist.barrier()
     return m
 

@@ -115,13 +115,21 @@ typedef struct afs_options {
 /* Record an event pair around every kernel launch of the synthesis calls; afs_kernel_times
  * returns their summed durations (measurement only: a few microseconds per launch). */
 #define AFS_PROFILE 0x2u
+/* Tree solver, lanes per utterance.  By default the library picks per call (per session: at its
+ * creation) from the batch: the voice kernel (64 lanes, one utterance per wave, two tube sections
+ * per lane: the shortest time per sample) while the batch is no larger than the GPU's SIMD count,
+ * the throughput kernel (16 lanes, four utterances per wave, six sections per lane) above.  These
+ * flags force one of them (not both).  The two kernels evaluate the same operations per section but
+ * are separate compilations: their audio agrees within the parity tolerances, not bit for bit. */
+#define AFS_LANES_16 0x4u
+#define AFS_LANES_64 0x8u
 
 typedef struct afs_config {
   double sampling_rate_hz; /* reference: 22050 (Constants.h:22-26); any rate is accepted */
   int32_t precision;       /* afs_precision */
   int32_t solver;          /* afs_solver */
   int32_t device;          /* HIP device ordinal */
-  uint32_t flags;          /* AFS_ASYNC | AFS_PROFILE */
+  uint32_t flags;          /* AFS_ASYNC | AFS_PROFILE | AFS_LANES_16 or AFS_LANES_64 */
   afs_options options;
 } afs_config;
 
@@ -157,6 +165,9 @@ void afs_destroy(afs_ctx *ctx);
 const char *afs_last_error(const afs_ctx *ctx);
 /* Use this hipStream_t (passed as void*) for all work of the context; NULL = default stream. */
 afs_status afs_set_stream(afs_ctx *ctx, void *hip_stream);
+/* Lanes per utterance the tree solver uses for a batch of this size (AFS_LANES_*; 1 for the
+ * one-lane solvers). */
+int32_t afs_lanes_per_utterance(const afs_ctx *ctx, int32_t batch);
 afs_status afs_synchronize(afs_ctx *ctx);
 
 /* Whole trajectories.  frames[batch][num_frames], seeds[batch] (srand() seed per utterance,

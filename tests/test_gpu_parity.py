@@ -23,8 +23,11 @@ pytestmark = pytest.mark.gpu
 
 GOLD_TOL = 1e-9
 RMS_TOL = 1e-4
-TREE_SOLVERS = ("tree",)           # the cooperative kernel (K1)
+# the cooperative kernel (K1) at both lane widths: "tree16" the throughput kernel (16 lanes per
+# utterance), "tree64" the voice kernel (64 lanes per utterance); "tree" lets the library pick
+TREE_SOLVERS = ("tree16", "tree64")
 SOLVERS = ("cholesky",) + TREE_SOLVERS
+LANES = {"tree16": 16, "tree64": 64}
 
 
 @pytest.fixture(scope="module")
@@ -35,7 +38,10 @@ def contexts():
     def get(fs, solver="cholesky", **opt):
         key = (fs, solver, tuple(sorted(opt.items())))
         if key not in cache:
-            cache[key] = Context(fs, solver=solver, **opt)
+            if solver in LANES:
+                cache[key] = Context(fs, solver="tree", lanes=LANES[solver], **opt)
+            else:
+                cache[key] = Context(fs, solver=solver, **opt)
         return cache[key]
 
     yield get
@@ -98,6 +104,32 @@ def test_batch_vs_oracle_mixed(contexts, oracle, solver):
         x = oracle.utterance(frames[u], hop, int(seeds[u]), fs)
         err = np.abs(y[u] - x).max()
         assert err <= GOLD_TOL, (u, err)
+
+
+def test_lane_widths(contexts, oracle):
+    """The library picks the voice kernel (64 lanes per utterance) for batches up to the GPU's
+    SIMD count and the throughput kernel (16) above, unless forced; both widths give the oracle's
+    audio (first 2048 samples within GOLD_TOL) on a mixed batch."""
+    from areafunctionsynthesis_amd.synthesizer import Context
+    auto = Context(22050.0, solver="tree")
+    try:
+        assert auto.lanes_per_utterance(1) == 64
+        assert auto.lanes_per_utterance(1024) == 64  # (MI355X: 256 CUs x 4 SIMDs)
+        assert auto.lanes_per_utterance(1025) == 16 and auto.lanes_per_utterance(8192) == 16
+    finally:
+        auto.close()
+    assert contexts(22050.0, "tree16").lanes_per_utterance(1) == 16
+    assert contexts(22050.0, "tree64").lanes_per_utterance(8192) == 64
+    assert contexts(22050.0, "cholesky").lanes_per_utterance(8) == 1
+    frames = np.stack([static_frames(oracle, n, 6, velum=v) for n, v in (("a:", 0.0), ("s", 1.0), ("(a)d(a):", 0.3))])
+    seeds = np.array([2, 3, 4], np.uint32)
+    y16 = contexts(22050.0, "tree16").synthesize(frames, 410, seeds=seeds)
+    y64 = contexts(22050.0, "tree64").synthesize(frames, 410, seeds=seeds)
+    for u in range(3):
+        x = oracle.utterance(frames[u], 410, int(seeds[u]), 22050.0)
+        assert np.abs(y16[u, :2048] - x[:2048]).max() <= GOLD_TOL
+        assert np.abs(y64[u, :2048] - x[:2048]).max() <= GOLD_TOL
+    assert np.abs(y16 - y64).max() <= 1e-8
 
 
 @pytest.mark.parametrize("solver", SOLVERS)
@@ -266,7 +298,7 @@ def _full_length_check(ctx, w, frames, stride, parity_report, label, solver):
     rms = np.sqrt(np.mean(err ** 2, axis=1))
     mx = np.abs(err).max(axis=1)
     flips = None
-    if solver in TREE_SOLVERS:
+    if solver in TREE_SOLVERS or solver == "tree":
         gd = ctx.rng_draws(B)[idx]
         flips = int(np.count_nonzero(gd != draws))
     parity_report.append(

@@ -55,10 +55,10 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   CK(hipMemcpy(ds, seeds, 4 * B, hipMemcpyHostToDevice));
   CK(hipMalloc(&dout, sizeof(double) * (size_t)B * (F - 1) * hop));
   CK(hipMalloc(&dlds, sizeof(double) * (size_t)B * tree_lds_doubles()));
-  CK(hipMalloc(&dlanes, (size_t)B * TW * tree_lane_bytes()));
+  CK(hipMalloc(&dlanes, (size_t)B * TW * tree_lane_bytes(TW)));
   CK(hipMalloc(&dprof, sizeof(uint64_t) * waves * PH_COUNT));
   CK(hipMalloc(&dp25, sizeof(double) * (size_t)B * (F - 1) * hop));
-  CK(launch_tree_reset(dlanes, dlds, B, ds, nullptr));
+  CK(launch_tree_reset(dlanes, dlds, B, ds, TW, nullptr));
   const int64_t T = (int64_t)(F - 1) * hop;
   uint64_t *dplan;
   CK(hipMalloc(&dplan, (size_t)B * T * PLAN_RECORD_BYTES));
