@@ -34,7 +34,9 @@ def test_kernel_times_count_every_launch(oracle):
     kt = ctx.kernel_times()
     assert kt["synth_launches"] >= 1 and kt["synth_ms"] > 0.0
     assert kt["plan_launches"] == kt["synth_launches"]  # one noise-source plan per tree launch
-    assert ctx.kernel_times() == {"synth_ms": 0.0, "synth_launches": 0, "plan_ms": 0.0, "plan_launches": 0}
+    assert kt["output_launches"] == kt["synth_launches"] and kt["output_ms"] > 0.0  # K6 after every K1
+    assert ctx.kernel_times() == {"synth_ms": 0.0, "synth_launches": 0, "plan_ms": 0.0, "plan_launches": 0,
+                                  "output_ms": 0.0, "output_launches": 0}
     ctx.close()
     plain = Context(44100.0)
     with pytest.raises(Exception):
@@ -54,6 +56,9 @@ def test_comm_gather_one_rank():
     comm.fence()
     comm.synchronize()
     assert torch.equal(root, x)
+    t = comm.gather_times()  # (afs_comm_gather_times: events on the comm's stream)
+    assert t["gathers"] == 1 and t["gather_ms"] >= 0.0
+    assert comm.gather_times() == {"gather_ms": 0.0, "gathers": 0}
     comm.close()
     ctx.close()
 
