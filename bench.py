@@ -381,6 +381,9 @@ def main() -> None:
                          "playTargetSequence (per-sample tubes, hop 1)")
     ap.add_argument("--no-sub-configs", action="store_true",
                     help="skip the config-5 / config-3 sub-objects (one GPU, default workload only)")
+    ap.add_argument("--lanes", type=int, choices=(16, 64), default=None,
+                    help="tree solver: force 16 (throughput kernel) or 64 (voice kernel) lanes per utterance; "
+                         "default: the library's choice for the batch")
     ap.add_argument("--sub-steps", type=int, default=2)
     ap.add_argument("--sub-cpu-utterances", type=int, default=16)
     args = ap.parse_args()
@@ -403,7 +406,7 @@ def main() -> None:
 
     digest = kernel_digest()
     B = args.batch
-    ctx = Context(args.fs, solver=args.solver, device=local, async_calls=True, profile=True)
+    ctx = Context(args.fs, solver=args.solver, device=local, async_calls=True, profile=True, lanes=args.lanes)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     first, _ = sharding.shard_range(rank, world, B)
@@ -443,6 +446,7 @@ def main() -> None:
                 "fs_hz": args.fs,
                 "hop": m.hop,
                 "solver": args.solver,
+                "lanes_per_utterance": ctx.lanes_per_utterance(B),
                 "kernel_sources": digest,
                 "parallelism": f"dp{world} (utterance shards; int16 audio gathered to rank 0 by afs_gather_pcm over "
                                "RCCL, overlapped with the next step)" if world > 1 else "dp1",
