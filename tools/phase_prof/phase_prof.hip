@@ -11,9 +11,16 @@
 using namespace afs;
 using namespace afs::tree;
 
-__global__ void __launch_bounds__(64 * WPB, AFS_TREE_MIN_WAVES) tree_prof_kernel(TreeArgs a, uint64_t *prof) {
-  __shared__ WaveLds lds;
-  tree_synth_body<true, AFS_GLOTTIS_TRIANGULAR>(a, lds, prof);  // (the profiler runs the default glottis)
+// lanes per utterance of the profiled kernel (-DPP_W=64: the voice kernel)
+#ifndef PP_W
+#define PP_W TREE_W
+#endif
+constexpr int PW = PP_W;
+constexpr int PWPB = Geom<PW>::WPB, PUPB = Geom<PW>::UPB;
+
+__global__ void __launch_bounds__(64 * PWPB, AFS_TREE_MIN_WAVES) tree_prof_kernel(TreeArgs a, uint64_t *prof) {
+  __shared__ WaveLdsT<PW> lds;
+  tree_synth_body<true, AFS_GLOTTIS_TRIANGULAR, false, PW>(a, lds, prof);  // (the profiler runs the default glottis)
 }
 
 #define CK(x)                                                                  \
@@ -29,7 +36,7 @@ extern "C" int pp_phase_count() { return PH_COUNT; }
 
 // frames[B][F] host; cycles[PH_COUNT] = sum over waves; returns kernel ms in *ms.
 static std::vector<uint64_t> g_wave;  // per-wave cycle totals of the last pp_run
-extern "C" int pp_waves_per_block() { return WPB; }
+extern "C" int pp_waves_per_block() { return PWPB; }
 extern "C" void pp_wave_totals(uint64_t *out) {
   for (size_t w = 0; w < g_wave.size(); ++w) out[w] = g_wave[w];
 }
@@ -46,7 +53,7 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   void *dlanes;
   uint64_t *dprof;
   double *dp25;  // section 25's pressures (K6's tone input; the kernel stores them every sample)
-  const int blocks = (B + UPB - 1) / UPB, waves = blocks * WPB;
+  const int blocks = (B + PUPB - 1) / PUPB, waves = blocks * PWPB;
   CK(hipMalloc(&dt, sizeof(Tables)));
   CK(hipMemcpy(dt, ht, sizeof(Tables), hipMemcpyHostToDevice));
   CK(hipMalloc(&df, sizeof(afs_frame) * B * F));
@@ -55,10 +62,10 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   CK(hipMemcpy(ds, seeds, 4 * B, hipMemcpyHostToDevice));
   CK(hipMalloc(&dout, sizeof(double) * (size_t)B * (F - 1) * hop));
   CK(hipMalloc(&dlds, sizeof(double) * (size_t)B * tree_lds_doubles()));
-  CK(hipMalloc(&dlanes, (size_t)B * TW * tree_lane_bytes(TW)));
+  CK(hipMalloc(&dlanes, (size_t)B * PW * tree_lane_bytes(PW)));
   CK(hipMalloc(&dprof, sizeof(uint64_t) * waves * PH_COUNT));
   CK(hipMalloc(&dp25, sizeof(double) * (size_t)B * (F - 1) * hop));
-  CK(launch_tree_reset(dlanes, dlds, B, ds, TW, nullptr));
+  CK(launch_tree_reset(dlanes, dlds, B, ds, PW, nullptr));
   const int64_t T = (int64_t)(F - 1) * hop;
   uint64_t *dplan;
   CK(hipMalloc(&dplan, (size_t)B * T * PLAN_RECORD_BYTES));
@@ -69,7 +76,7 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0, nullptr));
-  hipLaunchKernelGGL(tree_prof_kernel, dim3(blocks), dim3(64 * WPB), 0, nullptr, a, dprof);
+  hipLaunchKernelGGL(tree_prof_kernel, dim3(blocks), dim3(64 * PWPB), 0, nullptr, a, dprof);
   CK(hipGetLastError());
   CK(hipEventRecord(e1, nullptr));
   CK(hipEventSynchronize(e1));
