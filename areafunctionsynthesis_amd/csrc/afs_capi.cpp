@@ -149,8 +149,18 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       hbuf[0] = (afs::tree::PlanHop *)c->hops[0];
       hbuf[1] = (afs::tree::PlanHop *)c->hops[ov ? 1 : 0];
     }
-    // K6's glottal-tone input: section 25's pressure per sample of the launch
-    if ((st = ensure(c, &c->p25, &c->p25_bytes, (size_t)B * (size_t)per * sizeof(double))) != AFS_OK) return st;
+    // K6's glottal-tone input: section 25's pressure per sample of the launch.  Laid out so that
+    // every utterance's row sits at the same position in its 128-byte lines as its output row
+    // (stride and base congruent to the output's modulo 16 doubles): K1 stores both through one
+    // line-aligned window (tree_kernel.h).
+    const int64_t p25_stride = per + ((ostride - per) % 16 + 16) % 16;
+    if ((st = ensure(c, &c->p25, &c->p25_bytes, ((size_t)B * (size_t)p25_stride + 32) * sizeof(double))) != AFS_OK)
+      return st;
+    auto p25_row0 = [&](int64_t s0) {  // the p25 base for the launch whose outputs start at out + s0
+      const int64_t want = (int64_t)((reinterpret_cast<uintptr_t>(out + s0) >> 3) & 15);
+      const int64_t have = (int64_t)((reinterpret_cast<uintptr_t>(c->p25) >> 3) & 15);
+      return (double *)c->p25 + ((want - have) % 16 + 16) % 16;
+    };
     hipStream_t ps = ov ? c->plan_stream : c->stream;
     const int two = c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0;
     const afs::SecRec *uo = c->dev_tab->consts.sec;
@@ -182,14 +192,14 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
                       (const uint64_t *)buf[k & 1], per, lanes, (double *)ws, B, c->host_tab.uni,
-                      hbuf[k & 1], hstride, (double *)c->p25, per};
+                      hbuf[k & 1], hstride, p25_row0(s0), p25_stride};
       hipEvent_t e1 = prof_event(c);
       HIP_TRY(c, afs::launch_tree_synth(a, width, c->stream));
       hipEvent_t e2 = prof_event(c);
       prof_pair(c, e1, e2, 0);
       // K6: the glottal-tone filter and the output stage of the launch's samples
       HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B,
-                                         (const double *)c->p25, per, c->cfg.options.radiation_from_skin, c->stream));
+                                         p25_row0(s0), p25_stride, c->cfg.options.radiation_from_skin, c->stream));
       prof_pair(c, e2, prof_event(c), 2);
       if (ov) HIP_TRY(c, hipEventRecord(c->ev_free[k & 1], c->stream));
     }

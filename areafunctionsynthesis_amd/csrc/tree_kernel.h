@@ -234,12 +234,12 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
   // the old right one (frame_shift).
   NextFrame<W> nf{};
   // The per-sample outputs (the radiated flow: every lane has it; section 25's pressure: lane 2)
-  // go to LDS windows of 16 samples aligned to the 128-byte lines of o and p25o, and lanes 0-15
-  // store a window as one whole line when its last sample is written (or the launch ends): one
-  // coalesced store per line instead of 16 single 8-byte stores, which the memory system wrote
-  // back as partial lines (2x the stored bytes, profiles/pmc_traffic.json r03aj).
+  // go to an LDS window of the 16 samples of one 128-byte line of o -- p25o sits at the same
+  // position in its lines (afs_capi.cpp lays it out so) -- and lanes 0-15 store the window as one
+  // whole line of each array when its last sample is written (or the launch ends): one coalesced
+  // store per line instead of 16 single 8-byte stores, which the memory system wrote back as
+  // partial lines (2x the stored bytes, profiles/pmc_traffic.json r03aj).
   const int o_line = (int)((reinterpret_cast<uintptr_t>(o) >> 3) & 15);
-  const int p_line = (int)((reinterpret_cast<uintptr_t>(p25o) >> 3) & 15);
   ex.sync();
   uint64_t next = hmixed ? pl[0] : 0;
   for (int64_t t = 0; t < n; ++t) {
@@ -259,16 +259,23 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
       if (i + 1 == hop && t + 1 < n) nf.load(gl, fu + k + 1);
     }
     sample_step<W, MODEL>(ex, X, a.uni, C, ratio, true);
+#if defined(AFS_AB_DIRECT_STORE)  // (temporary A/B: the round-3 single-lane 8-byte stores)
+    if (valid && gl == 0) o[t] = R.sample;
+    if (valid && gl == 2) p25o[t] = R.p[0];
+    (void)o_line;
+#else
     {
-      const int jo = (int)((o_line + t) & 15), jp = (int)((p_line + t) & 15);
-      X[X_OWIN + jo] = R.sample;                    // (the same value from every lane)
+      const int j = (o_line + (int)t) & 15;
+      X[X_OWIN + j] = R.sample;                 // (the same value from every lane)
       // section 25's new pressure (lane 2's slot 0), the glottal-tone filter's input in K6
-      if (gl == 2) X[X_PWIN + jp] = R.p[0];
-      const bool last = t + 1 == n;
-      // lane gl stores window entry gl: sample t - j + gl, if it belongs to this launch
-      if (valid && (jo == 15 || last) && gl <= jo && t - jo + gl >= 0) o[t - jo + gl] = X[X_OWIN + gl];
-      if (valid && (jp == 15 || last) && gl <= jp && t - jp + gl >= 0) p25o[t - jp + gl] = X[X_PWIN + gl];
+      if (gl == 2) X[X_PWIN + j] = R.p[0];
+      // lane gl stores window entry gl, sample t - j + gl, if it belongs to this launch
+      if (valid && (j == 15 || t + 1 == n) && gl <= j && t - j + gl >= 0) {
+        o[t - j + gl] = X[X_OWIN + gl];
+        p25o[t - j + gl] = X[X_PWIN + gl];
+      }
     }
+#endif
     if (++i == hop) {
       i = 0;
       ++k;
