@@ -1707,11 +1707,13 @@ AFS_HD inline double output_filter_one(double *X, const Consts &C, double flow) 
 }
 
 // o[0..n) holds the radiated flows of n consecutive samples; they are replaced by the audio
-// samples.  The filter state stays in registers over the run; the loads of the next 8 samples
-// are issued before the current 8 are filtered (their latency hides behind the filter chain).
-// (A 16-entry window moved once per 8-sample block instead of the per-sample shift -- the same
-// operations, 16 instead of 128 register moves per block -- measured 2 % slower end to end: the
-// window's 64 registers push persistent state into AGPRs, profiles/r03w_ab.txt.)
+// samples.  The filter state stays in registers over the run.  Whole blocks of 8 samples keep the
+// filters' histories in windows (x and y of the last 8 + the block's 8 samples, oldest first), so
+// that sample i of a block reads its taps at fixed window positions and the window moves once per
+// block (8 moves instead of 56 per block and filter); the loads of the next block are issued before
+// the current one is filtered (clamped indices: no branch), and the last n % 8 samples run one by
+// one.  (In K1, where the filter ran until round 3, the windows' registers pushed persistent state
+// into AGPRs: -2 %, profiles/r03w_ab.txt; K6 has the registers to spare.)
 // TONE: first the glottal-tone filter (skin radiation, TdsModel.cpp:687-705) over p25[i], section
 // 25's new pressure of sample i, its output added to the flow o[i] (the same operations as
 // phase_output, so bitwise the same audio): one loop, so that the tone chain of sample i + 1 and
@@ -1723,82 +1725,97 @@ AFS_HD inline void output_filter_run_t(double *X, const Consts &C, double *o, in
   // trajectory bit for bit; with contraction the compiler may pair the terms differently in
   // different unrolled positions)
 #pragma clang fp contract(off)
-  double sx[8], sy[8], ca[9], cb[9];
+  double wx[16], wy[16], ca[9], cb[9];  // wx[7 - k] = x_{t-1-k} at a block's start (wx[7]: newest)
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { sx[k] = X[X_OUTF + k]; sy[k] = X[X_OUTF + 8 + k]; }
+  for (int k = 0; k < 8; ++k) { wx[7 - k] = X[X_OUTF + k]; wy[7 - k] = X[X_OUTF + 8 + k]; }
 #pragma unroll
   for (int k = 0; k <= 8; ++k) { ca[k] = C.h.out_a[k]; cb[k] = C.h.out_b[k]; }
   const double inv_dt = C.h.inv_dt;
   double prev = X[X_PREVFLOW];
   bool nonfin = false;
-  double tx[4], ty[4], ta[5], tb[5];
+  double tx[12], ty[12], ta[5], tb[5];  // tone filter windows: tx[3 - k] = x_{t-1-k}
   if constexpr (TONE) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { tx[k] = X[X_TONE + k]; ty[k] = X[X_TONE + 4 + k]; }
+    for (int k = 0; k < 4; ++k) { tx[3 - k] = X[X_TONE + k]; ty[3 - k] = X[X_TONE + 4 + k]; }
 #pragma unroll
     for (int k = 0; k <= 4; ++k) { ta[k] = C.h.tone_a[k]; tb[k] = C.h.tone_b[k]; }
   }
+  // one sample with its taps at window offset b (sample i of a block: b = i)
+  auto step = [&](int b, double flow, double xp) -> double {
+    if constexpr (TONE) {
+      double tacc = ta[0] * xp;
+#pragma unroll
+      for (int k = 1; k <= 4; ++k) {
+        tacc += ta[k] * tx[4 + b - k];
+        tacc += tb[k] * ty[4 + b - k];
+      }
+      tx[4 + b] = xp;
+      ty[4 + b] = tacc;
+      flow += tacc;
+    }
+    const double op = (flow - prev) * inv_dt;
+    prev = flow;
+    double acc = ca[0] * op;
+#pragma unroll
+    for (int k = 1; k <= 8; ++k) {
+      acc += ca[k] * wx[8 + b - k];
+      acc += cb[k] * wy[8 + b - k];
+    }
+    wx[8 + b] = op;
+    wy[8 + b] = acc;
+    double smp = acc * 0.004;
+    smp = smp * (1.0 / 32767);
+    nonfin = nonfin || !isfinite(smp);
+    return smp;
+  };
+  auto shift = [&](int m) {  // the window after m samples: drop the m oldest entries
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (j + m < 16) { wx[j] = wx[j + m]; wy[j] = wy[j + m]; }
+    }
+    if constexpr (TONE) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j + m < 12) { tx[j] = tx[j + m]; ty[j] = ty[j + m]; }
+      }
+    }
+  };
+  const int nb = n / 8 * 8;
   double f[8], fp[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    f[i] = (i < n) ? o[i] : 0.0;
-    if constexpr (TONE) fp[i] = (i < n) ? p25[i] : 0.0;
+    const int q = i < n ? i : (n > 0 ? n - 1 : 0);
+    f[i] = n > 0 ? o[q] : 0.0;
+    fp[i] = (TONE && n > 0) ? p25[q] : 0.0;
   }
-  for (int t0 = 0; t0 < n; t0 += 8) {
+  for (int t0 = 0; t0 < nb; t0 += 8) {
     double g[8], gp[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      g[i] = (t0 + 8 + i < n) ? o[t0 + 8 + i] : 0.0;
-      if constexpr (TONE) gp[i] = (t0 + 8 + i < n) ? p25[t0 + 8 + i] : 0.0;
+    for (int i = 0; i < 8; ++i) {  // (the next block's inputs; indices clamped into the run)
+      const int q = t0 + 8 + i < n ? t0 + 8 + i : n - 1;
+      g[i] = o[q];
+      gp[i] = TONE ? p25[q] : 0.0;
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (t0 + i >= n) break;
-      double flow = f[i];
-      if constexpr (TONE) {
-        const double x = fp[i];
-        double tacc = ta[0] * x;
-#pragma unroll
-        for (int k = 1; k <= 4; ++k) {
-          tacc += ta[k] * tx[k - 1];
-          tacc += tb[k] * ty[k - 1];
-        }
-#pragma unroll
-        for (int k = 3; k > 0; --k) { tx[k] = tx[k - 1]; ty[k] = ty[k - 1]; }
-        tx[0] = x;
-        ty[0] = tacc;
-        flow += tacc;
-      }
-      const double op = (flow - prev) * inv_dt;
-      prev = flow;
-      double acc = ca[0] * op;
-#pragma unroll
-      for (int k = 1; k <= 8; ++k) {
-        acc += ca[k] * sx[k - 1];
-        acc += cb[k] * sy[k - 1];
-      }
-#pragma unroll
-      for (int k = 7; k > 0; --k) { sx[k] = sx[k - 1]; sy[k] = sy[k - 1]; }
-      sx[0] = op;
-      sy[0] = acc;
-      double smp = acc * 0.004;
-      smp = smp * (1.0 / 32767);
-      nonfin = nonfin || !isfinite(smp);
-      o[t0 + i] = smp;
-    }
+    for (int i = 0; i < 8; ++i) o[t0 + i] = step(i, f[i], fp[i]);
+    shift(8);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       f[i] = g[i];
-      if constexpr (TONE) fp[i] = gp[i];
+      fp[i] = gp[i];
     }
   }
+  for (int t = nb; t < n; ++t) {  // the last n % 8 samples
+    o[t] = step(0, o[t], TONE ? p25[t] : 0.0);
+    shift(1);
+  }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { X[X_OUTF + k] = sx[k]; X[X_OUTF + 8 + k] = sy[k]; }
+  for (int k = 0; k < 8; ++k) { X[X_OUTF + k] = wx[7 - k]; X[X_OUTF + 8 + k] = wy[7 - k]; }
   X[X_PREVFLOW] = prev;
   if (nonfin) X[X_NONFIN] = 1.0;
   if constexpr (TONE) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { X[X_TONE + k] = tx[k]; X[X_TONE + 4 + k] = ty[k]; }
+    for (int k = 0; k < 4; ++k) { X[X_TONE + k] = tx[3 - k]; X[X_TONE + 4 + k] = ty[3 - k]; }
   }
 }
 
