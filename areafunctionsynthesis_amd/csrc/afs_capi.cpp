@@ -115,9 +115,36 @@ void prof_pair(afs_ctx *c, hipEvent_t a, hipEvent_t b, int kind) {
   if (a && b) c->timed.push_back({a, b, kind});
 }
 
+// Slot order of the tree kernel for utterances that share trajectories (row[u]: the utterance's
+// frame row): the utterances sorted by row, and the sorted list cut into contiguous chunks so that
+// the blocks one XCD runs at the same time play as few rows as possible -- each of the 8 XCDs has
+// its own L2, and blocks are dealt to them round-robin (block b shares an XCD with b + 8,
+// MI355X_MICROARCH.md, workgroup dispatch), in rounds of `conc` blocks (the blocks the GPU holds
+// at once).  Entry (block * upb + g) = the utterance of that slot, B for padding slots.
+std::vector<int32_t> xcd_order(const std::vector<int32_t> &row, int B, int upb, int conc) {
+  constexpr int XCDS = 8;
+  std::vector<int32_t> idx((size_t)B);
+  for (int u = 0; u < B; ++u) idx[(size_t)u] = u;
+  std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) { return row[(size_t)a] < row[(size_t)b]; });
+  const int nb = (B + upb - 1) / upb;
+  conc = std::max(conc, 1);
+  std::vector<int32_t> order((size_t)nb * (size_t)upb, B);
+  for (int r0 = 0; r0 < nb; r0 += conc) {  // one round: blocks r0 .. r0 + nr - 1
+    const int nr = std::min(conc, nb - r0);
+    int chunk = r0;  // (the sorted chunks of this round, XCD by XCD)
+    for (int x = 0; x < XCDS; ++x)
+      for (int b = r0 + x; b < r0 + nr; b += XCDS, ++chunk)
+        for (int g = 0; g < upb; ++g) {
+          const int64_t q = (int64_t)chunk * upb + g;
+          if (q < B) order[(size_t)b * upb + g] = idx[(size_t)q];
+        }
+  }
+  return order;
+}
+
 afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int rows, int ntrans, int hop,
                       double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B,
-                      int width, const int32_t *frame_row = nullptr) {
+                      int width, const int32_t *frame_row = nullptr, const int32_t *order = nullptr) {
   if (tree(c)) {
     // Launch chunks of `per` samples: K5 (the chunk's noise-source plans), then K1.  With
     // AFS_PLAN_OVERLAP=1 in the environment (afs_ctx::overlap), K5 of chunk k + 1 runs on the
@@ -192,7 +219,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
                       (const uint64_t *)buf[k & 1], per, lanes, (double *)ws, B, c->host_tab.uni,
-                      hbuf[k & 1], hstride, p25_row0(s0), p25_stride};
+                      hbuf[k & 1], hstride, p25_row0(s0), p25_stride, order};
       hipEvent_t e1 = prof_event(c);
       HIP_TRY(c, afs::launch_tree_synth(a, width, c->stream));
       hipEvent_t e2 = prof_event(c);
@@ -903,12 +930,25 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
     plan.hold_j = j;
   }
   afs_status s;
+  const int width = lanes_for(c, B);
+  // tree solver: the XCD-aware slot order of the utterances by trajectory (xcd_order)
+  std::vector<int32_t> order;
+  if (tree(c)) {
+    const int upb = width == afs::TREE_VOICE_W ? 1 : 4 * afs::TREE_WPB;
+    // blocks the GPU holds at once: the voice kernel one wave (block) per SIMD, the throughput
+    // kernel one block per CU (its LDS)
+    const int conc = width == afs::TREE_VOICE_W ? c->simds : c->simds / 4;
+    order = xcd_order(row, B, upb, conc);
+  }
   const size_t seq_bytes = seq.size() * sizeof(double);
-  if ((s = ensure(c, &c->tgt, &c->tgt_bytes, seq_bytes + (size_t)B * sizeof(int32_t))) != AFS_OK) return s;
+  const size_t row_bytes = (size_t)B * sizeof(int32_t), ord_bytes = order.size() * sizeof(int32_t);
+  if ((s = ensure(c, &c->tgt, &c->tgt_bytes, seq_bytes + row_bytes + ord_bytes)) != AFS_OK) return s;
   double *dseq = (double *)c->tgt;
   int32_t *drow = (int32_t *)((char *)c->tgt + seq_bytes);
+  int32_t *dord = order.empty() ? nullptr : (int32_t *)((char *)c->tgt + seq_bytes + row_bytes);
   HIP_TRY(c, hipMemcpyAsync(dseq, seq.data(), seq_bytes, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(drow, row.data(), (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(drow, row.data(), row_bytes, hipMemcpyHostToDevice, c->stream));
+  if (dord) HIP_TRY(c, hipMemcpyAsync(dord, order.data(), ord_bytes, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));  // the host vectors die with this call
   const uint32_t *dseeds = seeds;
   if (seeds && !is_device_ptr(seeds)) {
@@ -923,7 +963,6 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
     dout = (double *)c->stage_out;
   }
   const int64_t bp = pad64(B);
-  const int width = lanes_for(c, B);
   if ((s = ensure(c, &c->ws, &c->ws_bytes, ws_bytes_for(c, bp))) != AFS_OK) return s;
   if ((s = ensure(c, (void **)&c->rng, &c->rng_bytes, (size_t)(32 * bp) * sizeof(int32_t))) != AFS_OK) return s;
   if (tree(c) && (s = ensure(c, &c->tree_lanes, &c->tree_lanes_bytes, lanes_bytes_for(c, bp, width))) != AFS_OK)
@@ -941,7 +980,7 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
     const int nk = (int)std::min<int64_t>(Tc, T - k0);
     HIP_TRY(c, afs::launch_target_frames(dseq, Q, plan, k0, nk + 1, Tc + 1, dframes, c->stream));
     if ((s = run_chunks(c, dframes, Tc + 1, Q, nk, 1, dout + k0, T, c->ws, c->rng, c->tree_lanes, bp, B, width,
-                        drow)) != AFS_OK)
+                        drow, dord)) != AFS_OK)
       return s;
   }
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));

@@ -33,6 +33,10 @@ struct TreeArgs {
   // section 25's pressure per sample (p25[u * p25_stride + s - s_begin]), K6's glottal-tone input
   double *p25 = nullptr;
   int64_t p25_stride = 0;
+  // utterance of slot block * (utterances per block) + g, or the identity when null (entries >= B:
+  // padding slots); shared trajectories (frame_row) order the utterances by row so that the blocks
+  // one XCD runs at a time play few rows (afs_capi.cpp xcd_order)
+  const int32_t *order = nullptr;
 };
 // K5: the noise-source plans of samples [s_begin, s_end) of `rows` frame rows.
 struct PlanArgs {

@@ -184,7 +184,8 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
   constexpr int UPB_ = Geom<W>::UPB, WPB_ = Geom<W>::WPB;
   const int lane = threadIdx.x;  // 0 .. 64 WPB - 1
   const int g = lane / W, gl = lane % W;
-  const int u = blockIdx.x * UPB_ + g;
+  const int slot = blockIdx.x * UPB_ + g;
+  const int u = a.order ? a.order[slot] : slot;
   const bool valid = u < a.B;
   const int ue = valid ? u : 0;
   double *X = lds.X[g];
@@ -240,6 +241,9 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
   // store per line instead of 16 single 8-byte stores, which the memory system wrote back as
   // partial lines (2x the stored bytes, profiles/pmc_traffic.json r03aj).
   const int o_line = (int)((reinterpret_cast<uintptr_t>(o) >> 3) & 15);
+#if defined(AFS_AB_REG_WINDOW)
+  double wo = 0.0, wp = 0.0;
+#endif
   ex.sync();
   uint64_t next = hmixed ? pl[0] : 0;
   for (int64_t t = 0; t < n; ++t) {
@@ -259,7 +263,21 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
       if (i + 1 == hop && t + 1 < n) nf.load(gl, fu + k + 1);
     }
     sample_step<W, MODEL>(ex, X, a.uni, C, ratio, true);
-#if defined(AFS_AB_DIRECT_STORE)  // (temporary A/B: the round-3 single-lane 8-byte stores)
+#if defined(AFS_AB_REG_WINDOW)  // (temporary A/B: the window in registers: lane gl keeps entry gl)
+    {
+      const int j = (o_line + (int)t) & 15;
+      const uint64_t pb = __builtin_bit_cast(uint64_t, R.p[0]);  // lane 2's p[25] to the row
+      const double p25v = __builtin_bit_cast(double, ((uint64_t)(uint32_t)AFS_DPP((int)(uint32_t)(pb >> 32), 0x152, 0xF, 0xF, false) << 32) |
+                                                         (uint32_t)AFS_DPP((int)(uint32_t)pb, 0x152, 0xF, 0xF, false));
+      const bool mine = gl == j;
+      wo = mine ? R.sample : wo;
+      wp = mine ? p25v : wp;
+      if (valid && (j == 15 || t + 1 == n) && gl <= j && t - j + gl >= 0) {
+        o[t - j + gl] = wo;
+        p25o[t - j + gl] = wp;
+      }
+    }
+#elif defined(AFS_AB_DIRECT_STORE)  // (temporary A/B: the round-3 single-lane 8-byte stores)
     if (valid && gl == 0) o[t] = R.sample;
     if (valid && gl == 2) p25o[t] = R.p[0];
     (void)o_line;
