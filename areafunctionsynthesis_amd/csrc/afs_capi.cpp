@@ -368,6 +368,7 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return bail(AFS_ERR_HIP);
   if (const char *e = std::getenv("AFS_PLAN_OVERLAP")) ctx->overlap = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_PLAN_DENSE")) ctx->plan_dense = std::atoi(e) != 0;
+  if (const char *e = std::getenv("AFS_XCD_ORDER")) ctx->xcd_order = std::atoi(e) != 0;
   if (hipStreamCreateWithFlags(&ctx->plan_stream, hipStreamNonBlocking) != hipSuccess) return bail(AFS_ERR_HIP);
   for (hipEvent_t *e : {&ctx->ev_go, &ctx->ev_plan[0], &ctx->ev_plan[1], &ctx->ev_free[0], &ctx->ev_free[1]})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return bail(AFS_ERR_HIP);
@@ -933,7 +934,7 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
   const int width = lanes_for(c, B);
   // tree solver: the XCD-aware slot order of the utterances by trajectory (xcd_order)
   std::vector<int32_t> order;
-  if (tree(c)) {
+  if (tree(c) && c->xcd_order) {
     const int upb = width == afs::TREE_VOICE_W ? 1 : 4 * afs::TREE_WPB;
     // blocks the GPU holds at once: the voice kernel one wave (block) per SIMD, the throughput
     // kernel one block per CU (its LDS)

@@ -72,6 +72,30 @@ class TorchTransport:
             self.fence(slot)
 
 
+class StagedTorchTransport:
+    """Test transport for bench.py's multi-process path on one GPU (``--gather-transport gloo``):
+    each rank's int16 block goes through torch.distributed (gloo) on the host and lands in rank 0's
+    device root buffer.  It exercises every step of the path except RCCL itself (which
+    :class:`CommTransport` drives and tests/test_multi_gpu.py covers with one rank)."""
+
+    def __init__(self, dist, world: int, rank: int):
+        self.dist, self.world, self.rank = dist, world, rank
+
+    def gather(self, slot, local, root):
+        import torch
+        cpu = local.detach().to("cpu").contiguous().view(-1).view(torch.uint8)
+        recv = [torch.empty_like(cpu) for _ in range(self.world)] if self.rank == 0 else None
+        self.dist.gather(cpu, gather_list=recv, dst=0)
+        if self.rank == 0:
+            root.view(-1).view(torch.uint8).copy_(torch.cat(recv).to(root.device))
+
+    def fence(self, slot):
+        pass
+
+    def drain(self):
+        pass
+
+
 class PcmGather:
     """int16 audio of each step gathered to rank 0 while the next step synthesizes.
 

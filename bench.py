@@ -200,7 +200,12 @@ def measure(args, ctx, dev, stream, workload: str, B: int, first: int, world: in
 
     # the reference's output format (int16, Synthesizer.cpp:955-973) is produced on the GPU and
     # gathered to rank 0 by the library's RCCL gather while the next step synthesizes
-    transport = sharding.CommTransport(comm) if comm is not None else _NoGather()
+    if comm is not None:
+        transport = sharding.CommTransport(comm)
+    elif world > 1:  # (--gather-transport gloo: the test transport, tests/test_multi_gpu.py)
+        transport = sharding.StagedTorchTransport(dist, world, rank)
+    else:
+        transport = _NoGather()
     pcm = sharding.PcmGather(lambda x, o: ctx.to_int16(x, out=o), (B, m.T), world, rank, transport, device=dev)
 
     for _ in range(warmup):
@@ -236,12 +241,13 @@ def measure(args, ctx, dev, stream, workload: str, B: int, first: int, world: in
     m.multi = None
     if world > 1:
         # the slowest rank's kernel and gather times (HIP events; the gathers on the comm's stream)
-        gt = comm.gather_times()
+        gt = comm.gather_times() if comm is not None else {"gather_ms": 0.0, "gathers": 0}
         launches = max(1, m.kt["synth_launches"])
         mx = torch.tensor([m.kt["synth_ms"] / launches, gt["gather_ms"] / steps], dtype=torch.float64)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         m.multi = {"avg_launch_ms_max_over_ranks": float(mx[0]), "gather_ms_per_step_max_over_ranks": float(mx[1]),
                    "gathers_per_step_rank0": gt["gathers"] / steps,
+                   "transport": "rccl (afs_gather_pcm)" if comm is not None else "gloo via the host (test transport)",
                    "gather_timing": "HIP events on the comm's stream around each afs_gather_pcm "
                                     "(afs_comm_gather_times); the gather overlaps the next step's synthesis"}
         # self-check of the exchange: rank 0 compares the int16 rows it received (the last step's
@@ -385,6 +391,10 @@ def main() -> None:
                     help="tree solver: force 16 (throughput kernel) or 64 (voice kernel) lanes per utterance; "
                          "default: the library's choice for the batch")
     ap.add_argument("--sub-steps", type=int, default=2)
+    ap.add_argument("--gather-transport", choices=("rccl", "gloo"), default="rccl",
+                    help="N > 1: rccl (the library's afs_gather_pcm; default) or gloo through the host (test only)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="N > 1: every rank on device 0 (test of the multi-process path on a one-GPU box)")
     ap.add_argument("--sub-cpu-utterances", type=int, default=16)
     args = ap.parse_args()
 
@@ -397,6 +407,8 @@ def main() -> None:
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.one_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -411,7 +423,7 @@ def main() -> None:
     ctx.set_stream(stream.cuda_stream)
     first, _ = sharding.shard_range(rank, world, B)
     comm = None
-    if world > 1:
+    if world > 1 and args.gather_transport == "rccl":
         uid = [comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = Comm(ctx, uid[0], rank, world)
