@@ -81,3 +81,35 @@ def test_multi_synthesize_equals_single_device(oracle):
     assert np.array_equal(node.synthesize(frames, hop, seeds=seeds), ctx.to_int16(ctx.synthesize(frames, hop, seeds=seeds)))
     node.close()
     ctx.close()
+
+
+def test_bench_world2_gather_check_one_device():
+    """bench.py's multi-process path end to end at world size 2 (torch.distributed.run, both ranks
+    on this box's one GPU, the int16 blocks through gloo instead of RCCL): shards, the max-over-ranks
+    timing, and the self-check of the exchange -- rank 0 re-synthesizes the first and last utterance
+    of both blocks alone and finds the gathered rows bit for bit equal."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--batch", "24", "--seconds", "0.05",
+           "--no-cpu-baseline", "--gather-transport", "gloo", "--one-device"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 48 and d["value"] > 0
+    chk = d["gather_check"]
+    assert chk["bitwise_equal"], chk
+    assert chk["utterances_checked"] == [0, 23, 24, 47]
+    assert chk["lanes_per_utterance"] == 64  # (24 utterances per rank: the voice kernel, as the shards ran)
+    assert d["multi_gpu"]["transport"].startswith("gloo")
+    assert d["multi_gpu"]["avg_launch_ms_max_over_ranks"] > 0
