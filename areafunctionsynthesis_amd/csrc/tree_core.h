@@ -1281,16 +1281,16 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
     }
     const double G = LAB * idt + RAB;
     const double H = -idt * (LAB * uu + LA * uD) - (TH1 / TH) * (LAB * uur + LA * uDr) + Sx;
-    double m = -EB - G;
-    m -= EA;    // 0.0 without a source
-    double rhs = H + DB;
-    rhs -= DA;  // 0.0 without a source
-    Xw[X_DIAG + i] = -m;
-    Xw[X_RHS + i] = -rhs;
+    // The reference's row (TdsModel.cpp:1913-2001) is m = -E_B - G - E_A on the diagonal and
+    // rhs = H + D_B - D_A; the SPD system stores -m and -rhs.  Written as the negated sums
+    // themselves -- exactly the same values, negation being exact and rounding symmetric -- so
+    // that no stored value needs a sign flip (a v_xor per value).
+    Xw[X_DIAG + i] = (EB + G) + EA;   // -m   (E_A: 0.0 without a source)
+    Xw[X_RHS + i] = DA - (H + DB);    // -rhs (D_A: 0.0 without a source)
     // edges of section s: (in, out0) = -E, (in, out1) = -E, (out0, out1) = E + L/(dt th) + R1
     xat(Xw, q.x_e0) = -EB;
     xat(Xw, q.x_e1) = -EB;
-    xat(Xw, q.x_e2) = -(-EB - (LB * idt + R1B));
+    xat(Xw, q.x_e2) = EB + (LB * idt + R1B);
   }
   constexpr int J64 = (S_LAST_MOUTH - DYN0) / W, J83 = S::ND + (S_LAST_NOSE - 46) / W;
 #pragma unroll
@@ -1313,16 +1313,16 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
       const double Rrad = dyn ? X[X_RRAD] : C.h.rrad_nose;  // (network phase / tables)
       double F = LA2 * idt + RA2 + Rrad;
       double H = -(LA2 * idt) * (uR + uL) - (LA2 * (TH1 / TH)) * (uRr + uLr) + Sr;
-      Xw[X_DIAG + rc] = -(-EB - F);
-      Xw[X_RHS + rc] = -(H - DB);
+      Xw[X_DIAG + rc] = EB + F;   // (negated sums, as the slot rows)
+      Xw[X_RHS + rc] = DB - H;
     }
     {
       const double Lrad = dyn ? X[X_RRAD + 1] : C.h.lrad_nose;
       double LAB2 = LA2 + Lrad;
       double G = LAB2 * idt + RA2;
       double H = -idt * (LA2 * uR + LAB2 * uL) - (TH1 / TH) * (LA2 * uRr + LAB2 * uLr) + Sr;
-      Xw[X_DIAG + lc] = -(-EB - G);
-      Xw[X_RHS + lc] = -(H - DB);
+      Xw[X_DIAG + lc] = EB + G;
+      Xw[X_RHS + lc] = DB - H;
     }
   }
 }
