@@ -146,24 +146,96 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
                       double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B,
                       int width, const int32_t *frame_row = nullptr, const int32_t *order = nullptr) {
   if (tree(c)) {
-    // Launch chunks of `per` samples: K5 (the chunk's noise-source plans), then K1.  With
-    // AFS_PLAN_OVERLAP=1 in the environment (afs_ctx::overlap), K5 of chunk k + 1 runs on the
-    // plan stream beside K1 of chunk k instead: two plan buffers, K5 of chunk k + 1 waits until
-    // K1 of chunk k - 1 has read that buffer, K1 of chunk k waits for its plans.  K5 (80 VGPRs,
-    // 4 KB of LDS per block) fits beside K1's wave, but the measured gain (+1.4 %) came with
-    // runs where K1 slowed by 9 % beside it, so the default is sequential.
     const int64_t S = (int64_t)ntrans * hop;
+    const int two = c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0;
+    const afs::SecRec *uo = c->dev_tab->consts.sec;
+    afs_status st;
+    // K6's glottal-tone input: section 25's pressure per sample of a launch.  Laid out so that
+    // every utterance's row sits at the same position in its 128-byte lines as its output row
+    // (stride and base congruent to the output's modulo 16 doubles): K1 stores both through one
+    // line-aligned window (tree_kernel.h).
+    auto p25_for = [&](int64_t per, int64_t *stride) -> afs_status {
+      *stride = per + ((ostride - per) % 16 + 16) % 16;
+      return ensure(c, &c->p25, &c->p25_bytes, ((size_t)B * (size_t)*stride + 32) * sizeof(double));
+    };
+    auto p25_row0 = [&](int64_t s0) {  // the p25 base for the launch whose outputs start at out + s0
+      const int64_t want = (int64_t)((reinterpret_cast<uintptr_t>(out + s0) >> 3) & 15);
+      const int64_t have = (int64_t)((reinterpret_cast<uintptr_t>(c->p25) >> 3) & 15);
+      return (double *)c->p25 + ((want - have) % 16 + 16) % 16;
+    };
+    // K1 over samples [s0, s1), then K6 over them (both timed)
+    auto synth = [&](int64_t s0, int64_t s1, const uint64_t *plan, int64_t plan_stride, const afs::tree::PlanHop *hops,
+                     int64_t hop_stride, int64_t p25_stride) -> afs_status {
+      afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride, plan, plan_stride, lanes,
+                      (double *)ws, B, c->host_tab.uni, hops, hop_stride, p25_row0(s0), p25_stride, order};
+      hipEvent_t e1 = prof_event(c);
+      HIP_TRY(c, afs::launch_tree_synth(a, width, c->stream));
+      hipEvent_t e2 = prof_event(c);
+      prof_pair(c, e1, e2, 0);
+      // K6: the glottal-tone filter and the output stage of the launch's samples
+      HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B, p25_row0(s0),
+                                         p25_stride, c->cfg.options.radiation_from_skin, c->stream));
+      prof_pair(c, e2, prof_event(c), 2);
+      return AFS_OK;
+    };
+    // Hop mode (tree solver, hops >= PLAN_HOP_MIN): K5 decides every hop of the call first -- one
+    // record per (row, hop), the hops it cannot decide at once listed -- the host reads the list's
+    // length, and K5's second stage writes the dense records of the listed hops whose samples
+    // differ (mixed) into a compact array (slot = list entry).  K1 then runs the call in launches
+    // of up to 65536 samples, each hop's words evaluated from its record (or read from its dense
+    // slot).  One K1 launch per second of 44.1 kHz audio instead of one per 4096 samples: no
+    // state save / restore and launch tail in between (+0.6 %, profiles/r04c_store_launch_ab.txt).
+    // A list whose dense records would exceed the plan budget falls back to the chunked path.
+    const bool hops = !c->plan_dense && hop >= afs::tree::PLAN_HOP_MIN;
+    const int64_t call_hops = afs::plan_hop_slots(0, S, hop);
+    if (hops && (int64_t)rows * call_hops * (int64_t)sizeof(afs::tree::PlanHop) <= c->plan_budget) {
+      const int64_t hstride = call_hops;
+      const size_t hbytes = (size_t)rows * (size_t)hstride * sizeof(afs::tree::PlanHop);
+      if ((st = ensure(c, &c->hops[0], &c->hops_bytes[0], hbytes)) != AFS_OK) return st;
+      if ((st = ensure(c, &c->plan_work[0], &c->plan_work_bytes[0], (size_t)afs::plan_work_bytes(rows, hstride))) != AFS_OK)
+        return st;
+      afs::tree::PlanHop *hbuf = (afs::tree::PlanHop *)c->hops[0];
+      uint32_t *work = (uint32_t *)c->plan_work[0];
+      afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, 0, S, nullptr, 0, two, uo, hbuf, hstride, work, true};
+      hipEvent_t e0 = prof_event(c);
+      HIP_TRY(c, afs::launch_plan_hops_iv(pa, c->stream));
+      HIP_TRY(c, hipMemcpyAsync(c->hcount, work, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));  // (the list's length sizes the dense records)
+      const int64_t listed = (int64_t)(uint32_t)*c->hcount;
+      const int64_t dense_bytes = listed * hop * afs::PLAN_RECORD_BYTES;
+      if (dense_bytes <= c->plan_budget) {
+        if (dense_bytes > 0 && (st = ensure(c, &c->plan, &c->plan_bytes, (size_t)dense_bytes)) != AFS_OK) return st;
+        pa.plan = (uint64_t *)c->plan;
+        HIP_TRY(c, afs::launch_plan_hops_wave(pa, c->stream));
+        prof_pair(c, e0, prof_event(c), 1);
+        const int64_t per = std::min<int64_t>(S, 65536);
+        int64_t p25_stride = 0;
+        if ((st = p25_for(per, &p25_stride)) != AFS_OK) return st;
+        for (int64_t s0 = 0; s0 < S; s0 += per) {
+          const int64_t s1 = std::min(S, s0 + per);
+          // (K1 indexes the records from the launch's first hop)
+          if ((st = synth(s0, s1, (const uint64_t *)c->plan, 0, hbuf + s0 / hop, hstride, p25_stride)) != AFS_OK)
+            return st;
+        }
+        return AFS_OK;
+      }
+      prof_pair(c, e0, prof_event(c), 1);
+    }
+    // Chunked path: launches of `per` samples, each K5 (the chunk's plans: dense records, or in
+    // hop mode the chunk's hop records with sample-indexed dense records) and then K1.  With
+    // AFS_PLAN_OVERLAP=1 in the environment (afs_ctx::overlap), K5 of chunk k + 1 runs on the plan
+    // stream beside K1 of chunk k instead: two plan buffers, K5 of chunk k + 1 waits until K1 of
+    // chunk k - 1 has read that buffer, K1 of chunk k waits for its plans.  K5 (80 VGPRs, 4 KB of
+    // LDS per block) fits beside K1's wave, but the measured gain (+1.4 %) came with runs where K1
+    // slowed by 9 % beside it, so the default is sequential.
     const int64_t per = std::max<int64_t>(1, std::min<int64_t>({S, 65536, c->plan_budget / ((int64_t)rows * afs::PLAN_RECORD_BYTES)}));
     const int64_t nch = (S + per - 1) / per;
-    const size_t pbytes = (size_t)rows * (size_t)per * afs::PLAN_RECORD_BYTES;
-    afs_status st = ensure(c, &c->plan, &c->plan_bytes, pbytes);
-    if (st != AFS_OK) return st;
+    // (hop mode: compact dense records, at most every hop the chunk touches: rows x (per + hop))
+    const size_t pbytes = (size_t)rows * (size_t)(per + (hops ? hop : 0)) * afs::PLAN_RECORD_BYTES;
+    if ((st = ensure(c, &c->plan, &c->plan_bytes, pbytes)) != AFS_OK) return st;
     const bool ov = c->overlap && nch > 1;
     if (ov && (st = ensure(c, &c->plan2, &c->plan2_bytes, pbytes)) != AFS_OK) return st;
     void *buf[2] = {c->plan, ov ? c->plan2 : c->plan};
-    // hop mode (tree solver, hops >= PLAN_HOP_MIN): K5 writes one record per (row, hop) and the
-    // dense records of mixed hops only; K1 evaluates the words from the hop records
-    const bool hops = !c->plan_dense && hop >= afs::tree::PLAN_HOP_MIN;
     const int64_t hstride = afs::plan_hop_slots(0, per, hop) + 1;  // (a chunk may start inside a hop)
     afs::tree::PlanHop *hbuf[2] = {nullptr, nullptr};
     if (hops) {
@@ -176,25 +248,13 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       hbuf[0] = (afs::tree::PlanHop *)c->hops[0];
       hbuf[1] = (afs::tree::PlanHop *)c->hops[ov ? 1 : 0];
     }
-    // K6's glottal-tone input: section 25's pressure per sample of the launch.  Laid out so that
-    // every utterance's row sits at the same position in its 128-byte lines as its output row
-    // (stride and base congruent to the output's modulo 16 doubles): K1 stores both through one
-    // line-aligned window (tree_kernel.h).
-    const int64_t p25_stride = per + ((ostride - per) % 16 + 16) % 16;
-    if ((st = ensure(c, &c->p25, &c->p25_bytes, ((size_t)B * (size_t)p25_stride + 32) * sizeof(double))) != AFS_OK)
-      return st;
-    auto p25_row0 = [&](int64_t s0) {  // the p25 base for the launch whose outputs start at out + s0
-      const int64_t want = (int64_t)((reinterpret_cast<uintptr_t>(out + s0) >> 3) & 15);
-      const int64_t have = (int64_t)((reinterpret_cast<uintptr_t>(c->p25) >> 3) & 15);
-      return (double *)c->p25 + ((want - have) % 16 + 16) % 16;
-    };
+    int64_t p25_stride = 0;
+    if ((st = p25_for(per, &p25_stride)) != AFS_OK) return st;
     hipStream_t ps = ov ? c->plan_stream : c->stream;
-    const int two = c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0;
-    const afs::SecRec *uo = c->dev_tab->consts.sec;
     auto plan_chunk = [&](int64_t k) -> afs_status {
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)buf[k & 1], per, two, uo,
-                       hbuf[k & 1], hstride, hops ? (uint32_t *)c->plan_work[ov ? (k & 1) : 0] : nullptr};
+                       hbuf[k & 1], hstride, hops ? (uint32_t *)c->plan_work[ov ? (k & 1) : 0] : nullptr, hops};
       hipEvent_t e0 = prof_event(c, ps);
       HIP_TRY(c, hops ? afs::launch_plan_hops(pa, ps) : afs::launch_plan(pa, ps));
       prof_pair(c, e0, prof_event(c, ps), 1);
@@ -217,17 +277,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
         HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_plan[k & 1], 0));
       }
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
-      afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride,
-                      (const uint64_t *)buf[k & 1], per, lanes, (double *)ws, B, c->host_tab.uni,
-                      hbuf[k & 1], hstride, p25_row0(s0), p25_stride, order};
-      hipEvent_t e1 = prof_event(c);
-      HIP_TRY(c, afs::launch_tree_synth(a, width, c->stream));
-      hipEvent_t e2 = prof_event(c);
-      prof_pair(c, e1, e2, 0);
-      // K6: the glottal-tone filter and the output stage of the launch's samples
-      HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B,
-                                         p25_row0(s0), p25_stride, c->cfg.options.radiation_from_skin, c->stream));
-      prof_pair(c, e2, prof_event(c), 2);
+      if ((st = synth(s0, s1, (const uint64_t *)buf[k & 1], per, hbuf[k & 1], hstride, p25_stride)) != AFS_OK) return st;
       if (ov) HIP_TRY(c, hipEventRecord(c->ev_free[k & 1], c->stream));
     }
     return AFS_OK;

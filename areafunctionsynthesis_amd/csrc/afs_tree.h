@@ -19,7 +19,8 @@ struct TreeArgs {
   int64_t s_begin, s_end;
   double *out;              // out[u * out_stride + s - s_begin]
   int64_t out_stride;
-  const uint64_t *plan;     // plan[(row(u) * plan_stride + s - s_begin) * 16 + w] (tree_plan.h)
+  const uint64_t *plan;     // plan[(row(u) * plan_stride + s - s_begin) * 16 + w] (tree_plan.h); hop
+                            // mode: the compact dense records of the mixed hops (PlanArgs::compact)
   int64_t plan_stride;
   void *lane_state;         // per-lane register state, B * lanes entries (Lane<lanes>)
   double *lds_state;        // per-utterance LDS block, B * tree_lds_doubles()
@@ -54,6 +55,10 @@ struct PlanArgs {
   int64_t hop_stride = 0;
   uint32_t *work = nullptr;  // hop mode: a counter and rows * hop slots entries (the hops decided
                              // sample by sample)
+  // hop mode: the dense records of a mixed hop go to slot e of a compact array (e: its work-list
+  // entry; plan[(e * hop + i) * 16 + w] for the hop's sample i; PlanHop::dense = e) instead of
+  // sample-indexed rows (the diagnostics' layout)
+  bool compact = false;
 };
 constexpr int64_t PLAN_RECORD_BYTES = 128;
 // Hop slots a launch of samples [s0, s1) spans.
@@ -89,6 +94,10 @@ hipError_t launch_tree_draws(const double *lds_state, int B, int64_t *draws, hip
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st);
 // K5 in hop mode: the hop records of the launch's hops, the dense records of its mixed hops
 hipError_t launch_plan_hops(const PlanArgs &a, hipStream_t st);
+// ... in its two stages: the interval decisions (records of the decided hops, the work list of the
+// others; a.work[0] = its length) and the per-sample decisions of the listed hops
+hipError_t launch_plan_hops_iv(const PlanArgs &a, hipStream_t st);
+hipError_t launch_plan_hops_wave(const PlanArgs &a, hipStream_t st);
 // diagnostics: the tree kernel's per-sample plan words from hop records (afs_plan_hop_words)
 hipError_t launch_tree_hop_words(const tree::PlanHop *h, const double *ratio, int n, uint64_t *out, hipStream_t st);
 // diagnostics: the tree kernel's tube interpolation (afs_tube_interpolate)

@@ -162,6 +162,7 @@ __global__ void __launch_bounds__(HOP_WAVE) plan_hop_wave_kernel(PlanArgs a, int
       hl = PlanHop{};
       const bool ok = plan_hop_inputs(k0, fl, fr, a.uo, a.two_mass != 0, hl);
       hl.mixed = (mixed || !ok) ? 1u : 0u;
+      hl.dense = a.compact ? e : 0u;
     }
     __syncthreads();
     mixed = reinterpret_cast<const PlanHop *>(hop_lds)->mixed != 0;
@@ -171,7 +172,8 @@ __global__ void __launch_bounds__(HOP_WAVE) plan_hop_wave_kernel(PlanArgs a, int
       for (int i = i0 + lane; i < i1; i += HOP_WAVE) {
         uint64_t w[PLAN_WORDS];
         plan_sample<true>(fl, fr, (double)i / (double)a.hop, a.uo, a.two_mass != 0, w);
-        ulonglong2 *o = (ulonglong2 *)(a.plan + (row * a.plan_stride + (h * a.hop + i - a.s_begin)) * PLAN_WORDS);
+        const int64_t rec = a.compact ? (int64_t)e * a.hop + i : row * a.plan_stride + (h * a.hop + i - a.s_begin);
+        ulonglong2 *o = (ulonglong2 *)(a.plan + rec * PLAN_WORDS);
 #pragma unroll
         for (int q = 0; q < PLAN_WORDS / 2; ++q) o[q] = make_ulonglong2(w[2 * q], w[2 * q + 1]);
       }
@@ -182,7 +184,7 @@ __global__ void __launch_bounds__(HOP_WAVE) plan_hop_wave_kernel(PlanArgs a, int
 
 }  // namespace
 
-hipError_t launch_plan_hops(const PlanArgs &a, hipStream_t st) {
+hipError_t launch_plan_hops_iv(const PlanArgs &a, hipStream_t st) {
   const int64_t n = a.s_end - a.s_begin;
   if (n <= 0 || a.rows <= 0) return hipSuccess;
   if (!a.hops || a.hop < PLAN_HOP_MIN) return hipErrorInvalidValue;
@@ -192,10 +194,23 @@ hipError_t launch_plan_hops(const PlanArgs &a, hipStream_t st) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(plan_hop_iv_kernel, dim3((unsigned)((n_hops + HOP_IV_BLOCK - 1) / HOP_IV_BLOCK)),
                      dim3(HOP_IV_BLOCK), 0, st, a, slots);
+  return hipGetLastError();
+}
+
+hipError_t launch_plan_hops_wave(const PlanArgs &a, hipStream_t st) {
+  const int64_t n = a.s_end - a.s_begin;
+  if (n <= 0 || a.rows <= 0) return hipSuccess;
+  if (!a.hops || a.hop < PLAN_HOP_MIN || !a.work) return hipErrorInvalidValue;
+  const int64_t slots = plan_hop_slots(a.s_begin, a.s_end, a.hop), n_hops = (int64_t)a.rows * slots;
   // (a fixed grid: the list's length is on the device; every wave leaves its loop at its end)
   const int64_t waves = n_hops < 2048 ? n_hops : 2048;
   hipLaunchKernelGGL(plan_hop_wave_kernel, dim3((unsigned)waves), dim3(HOP_WAVE), 0, st, a, slots);
   return hipGetLastError();
+}
+
+hipError_t launch_plan_hops(const PlanArgs &a, hipStream_t st) {
+  const hipError_t e = launch_plan_hops_iv(a, st);
+  return e != hipSuccess ? e : launch_plan_hops_wave(a, st);
 }
 
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {

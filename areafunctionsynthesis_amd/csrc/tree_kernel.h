@@ -221,12 +221,15 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
   double hp[4] = {0.0, 0.0, 0.0, 0.0};
   uint32_t hkind = PK_CONST;
   bool hmixed = !HOPS;
+  // a mixed hop's dense records (compact: slot h->dense of a.plan), word gl % 16 of sample 0
+  const uint64_t *pd = nullptr;
   auto hop_load = [&](const PlanHop *h) {
     const double2 *q = reinterpret_cast<const double2 *>(h->p[gl & (PLAN_WORDS - 1)]);
     const double2 v0 = q[0], v1 = q[1];
     hp[0] = v0.x; hp[1] = v0.y; hp[2] = v1.x; hp[3] = v1.y;
     hkind = h->kind[gl & (PLAN_WORDS - 1)];
     hmixed = h->mixed != 0;
+    pd = a.plan + (int64_t)h->dense * hop * PLAN_WORDS + (gl & (PLAN_WORDS - 1));
   };
   if constexpr (HOPS) hop_load(hr);
   // Dense kernel (hops < 32: target sequences play one frame per sample): the fields of the
@@ -245,7 +248,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
   double wo = 0.0, wp = 0.0;
 #endif
   ex.sync();
-  uint64_t next = hmixed ? pl[0] : 0;
+  uint64_t next = hmixed ? (HOPS ? pd[i * PLAN_WORDS] : pl[0]) : 0;
   for (int64_t t = 0; t < n; ++t) {
     // (divided at the top of each step: the next sample's ratio computed at the end of the
     // previous step instead measured -2.5 %, profiles/r03ad_ab.txt)
@@ -256,7 +259,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
       R.planw = hmixed ? next : ev;
       // (a hop that is not mixed reads its own record's first word: a cache hit, no branch; the
       // load under a branch instead measured the same, profiles/r03w_ab.txt)
-      next = *(hmixed ? pl + tn * PLAN_WORDS : reinterpret_cast<const uint64_t *>(hr));
+      next = *(hmixed ? pd + (i + 1 < hop ? i + 1 : i) * PLAN_WORDS : reinterpret_cast<const uint64_t *>(hr));
     } else {
       R.planw = next;
       next = pl[tn * PLAN_WORDS];  // the next sample's word, a sample ahead
@@ -301,7 +304,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
         if constexpr (HOPS) {
           frame_load<W>(gl, R, X, fu + (k - 1), fu + k);
           hop_load(++hr);
-          if (hmixed) next = pl[(t + 1) * PLAN_WORDS];
+          if (hmixed) next = pd[0];
         } else {
           frame_shift<W>(gl, R, X, nf);
         }

@@ -463,7 +463,8 @@ struct PlanHop {
   double p[PLAN_WORDS][4];  // lane w: its word's inputs (PK_CONST: the word's bits in p[w][0])
   uint8_t kind[PLAN_WORDS];
   uint32_t mixed;           // 1: the hop's samples use the dense records
-  uint32_t pad[3];
+  uint32_t dense;           // compact dense records (PlanArgs::compact): the mixed hop's slot
+  uint32_t pad[2];
 };
 static_assert(sizeof(PlanHop) == 544, "hop record layout (K1 loads p[w] as two 16-byte words)");
 constexpr int PLAN_HOP_MIN = 32;  // shorter hops (target sequences: hop 1) keep dense records
