@@ -191,6 +191,7 @@ def measure(args, ctx, dev, stream, workload: str, B: int, first: int, world: in
     else:
         m.shapes, m.targets, m.seeds = vcv_targets(B, first_utterance=first)
         m.hop, m.T = 1, ctx.target_sequence_samples()
+        m.distinct = int(np.unique(m.targets, axis=0).shape[0])  # (one tube trajectory per distinct sequence)
 
         def synth():
             ctx.play_target_sequences(m.shapes, m.targets, seeds=seeds_dev, out=out_dev)
@@ -352,6 +353,16 @@ def describe(args, m: Measured, world: int, digest: str) -> dict:
         "binding_resource": "neither HBM nor MFMA: the latency of the per-sample fp64 recurrence "
                             "(SURVEY.md 8(d)); see fp64",
     }
+    if m.workload == "vcv":
+        # hop 1: every utterance reads its trajectory's frame each sample, but the batch plays only
+        # `distinct` trajectories (afs_play_target_sequences builds one per distinct target sequence)
+        roof["algorithmic_bytes_meaning"] = (
+            "per-utterance bytes: one 1072-B frame per utterance-sample (hop 1) + the 8-B output sample; "
+            f"the {B} utterances play {m.distinct} distinct trajectories, so the distinct frame bytes are "
+            "far fewer (distinct_frame_bytes_per_launch) and most frame reads hit the caches -- the "
+            "achieved GB/s above is a per-utterance rate, not HBM traffic (that is `traffic`)")
+        roof["distinct_trajectories"] = m.distinct
+        roof["distinct_frame_bytes_per_launch"] = float(m.distinct) * samples_per_launch / B * 1072.0
     if tr and tr.get("plan_kernel_traffic_bytes_per_launch") is not None:
         roof["plan_kernel_traffic_bytes_per_launch"] = tr["plan_kernel_traffic_bytes_per_launch"]
     return {"value": value, "ms_per_step": m.elapsed / m.steps * 1e3, "roofline": roof, "fp64": fp64,
