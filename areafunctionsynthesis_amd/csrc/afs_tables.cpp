@@ -443,9 +443,14 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
     int br = -1;
     if (a >= 0) br = (t->cout0[a] == s) ? t->cout1[a] : t->cout0[a];
     const bool da = a >= 0 && dyn(a), sa = a >= 0 && !dyn(a);
-    q.x_la = da ? (int16_t)(X_L + a - tree::DYN0) : zero;
-    q.x_ra = da ? (int16_t)(X_R1 + a - tree::DYN0) : zero;
-    q.x_ea = da ? (int16_t)(X_E + a - tree::DYN0) : zero;
+    // (a static source or none: entry NDYP - 1 of the dynamic arrays, which no slot writes -- absent
+    // slots store into entry NDYNS -- so it stays 0.0 from the reset; the row phase reads L, R1 and
+    // E of the source at fixed distances from x_la, tree_core.h phase_rows)
+    static_assert(tree::NDYP - 1 > tree::NDYNS, "a dynamic-array entry that no slot writes");
+    const int ad = da ? a - tree::DYN0 : tree::NDYP - 1;
+    q.x_la = (int16_t)(X_L + ad);
+    q.x_ra = (int16_t)(X_R1 + ad);
+    q.x_ea = (int16_t)(X_E + ad);
     q.c_la = sa ? t->L[a] : 0.0;
     q.c_ra = sa ? t->R[a] : 0.0;
     q.c_ea = sa ? t->E[a] : 0.0;

@@ -1239,9 +1239,10 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     const SecRec &q = rec[j];
+    // (the source's L, R1 and E sit at fixed distances in the dynamic arrays: one address)
     xla[j] = xat(X, q.x_la);
-    xra[j] = xat(X, q.x_ra);
-    xea[j] = xat(X, q.x_ea);
+    xra[j] = xat(X, q.x_la + (X_R1 - X_L) * 8);
+    xea[j] = xat(X, q.x_la + (X_E - X_L) * 8);
     xda[j] = xat(X, q.x_da);
     xsx[j] = xat(X, q.x_sx);
     xub[j] = xat(X, q.x_ub);
