@@ -97,11 +97,7 @@ enum : int {
   X_TVEL = X_TGLOT + 8,        // transvelar coupling filters H1, H2: x1..x4, y1..y4 each
   X_TVP = X_TVEL + 16,         // p[43], p[67] after the last update (transvelar filter inputs)
   X_RRAD = X_TVP + 2,          // mouth radiation R and L (section 64), from the network phase
-  // store windows of the synthesis kernel's per-sample outputs (tree_kernel.h): the radiated flows
-  // and section 25's pressures of the samples of one 128-byte line of each output array, stored
-  // line by line (empty between launches)
-  X_OWIN = X_RRAD + 2, X_PWIN = X_OWIN + 16,
-  X_TOTAL = X_PWIN + 16,
+  X_TOTAL = X_RRAD + 2,
   // LDS stride of the utterance blocks: 128 B modulo the 256-B bank row, so that the two
   // utterances of a 32-lane LDS lane group (ds_read_b64: lanes 0-31, 32-63) address the
   // same slot through disjoint banks

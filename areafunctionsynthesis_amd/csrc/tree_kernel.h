@@ -237,16 +237,16 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
   // behind that sample's work instead of stalling the frame transition; the new left frame is
   // the old right one (frame_shift).
   NextFrame<W> nf{};
-  // The per-sample outputs (the radiated flow: every lane has it; section 25's pressure: lane 2)
-  // go to an LDS window of the 16 samples of one 128-byte line of o -- p25o sits at the same
-  // position in its lines (afs_capi.cpp lays it out so) -- and lanes 0-15 store the window as one
-  // whole line of each array when its last sample is written (or the launch ends): one coalesced
-  // store per line instead of 16 single 8-byte stores, which the memory system wrote back as
-  // partial lines (2x the stored bytes, profiles/pmc_traffic.json r03aj).
+  // The per-sample outputs (the radiated flow: every lane has it; section 25's pressure: lane 2's
+  // slot 0) are held in a register window of the 16 samples of one 128-byte line of o -- lane j
+  // of the utterance keeps the sample at position j of the line; p25o sits at the same position in
+  // its lines (afs_capi.cpp lays it out so) -- and lanes 0-15 store the window as one whole line of
+  // each array when its last sample is in (or the launch ends): one coalesced store per line
+  // instead of 16 single 8-byte stores, which the memory system wrote back as partial lines (2x
+  // the stored bytes, profiles/pmc_traffic.json r03aj).  Measured against those stores and against
+  // the window in LDS: +0.4 % / +0.5 % (profiles/r04f_store_ab.txt).
   const int o_line = (int)((reinterpret_cast<uintptr_t>(o) >> 3) & 15);
-#if defined(AFS_AB_REG_WINDOW)
   double wo = 0.0, wp = 0.0;
-#endif
   ex.sync();
   uint64_t next = hmixed ? (HOPS ? pd[i * PLAN_WORDS] : pl[0]) : 0;
   for (int64_t t = 0; t < n; ++t) {
@@ -266,37 +266,18 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
       if (i + 1 == hop && t + 1 < n) nf.load(gl, fu + k + 1);
     }
     sample_step<W, MODEL>(ex, X, a.uni, C, ratio, true);
-#if defined(AFS_AB_REG_WINDOW)  // (temporary A/B: the window in registers: lane gl keeps entry gl)
     {
-      const int j = (o_line + (int)t) & 15;
-      const uint64_t pb = __builtin_bit_cast(uint64_t, R.p[0]);  // lane 2's p[25] to the row
-      const double p25v = __builtin_bit_cast(double, ((uint64_t)(uint32_t)AFS_DPP((int)(uint32_t)(pb >> 32), 0x152, 0xF, 0xF, false) << 32) |
-                                                         (uint32_t)AFS_DPP((int)(uint32_t)pb, 0x152, 0xF, 0xF, false));
+      const int j = (o_line + (int)t) & 15;  // the sample's position in its line
+      const double p25v = GpuExec<PROF, W>::template dpp<0x152>(R.p[0]);  // lane 2's p[25] to its row
       const bool mine = gl == j;
       wo = mine ? R.sample : wo;
       wp = mine ? p25v : wp;
+      // lane gl stores window entry gl, sample t - j + gl, if it belongs to this launch
       if (valid && (j == 15 || t + 1 == n) && gl <= j && t - j + gl >= 0) {
         o[t - j + gl] = wo;
         p25o[t - j + gl] = wp;
       }
     }
-#elif defined(AFS_AB_DIRECT_STORE)  // (temporary A/B: the round-3 single-lane 8-byte stores)
-    if (valid && gl == 0) o[t] = R.sample;
-    if (valid && gl == 2) p25o[t] = R.p[0];
-    (void)o_line;
-#else
-    {
-      const int j = (o_line + (int)t) & 15;
-      X[X_OWIN + j] = R.sample;                 // (the same value from every lane)
-      // section 25's new pressure (lane 2's slot 0), the glottal-tone filter's input in K6
-      if (gl == 2) X[X_PWIN + j] = R.p[0];
-      // lane gl stores window entry gl, sample t - j + gl, if it belongs to this launch
-      if (valid && (j == 15 || t + 1 == n) && gl <= j && t - j + gl >= 0) {
-        o[t - j + gl] = X[X_OWIN + gl];
-        p25o[t - j + gl] = X[X_PWIN + gl];
-      }
-    }
-#endif
     if (++i == hop) {
       i = 0;
       ++k;
