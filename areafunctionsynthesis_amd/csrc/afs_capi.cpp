@@ -208,7 +208,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
         pa.plan = (uint64_t *)c->plan;
         HIP_TRY(c, afs::launch_plan_hops_wave(pa, c->stream));
         prof_pair(c, e0, prof_event(c), 1);
-        const int64_t per = std::min<int64_t>(S, 65536);
+        const int64_t per = std::min<int64_t>(S, c->launch_cap);
         int64_t p25_stride = 0;
         if ((st = p25_for(per, &p25_stride)) != AFS_OK) return st;
         for (int64_t s0 = 0; s0 < S; s0 += per) {
@@ -228,7 +228,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     // chunk k - 1 has read that buffer, K1 of chunk k waits for its plans.  K5 (80 VGPRs, 4 KB of
     // LDS per block) fits beside K1's wave, but the measured gain (+1.4 %) came with runs where K1
     // slowed by 9 % beside it, so the default is sequential.
-    const int64_t per = std::max<int64_t>(1, std::min<int64_t>({S, 65536, c->plan_budget / ((int64_t)rows * afs::PLAN_RECORD_BYTES)}));
+    const int64_t per = std::max<int64_t>(1, std::min<int64_t>({S, c->launch_cap, c->plan_budget / ((int64_t)rows * afs::PLAN_RECORD_BYTES)}));
     const int64_t nch = (S + per - 1) / per;
     // (hop mode: compact dense records, at most every hop the chunk touches: rows x (per + hop))
     const size_t pbytes = (size_t)rows * (size_t)(per + (hops ? hop : 0)) * afs::PLAN_RECORD_BYTES;
@@ -419,6 +419,10 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   if (const char *e = std::getenv("AFS_PLAN_OVERLAP")) ctx->overlap = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_PLAN_DENSE")) ctx->plan_dense = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_XCD_ORDER")) ctx->xcd_order = std::atoi(e) != 0;
+  if (const char *e = std::getenv("AFS_LAUNCH_SAMPLES")) {  // (A/B and latency studies: samples per K1 launch)
+    const long long v = std::atoll(e);
+    if (v > 0) ctx->launch_cap = std::min<int64_t>(v, 65536);
+  }
   if (hipStreamCreateWithFlags(&ctx->plan_stream, hipStreamNonBlocking) != hipSuccess) return bail(AFS_ERR_HIP);
   for (hipEvent_t *e : {&ctx->ev_go, &ctx->ev_plan[0], &ctx->ev_plan[1], &ctx->ev_free[0], &ctx->ev_free[1]})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return bail(AFS_ERR_HIP);

@@ -201,6 +201,53 @@ AFS_HD inline double fast_div(double a, double b) {
 #endif
 }
 
+// The interpolation ratio i / hop of sample i of a hop (0 <= i < hop), from inv_hop = 1 / hop
+// (correctly rounded, once per launch): q = i * inv_hop, then one correction by the exact remainder
+// i - hop q (an fma): the correctly rounded quotient (Markstein's theorem), so bit for bit the
+// division the reference and K5 take (tests/test_hop_ratio.py checks every i < hop for every hop up
+// to 8192 and sampled hops up to 65536); one multiply and two fmas instead of the ~10 instructions of
+// an IEEE division on the sample's chain.  Host builds divide.
+AFS_HD inline double hop_ratio(int i, double dhop, double inv_hop) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double di = (double)i;
+  const double q = di * inv_hop;
+  return fma(fma(-dhop, q, di), inv_hop, q);
+#else
+  (void)inv_hop;
+  return (double)i / dhop;
+#endif
+}
+
+// x clamped from below (at_least) or above (at_most) at a positive constant c, as the reference's
+// `if (x < c) x = c`.  Device: one v_max_f64 / v_min_f64 (the select form is a compare and two
+// 32-bit selects of the constant's halves); equal for every x that is not a NaN (a NaN gives c --
+// the inputs here are areas, surfaces and controls, finite).  Host builds compare.
+AFS_HD inline double at_least(double x, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_fmax(x, c);
+#else
+  return x < c ? c : x;
+#endif
+}
+// max(x, 0) as the reference's `if (x < 0) x = 0` / `x < 0 ? 0 : x`: one v_max_f64 on the device.
+// Differs only for x = -0 (gives +0: every caller adds it to or multiplies it into a value whose
+// result is the same either way) and NaN (gives 0: a NaN flow, displacement or control is in the
+// system already).
+AFS_HD inline double nonneg(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_fmax(x, 0.0);
+#else
+  return x < 0.0 ? 0.0 : x;
+#endif
+}
+AFS_HD inline double at_most(double x, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_fmin(x, c);
+#else
+  return x > c ? c : x;
+#endif
+}
+
 // Word `kind` of a hop record at `ratio` (tree_plan.h plan_word_eval), branch-free on the
 // device: every lane evaluates one square root and one quotient and keeps its kind's value.
 // The interpolation is K5's and phase_interpolate's (uncontracted), so the area A is bit-identical.
@@ -218,8 +265,7 @@ AFS_HD inline uint64_t plan_word_fast(uint32_t kind, const double *p, double rat
     x = r1 * p[0] + ratio * p[1];
     y = r1 * p[2] + ratio * p[3];
   }
-  double a = x < AMIN ? AMIN : x;
-  a = a < 0.1 ? 0.1 : a;
+  const double a = at_least(at_least(x, AMIN), 0.1);
   const bool invd = kind == PK_INVD, fdn = kind == PK_FDN;
   // (a constant word's inputs are no area: its lane computes on them and discards the value)
   const double s = fast_sqrt(invd ? (4.0 * a) * (1.0 / PI) : a);
@@ -285,11 +331,20 @@ AFS_HD inline int slot_section(int j, int gl) {
 // ---------------------------------------------------------------------------
 // math helpers
 // ---------------------------------------------------------------------------
+// The section-area clamp (Tube.cpp:337).  clampA keeps a NaN (the reference's comparison does, and
+// a NaN frame area must give NaN audio from its transition on); clampA_num is at_least for the
+// per-sample areas whose NaN reaches the audio by another path as well: the interpolated pharynx /
+// mouth areas (a NaN frame area also makes that section's frame length NaN, frame_load, so the
+// interpolated length carries it into the system in the same sample) and the glottis areas (a NaN
+// there comes from NaN pressures, already in the system).
 AFS_HD inline double clampA(double a) { return a < AMIN ? AMIN : a; }
+AFS_HD inline double clampA_num(double a) { return at_least(a, AMIN); }
+// A frame's section length, NaN when the section's area is (see clampA_num).
+AFS_HD inline double frame_length(double area, double length) { return area != area ? area : length; }
 
 AFS_HD inline double glottis_q(double f0) {
   double q = 1.0 + (f0 - G_NAT_F0) * (1.0 / G_F0_DIV_Q);
-  return q < 0.05 ? 0.05 : q;
+  return at_least(q, 0.05);
 }
 
 // getOpenCloseDimensions (TriangularGlottis.cpp:474-576), as selects (the three cases and the
@@ -333,7 +388,7 @@ template <class CT>
 AFS_HD inline GlotOut two_mass_glottis(const CT &C, const double *gp, const double *p4, const double *rel,
                                        double *rel_out) {
   double Q = 1.0 + (gp[0] - TM_NAT_F0) * (1.0 / TM_F0_DIV_Q);  // getTensionParameter (:467-485)
-  if (Q < 0.05) Q = 0.05;
+  Q = at_least(Q, 0.05);
   const double f = fast_sqrt(Q), inv_f = fast_rcp(f), inv_q = fast_rcp(Q);
   const double len = TM_REST_LEN * f, th0 = TM_REST_THICK0 * inv_f, th1 = TM_REST_THICK1 * inv_f;
   const double rel0 = rel[0], rel1 = rel[1];
@@ -341,13 +396,13 @@ AFS_HD inline GlotOut two_mass_glottis(const CT &C, const double *gp, const doub
   // geometry
   double a0 = rest0 + rel0, a1 = rest1 + rel1;
   const double ab0 = a0, ab1 = a1;  // incTime's absolute displacements are not clipped
-  if (a0 < 0.0) a0 = 0.0;
-  if (a1 < 0.0) a1 = 0.0;
+  a0 = nonneg(a0);
+  a1 = nonneg(a1);
   double passive = 2.0 * rest1;
-  if (passive < 0.0) passive = 0.0;
+  passive = nonneg(passive);
   double chink = passive * TM_CHINK_LEN + gp[4];
-  if (chink < 0.0) chink = 0.0;
-  GlotOut go{clampA(2.0 * len * a0 + chink), clampA(2.0 * len * a1 + chink), th0, th1};
+  chink = nonneg(chink);
+  GlotOut go{clampA_num(2.0 * len * a0 + chink), clampA_num(2.0 * len * a1 + chink), th0, th1};
   // incTime
   const double crit = 0.5 * TM_CRIT_WIDTH;
   const double min0 = crit - rest0, min1 = crit - rest1;
@@ -526,8 +581,8 @@ AFS_HD inline void frame_load(int gl, Lane<W> &R, double *X, const afs_frame *fl
     if (m >= 0 && m < NPM) {
       R.aL[j] = clampA(fl->area_cm2[m]);   // the caller's Tube stores clamped areas (Tube.cpp:337)
       R.aR[j] = clampA(fr->area_cm2[m]);
-      R.lL[j] = fl->length_cm[m];
-      R.lR[j] = fr->length_cm[m];
+      R.lL[j] = frame_length(fl->area_cm2[m], fl->length_cm[m]);
+      R.lR[j] = frame_length(fr->area_cm2[m], fr->length_cm[m]);
     }
   }
   // (laterality, articulators and teeth position only steer the noise sources: tree_plan.h)
@@ -574,7 +629,7 @@ AFS_HD inline void frame_shift(int gl, Lane<W> &R, double *X, const NextFrame<W>
       R.aL[j] = R.aR[j];
       R.lL[j] = R.lR[j];
       R.aR[j] = clampA(nf.a[j]);
-      R.lR[j] = nf.l[j];
+      R.lR[j] = frame_length(nf.a[j], nf.l[j]);
     }
   }
   if (gl == 0) {
@@ -618,7 +673,7 @@ AFS_HD inline void phase_interpolate(int gl, Lane<W> &R, double *X, const Consts
     const int i = s - S_NOSE0;
     const double anose = open + ((double)(i * i) * (C.h.nose4_area - open)) * (1.0 / 16);
     // (both candidates clamped: one clamp after the select measured -0.2 %, profiles/r03x_ab.txt)
-    const double a = pm ? clampA(apm) : (nose ? clampA(anose) : 1.0);
+    const double a = pm ? clampA_num(apm) : (nose ? clampA(anose) : 1.0);
     R.acur[j] = a;
     R.lcur[j] = pm ? lpm : C.h.len_nose0;
   }
@@ -662,7 +717,7 @@ AFS_HD inline GlotRes glottis_eval(const GlotIn &in, const CT &C, double ratio, 
     // calcGeometry + getTubeData + Tube::setGlottisGeometry (TriangularGlottis.cpp:338-411)
     // (divisions sharing a denominator use one reciprocal; sqrt(m k) is a constant since
     // m ~ 1/q and k ~ q)
-    double chink = gp[4] < 0.0 ? 0.0 : gp[4];
+    double chink = nonneg(gp[4]);
     double q = glottis_q(gp[0]);
     double f = fast_sqrt(q);
     const double inv_f = fast_rcp(f), inv_q = fast_rcp(q);
@@ -671,7 +726,7 @@ AFS_HD inline GlotRes glottis_eval(const GlotIn &in, const CT &C, double ratio, 
     double th0 = G_REST_THICK0 * inv_f, th1 = G_REST_THICK1 * inv_f;
     double olen[2], clen[2], ow[2], cz[2];
     glottis_open_close(gp, cord, rel0, rel1, olen, clen, ow, cz);
-    res.go = GlotOut{clampA(olen[0] * ow[0] + chink), clampA(olen[1] * ow[1] + chink), th0, th1};
+    res.go = GlotOut{clampA_num(olen[0] * ow[0] + chink), clampA_num(olen[1] * ow[1] + chink), th0, th1};
     // incTime (TriangularGlottis.cpp:154-330) with the previous sample's pressures
     const double Tt = C.h.Tt;
     const double p0 = p4[0], p1 = p4[1], p2 = p4[2], p3 = p4[3];
@@ -723,7 +778,7 @@ AFS_HD inline GlotRes glottis_eval_split(const GlotIn &in, const CT &C, double r
     for (int k = 0; k < 6; ++k) gp[k] = r1 * in.fl[k] + ratio * in.fr[k];
   }
   const double rel0 = in.rel[0], rel1 = in.rel[1];
-  double chink = gp[4] < 0.0 ? 0.0 : gp[4];
+  double chink = nonneg(gp[4]);
   double q = glottis_q(gp[0]);
   double f = fast_sqrt(q);
   const double inv_f = fast_rcp(f), inv_q = fast_rcp(q);
@@ -735,7 +790,7 @@ AFS_HD inline GlotRes glottis_eval_split(const GlotIn &in, const CT &C, double r
   const double rest = m1 ? gp[3] : gp[2], rel = m1 ? rel1 : rel0, relp = m1 ? in.rel[3] : in.rel[2];
   double olen, clen, ow, cz;
   glottis_open_close_one(rest, cord, rel, olen, clen, ow, cz);
-  const double area = clampA(olen * ow + chink);
+  const double area = clampA_num(olen * ow + chink);
   const double th = K[6] * inv_f;
   const double Tt = C.h.Tt;
   const double p0 = p4[0], p1 = p4[1], p2 = p4[2], p3 = p4[3];
@@ -857,7 +912,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
     const double L = (RHO * 0.5 * len) * inv_area;
     const double Cc = (area * len) * (1.0 / (RHO * CSND * CSND));
     double surf = (2.0 * PI * r0) * len;
-    if (surf < AMIN) surf = AMIN;
+    surf = at_least(surf, AMIN);
     const bool walls = opt.soft_walls && !glot;
     const double alpha = walls ? surf * C.h.wall_invK : 0.0;
     const double beta = walls ? fma(R.w[j], C.h.wall_k1, fma(R.wr[j], C.h.wall_k2, R.wr2[j] * C.h.wall_k3)) : 0.0;
@@ -968,13 +1023,11 @@ AFS_HD inline double narrow_flow(const double *X, uint32_t o0, uint32_t o1) {
   double flow = 0.0;
   flow += xat(X, o0);  // (an absent output reads the zero slot)
   flow += xat(X, o1);
-  return flow < 0.0 ? 0.0 : flow;  // only outgoing flow (:1512-1517)
+  return nonneg(flow);  // only outgoing flow (:1512-1517)
 }
 
 AFS_HD inline double clamp_fc(double fc) {
-  if (fc < 50.0) fc = 50.0;
-  if (fc > 2000.0) fc = 2000.0;
-  return fc;
+  return at_most(at_least(fc, 50.0), 2000.0);
 }
 
 template <int W, class Xc>
@@ -985,7 +1038,7 @@ AFS_HD inline void phase_targets(Xc &x, int gl, Lane<W> &R, const double *X, con
   Target t[4];
   {  // glottis: A = the upper glottis section's area (this sample's glottis), clamped at 0.1
     const SecRec &q = C.sec[S_GLOT_UP];
-    const double A = a_glot_up < 0.1 ? 0.1 : a_glot_up;
+    const double A = at_least(a_glot_up, 0.1);
     const double v = narrow_flow(X, q.x_uo0, q.x_uo1) * fast_rcp(A);
     const double full = plan_double(x.template rec<PW_GAIN_G>()) * fabs(v) * v * v * fast_sqrt(A);
     const double fdn = plan_double(x.template rec<PW_FDN + 0>());

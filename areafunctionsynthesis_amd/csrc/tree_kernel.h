@@ -247,12 +247,14 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
   // the window in LDS: +0.4 % / +0.5 % (profiles/r04f_store_ab.txt).
   const int o_line = (int)((reinterpret_cast<uintptr_t>(o) >> 3) & 15);
   double wo = 0.0, wp = 0.0;
+  const double dhop = (double)hop, inv_hop = 1.0 / dhop;
   ex.sync();
   uint64_t next = hmixed ? (HOPS ? pd[i * PLAN_WORDS] : pl[0]) : 0;
   for (int64_t t = 0; t < n; ++t) {
-    // (divided at the top of each step: the next sample's ratio computed at the end of the
-    // previous step instead measured -2.5 %, profiles/r03ad_ab.txt)
-    const double ratio = (double)i / (double)hop;
+    // (the ratio at the top of each step -- the next sample's computed at the end of the previous
+    // step instead measured -2.5 %, profiles/r03ad_ab.txt; hop_ratio instead of the IEEE division
+    // +0.7 %, profiles/r04i_ab.txt)
+    const double ratio = hop_ratio(i, dhop, inv_hop);
     const int64_t tn = t + 1 < n ? t + 1 : t;
     if constexpr (HOPS) {
       const uint64_t ev = plan_word_fast(hkind, hp, ratio);
@@ -283,7 +285,11 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
       ++k;
       if (t + 1 < n) {
         if constexpr (HOPS) {
-          frame_load<W>(gl, R, X, fu + (k - 1), fu + k);
+          // the right frame becomes the left one (registers / LDS), only the new right frame is
+          // read: each frame crosses HBM once per utterance instead of twice
+          NextFrame<W> f{};
+          f.load(gl, fu + k);
+          frame_shift<W>(gl, R, X, f);
           hop_load(++hr);
           if (hmixed) next = pd[0];
         } else {
