@@ -174,6 +174,33 @@ def test_session_equals_trajectory(contexts, oracle, solver):
     syn.close()
 
 
+@pytest.mark.parametrize("solver", TREE_SOLVERS)
+def test_launch_split_is_bitwise(oracle, solver, monkeypatch):
+    """The tree path's launches (one per second of audio by default; AFS_LAUNCH_SAMPLES lowers it)
+    carry the lane and LDS state, the hop records and the frame cache across their boundaries: a
+    call split into launches of 1000 samples -- boundaries inside hops of 441 -- gives the same
+    audio bit for bit, static vowels and fricatives with their noise sources."""
+    from areafunctionsynthesis_amd.synthesizer import Context
+    frames = np.stack([static_frames(oracle, v, 12, velum=vel)
+                       for v, vel in (("a:", 0.0), ("s", 1.0), ("i:", 0.0), ("S", 0.0), ("u:", 0.5))])
+    seeds = np.arange(7, 7 + len(frames), dtype=np.uint32)
+    ys = []
+    for env in (None, "1000"):
+        if env is None:
+            monkeypatch.delenv("AFS_LAUNCH_SAMPLES", raising=False)
+        else:
+            monkeypatch.setenv("AFS_LAUNCH_SAMPLES", env)
+        ctx = Context(44100.0, solver="tree", lanes=LANES[solver], profile=True)
+        try:
+            ys.append(ctx.synthesize(frames, 441, seeds=seeds))
+            kt = ctx.kernel_times()
+        finally:
+            ctx.close()
+        assert kt["synth_launches"] == (1 if env is None else -(-11 * 441 // 1000))
+    assert np.array_equal(ys[0], ys[1])
+    assert np.isfinite(ys[0]).all()
+
+
 @pytest.mark.parametrize("solver", SOLVERS)
 def test_edge_cases(contexts, oracle, solver):
     ctx = contexts(44100.0, solver)
