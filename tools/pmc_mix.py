@@ -1,5 +1,5 @@
 """Dynamic instruction mix and cycle split of the synthesis kernel from the three SQ passes of
-tools/r03_session.sh (step `mix`, one bench step each): instructions and cycles per
+tools/session.sh (step `mix`, one bench step each): instructions and cycles per
 wave-sample (a wave holds 4 utterances; one audio sample of all four).  Writes
 profiles/pmc_mix.json under bench.py's key and the kernel sources' digest, and prints a table.
 
