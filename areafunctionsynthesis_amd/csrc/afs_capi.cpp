@@ -83,11 +83,14 @@ int lanes_for(const afs_ctx *c, int64_t B) {
   return B <= c->simds ? afs::TREE_VOICE_W : afs::TREE_W;
 }
 
-// Bytes of noise-source plans one tree launch may use (afs_ctx::plan_budget: 4 GiB, or
-// AFS_PLAN_BUDGET_MB); a launch covers at most plan_budget / (rows * 128 B) samples and at most
-// 65536 (4096 samples at 8192 rows).  One launch per second of 8192 utterances (a 46 GB plan
-// buffer) was measured no faster than 11 launches (302.7 vs 302.7 M samples/s), so the library
-// keeps the small footprint.
+// Bytes of noise-source plans one call may hold (afs_ctx::plan_budget: 4 GiB, or
+// AFS_PLAN_BUDGET_MB).  Hop mode keeps the hop records of the whole call and the dense records
+// of its mixed hops within it (static vowels: 446 MB of records for 8192 utterances x 1 s) and
+// runs launches of up to afs_ctx::launch_cap samples; the dense path (hops < 32, or past the
+// budget) runs launches of at most plan_budget / (rows * 128 B) samples (4096 at 8192 rows).
+// (Round 2 measured one launch per second with 46 GB of dense records no faster than 11
+// launches; round 4's compact hop-mode plans make the one launch +0.1..0.5 %,
+// profiles/r04h_launch_ab.txt.)
 constexpr int64_t PLAN_BUDGET_DEFAULT = (int64_t)4 << 30;
 
 // Launch the synthesis of frame transitions 1 .. ntrans (frames[row * fstride + k], k = 0 the

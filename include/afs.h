@@ -160,6 +160,15 @@ void afs_config_default(afs_config *cfg);
 const char *afs_status_string(afs_status s);
 int32_t afs_abi_version(void);
 
+/* Environment read by afs_create (studies and A/B runs; the defaults are the measured best):
+ *   AFS_PLAN_DENSE=1        every hop reads K5's dense per-sample records (bit-exact plan, below)
+ *   AFS_PLAN_BUDGET_MB=N    noise-plan memory per call (default 4096); past it the call runs in
+ *                           launches of at most N MB of plans
+ *   AFS_LAUNCH_SAMPLES=N    samples per synthesis-kernel launch at most (default 65536; the state
+ *                           crosses launches, the audio is the same bit for bit)
+ *   AFS_XCD_ORDER=0         shared trajectories (target sequences) in utterance order instead of
+ *                           the XCD-aware order
+ *   AFS_PLAN_OVERLAP=1      chunked path: K5 of the next launch beside K1 of this one */
 afs_status afs_create(afs_ctx **ctx, const afs_config *cfg);
 void afs_destroy(afs_ctx *ctx);
 const char *afs_last_error(const afs_ctx *ctx);
