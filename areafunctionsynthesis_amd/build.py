@@ -36,7 +36,11 @@ HEADERS = ["afs_model.h", "afs_ctx.h", "afs_gather.h", "afs_af.h", "afs_lane.h",
 # end (A/B alternated, profiles/r03k_sched_ab.txt; iterative-minreg -16 %, post-RA machine
 # scheduler / no machine sinking / no memop clustering neutral or slower).  Instruction order
 # only: the results are bit-identical.
-TREE_FLAGS = ["-mllvm", "-disable-machine-licm", "-ffp-contract=fast-honor-pragmas", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+# -fno-signed-zeros: the reference's accumulations from 0.0 (`double u = 0.0; u += x;`, ~35 per
+# sample) are kept as written in the source and compile to x; they differ from x only for x = -0,
+# and no comparison, product or sum in this kernel tells -0 from +0 except in a zero result (no
+# division by a possibly-zero value, no copysign).  A/B: profiles/r04n_nsz_ab.txt.
+TREE_FLAGS = ["-mllvm", "-disable-machine-licm", "-ffp-contract=fast-honor-pragmas", "-fno-signed-zeros", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 PER_SOURCE: dict = {"tds_tree.hip": list(TREE_FLAGS)}
 # (AFS_TREE_FLAGS: extra compiler flags for the tree kernel, for A/B builds of scheduler options)
 if os.environ.get("AFS_TREE_FLAGS"):

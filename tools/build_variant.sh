@@ -10,7 +10,7 @@ C=areafunctionsynthesis_amd/csrc
 O=/tmp/afs_variant_$TAG
 mkdir -p $O
 # the tree kernel's flags as build.py TREE_FLAGS (TREE_BASE overrides them, TREE_EXTRA adds)
-TREE_BASE=${TREE_BASE:-"-mllvm -disable-machine-licm -ffp-contract=fast-honor-pragmas -mllvm -amdgpu-sched-strategy=iterative-ilp"}
+TREE_BASE=${TREE_BASE:-"-mllvm -disable-machine-licm -ffp-contract=fast-honor-pragmas -fno-signed-zeros -mllvm -amdgpu-sched-strategy=iterative-ilp"}
 COMMON="-O3 -std=c++17 -fPIC -Wall -Wno-unused-function -ffp-contract=off -fno-strict-aliasing -Wno-unknown-pragmas --offload-arch=gfx950 $FLAGS"
 objs=""
 for s in afs_capi.cpp afs_comm.cpp afs_tables.cpp tds_lane.hip tds_tree.hip tds_plan.hip af_kernels.hip audio_kernels.hip; do

@@ -9,7 +9,7 @@ C=areafunctionsynthesis_amd/csrc
 OUT=${ISA_OUT:-/tmp/isa_phase}
 mkdir -p $OUT
 /opt/rocm/bin/hipcc -S --cuda-device-only -x hip tools/phase_prof/phase_prof.hip -o $OUT/pp.s --offload-arch=gfx950 \
-  -O3 -std=c++17 -fPIC -fno-strict-aliasing -Wno-unknown-pragmas -mllvm -disable-machine-licm \
+  -O3 -std=c++17 -fPIC -fno-strict-aliasing -Wno-unknown-pragmas -fno-signed-zeros -mllvm -disable-machine-licm \
   -ffp-contract=fast-honor-pragmas -mllvm -amdgpu-sched-strategy=iterative-ilp -I$C -Iinclude "$@" 2>/dev/null
 python3 - "$OUT/pp.s" <<'PY'
 import re, sys
