@@ -145,7 +145,31 @@ __global__ void target_frames_kernel(const double *seq, int Q, TargetPlan t, int
   for (int j = 0; j < 6; ++j) fr->glottis[j] = gp[j];
 }
 
+// The shape key of utterance u (shape_order, afs_capi.cpp): where its first frame's tube is
+// narrowest (section index, high word) and how narrow (the area as a float's bits, low word:
+// positive floats order as their bits).  A NaN area counts as wide.
+__global__ void utterance_key_kernel(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= B) return;
+  const afs_frame *f = frames + (int64_t)u * fstride;
+  double amin = 1.0e30;
+  int imin = 0;
+  for (int m = 0; m < AFS_NUM_TUBE_SECTIONS; ++m) {
+    const double a = f->area_cm2[m];
+    if (a < amin) { amin = a; imin = m; }
+  }
+  const float af = amin > 0.0 ? (float)amin : 0.0f;
+  keys[u] = ((uint64_t)imin << 32) | (uint64_t)__float_as_uint(af);
+}
+
 }  // namespace
+
+hipError_t launch_utterance_keys(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(utterance_key_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, frames, fstride, B,
+                     keys);
+  return hipGetLastError();
+}
 
 hipError_t launch_af_to_frames(const double *params, int64_t n, afs_frame *frames, hipStream_t st) {
   if (n <= 0) return hipSuccess;

@@ -422,6 +422,7 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   if (const char *e = std::getenv("AFS_PLAN_OVERLAP")) ctx->overlap = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_PLAN_DENSE")) ctx->plan_dense = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_XCD_ORDER")) ctx->xcd_order = std::atoi(e) != 0;
+  if (const char *e = std::getenv("AFS_SHAPE_ORDER")) ctx->shape_order = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_LAUNCH_SAMPLES")) {  // (A/B and latency studies: samples per K1 launch)
     const long long v = std::atoll(e);
     if (v > 0) ctx->launch_cap = std::min<int64_t>(v, 65536);
@@ -452,6 +453,7 @@ void afs_destroy(afs_ctx *c) {
   if (c->stage_out) (void)hipFree(c->stage_out);
   if (c->stage_seeds) (void)hipFree(c->stage_seeds);
   if (c->tgt) (void)hipFree(c->tgt);
+  if (c->keys) (void)hipFree(c->keys);
   if (c->plan_stream) (void)hipStreamSynchronize(c->plan_stream);
   if (c->plan) (void)hipFree(c->plan);
   if (c->plan2) (void)hipFree(c->plan2);
@@ -490,6 +492,39 @@ afs_status afs_synchronize(afs_ctx *c) {
 
 }  // extern "C"
 
+// Slot order of the 16-lane tree kernel for a batch of independent utterances: sorted by the shape
+// key of their first frame (where and how narrow the tube is: launch_utterance_keys), so that the
+// four utterances of a wave -- which run in lockstep and pay for the union of their branches
+// (noise sources, the cutoff filter's exponential, mixed hops) -- and the blocks of a compute unit
+// play alike shapes.  Each utterance's audio is the same in any slot.  Measured on the config-4
+// shard sorted by vowel: K1 -1.4 % (static vowels), -1.1 % (fricatives),
+// profiles/r04r_order_study.txt.  One key kernel, a 64-KB read-back and a host sort per call; off
+// for the voice kernel (one utterance per wave), batches of one block and AFS_SHAPE_ORDER=0.
+static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstride, int B, int width,
+                              const int32_t **dord) {
+  *dord = nullptr;
+  const int upb = 4 * afs::TREE_WPB;
+  if (!tree(c) || !c->shape_order || width == afs::TREE_VOICE_W || B <= upb) return AFS_OK;
+  const int nb = (B + upb - 1) / upb;
+  const size_t kbytes = (size_t)B * sizeof(uint64_t), obytes = (size_t)nb * upb * sizeof(int32_t);
+  afs_status s;
+  if ((s = ensure(c, &c->keys, &c->keys_bytes, kbytes + obytes)) != AFS_OK) return s;
+  uint64_t *dkeys = (uint64_t *)c->keys;
+  int32_t *dorder = (int32_t *)((char *)c->keys + kbytes);
+  HIP_TRY(c, afs::launch_utterance_keys(dframes, fstride, B, dkeys, c->stream));
+  c->hkeys.resize((size_t)B);
+  HIP_TRY(c, hipMemcpyAsync(c->hkeys.data(), dkeys, kbytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  std::vector<int32_t> idx((size_t)B);
+  for (int u = 0; u < B; ++u) idx[(size_t)u] = u;
+  std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) { return c->hkeys[(size_t)a] < c->hkeys[(size_t)b]; });
+  c->horder.assign((size_t)nb * upb, B);
+  for (int q = 0; q < B; ++q) c->horder[(size_t)q] = idx[(size_t)q];
+  HIP_TRY(c, hipMemcpyAsync(dorder, c->horder.data(), obytes, hipMemcpyHostToDevice, c->stream));
+  *dord = dorder;
+  return AFS_OK;
+}
+
 // afs_synthesize; force_async: leave the stream running unless a host buffer needs a wait
 static afs_status synth_core(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B, int32_t F,
                              int32_t hop, double *out, uint8_t *nonfinite, afs_report *rep, bool force_async) {
@@ -527,7 +562,10 @@ static afs_status synth_core(afs_ctx *c, const afs_frame *frames, const uint32_t
     return s;
   if ((s = reset_state(c, c->ws, c->rng, c->tree_lanes, bp, B, dseeds, width)) != AFS_OK) return s;
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-  if ((s = run_chunks(c, dframes, F, B, F - 1, hop, dout, T, c->ws, c->rng, c->tree_lanes, bp, B, width)) != AFS_OK)
+  const int32_t *dord = nullptr;
+  if ((s = shape_order(c, dframes, F, B, width, &dord)) != AFS_OK) return s;
+  if ((s = run_chunks(c, dframes, F, B, F - 1, hop, dout, T, c->ws, c->rng, c->tree_lanes, bp, B, width, nullptr,
+                      dord)) != AFS_OK)
     return s;
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   c->last_B = B;

@@ -45,6 +45,11 @@ struct afs_ctx {
   bool plan_dense = false;             // AFS_PLAN_DENSE=1: dense records at every hop (A/B, tests)
   bool xcd_order = true;               // AFS_XCD_ORDER=0: shared trajectories in utterance order (A/B)
   int64_t launch_cap = 65536;          // samples per K1 launch at most (AFS_LAUNCH_SAMPLES lowers it)
+  bool shape_order = true;             // AFS_SHAPE_ORDER=0: afs_synthesize's utterances in call order
+  void *keys = nullptr;                // shape keys (device) and the slot order built from them
+  size_t keys_bytes = 0;
+  std::vector<uint64_t> hkeys;
+  std::vector<int32_t> horder;
   hipStream_t plan_stream = nullptr;  // K5 of the next launch, beside K1 of this one (overlap)
   bool overlap = false;                // AFS_PLAN_OVERLAP=1 (afs_capi.cpp run_chunks)
   hipEvent_t ev_go = nullptr, ev_plan[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};

@@ -168,6 +168,9 @@ int32_t afs_abi_version(void);
  *                           crosses launches, the audio is the same bit for bit)
  *   AFS_XCD_ORDER=0         shared trajectories (target sequences) in utterance order instead of
  *                           the XCD-aware order
+ *   AFS_SHAPE_ORDER=0       afs_synthesize's utterances in call order in the 16-lane kernel's
+ *                           slots instead of sorted by the shape of their first frame (the audio
+ *                           of each utterance is the same either way)
  *   AFS_PLAN_OVERLAP=1      chunked path: K5 of the next launch beside K1 of this one */
 afs_status afs_create(afs_ctx **ctx, const afs_config *cfg);
 void afs_destroy(afs_ctx *ctx);
