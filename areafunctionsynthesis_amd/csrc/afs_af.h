@@ -29,8 +29,8 @@ struct TargetPlan {
 hipError_t launch_target_frames(const double *seq, int Q, const TargetPlan &plan, int64_t k0, int n,
                                 int64_t fstride, afs_frame *frames, hipStream_t st);
 
-// keys[u] = the shape key of utterance u's first frame frames[u * fstride] (where and how narrow
-// its tube is), for the slot order of the tree kernel (afs_capi.cpp shape_order).
+// keys[u] = the shape key of utterance u's first frame frames[u * fstride] (how narrow its tube is
+// and where), for the slot order of the tree kernel (afs_capi.cpp shape_order).
 hipError_t launch_utterance_keys(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, hipStream_t st);
 
 }  // namespace afs

@@ -493,13 +493,14 @@ afs_status afs_synchronize(afs_ctx *c) {
 }  // extern "C"
 
 // Slot order of the 16-lane tree kernel for a batch of independent utterances: sorted by the shape
-// key of their first frame (where and how narrow the tube is: launch_utterance_keys), so that the
+// key of their first frame (how narrow the tube is and where: launch_utterance_keys), so that the
 // four utterances of a wave -- which run in lockstep and pay for the union of their branches
 // (noise sources, the cutoff filter's exponential, mixed hops) -- and the blocks of a compute unit
-// play alike shapes.  Each utterance's audio is the same in any slot.  Measured on the config-4
-// shard sorted by vowel: K1 -1.4 % (static vowels), -1.1 % (fricatives),
-// profiles/r04r_order_study.txt.  One key kernel, a 64-KB read-back and a host sort per call; off
-// for the voice kernel (one utterance per wave), batches of one block and AFS_SHAPE_ORDER=0.
+// play alike shapes, the heaviest (narrowest constrictions) first.  Each utterance's audio is the
+// same in any slot.  Config-4 shard: +2.7 % static vowels, +1.4 % fricatives against the call order
+// (profiles/r04s_shape_order_ab.txt, r04v_shape_key_ab.txt).  One key kernel, a 64-KB read-back and
+// a host sort per call; off for the voice kernel (one utterance per wave), batches of one block and
+// AFS_SHAPE_ORDER=0.
 static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstride, int B, int width,
                               const int32_t **dord) {
   *dord = nullptr;

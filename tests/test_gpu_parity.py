@@ -201,6 +201,31 @@ def test_launch_split_is_bitwise(oracle, solver, monkeypatch):
     assert np.isfinite(ys[0]).all()
 
 
+def test_slot_order_is_invisible(oracle, monkeypatch):
+    """afs_synthesize places a batch's utterances in the 16-lane kernel's slots sorted by the shape
+    of their first frame (afs_capi.cpp shape_order); each utterance's audio is the same wherever it
+    runs: a permuted batch gives the permuted audio bit for bit, and so does the call order
+    (AFS_SHAPE_ORDER=0)."""
+    from areafunctionsynthesis_amd.synthesizer import Context
+    names = ("a:", "i:", "s", "u:", "S", "e:", "f", "o:")
+    B = 40  # (three blocks of 16 utterances)
+    frames = np.stack([static_frames(oracle, names[u % len(names)], 4, velum=0.5 * (u % 3 == 0)) for u in range(B)])
+    seeds = np.arange(100, 100 + B, dtype=np.uint32)
+    perm = np.random.default_rng(5).permutation(B)
+    ys = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("AFS_SHAPE_ORDER", env)
+        ctx = Context(44100.0, solver="tree", lanes=16)
+        try:
+            ys[env] = ctx.synthesize(frames, 441, seeds=seeds)
+            yp = ctx.synthesize(np.ascontiguousarray(frames[perm]), 441, seeds=seeds[perm])
+        finally:
+            ctx.close()
+        assert np.array_equal(yp, ys[env][perm])
+    assert np.array_equal(ys["1"], ys["0"])
+    assert np.isfinite(ys["1"]).all()
+
+
 @pytest.mark.parametrize("solver", SOLVERS)
 def test_edge_cases(contexts, oracle, solver):
     ctx = contexts(44100.0, solver)
