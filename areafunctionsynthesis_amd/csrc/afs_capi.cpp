@@ -1033,8 +1033,8 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
   if (tree(c) && c->xcd_order) {
     const int upb = width == afs::TREE_VOICE_W ? 1 : 4 * afs::TREE_WPB;
     // blocks the GPU holds at once: the voice kernel one wave (block) per SIMD, the throughput
-    // kernel one block per CU (its LDS)
-    const int conc = width == afs::TREE_VOICE_W ? c->simds : c->simds / 4;
+    // kernel one wave per SIMD in blocks of TREE_WPB waves (4 / TREE_WPB blocks per CU, its LDS)
+    const int conc = width == afs::TREE_VOICE_W ? c->simds : c->simds / afs::TREE_WPB;
     order = xcd_order(row, B, upb, conc);
   }
   const size_t seq_bytes = seq.size() * sizeof(double);

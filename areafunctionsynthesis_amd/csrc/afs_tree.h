@@ -70,7 +70,10 @@ inline int64_t plan_work_bytes(int64_t rows, int64_t slots) { return (rows * slo
 #define AFS_TREE_W 16
 #endif
 #ifndef AFS_TREE_WPB
-#define AFS_TREE_WPB 4
+// waves per block of the throughput kernel: 2 (8 utterances, 78 KB of LDS: two blocks per CU).  With
+// the slot order by shape, finer blocks balance the compute units' two rounds better: +0.6 % static
+// vowels against 4 (profiles/r04ab_wpb_ab.txt; without the order it measured neutral, r04p)
+#define AFS_TREE_WPB 2
 #endif
 #ifndef AFS_TREE_MIN_WAVES
 #define AFS_TREE_MIN_WAVES 1  // waves per SIMD the register allocation must allow
