@@ -111,10 +111,6 @@ typedef struct afs_options {
   double flow_separation_area_ratio; /* 1.0 */
 } afs_options;
 
-/* Return once the work is queued (device buffers only).  A call still waits on the host for the
- * small read-backs it needs to size or order its launches -- the noise-plan work list of the hop
- * path and the shape keys of the slot order (a few microseconds of device work each) -- so the
- * device may be idle between calls for that long. */
 #define AFS_ASYNC 0x1u
 /* Record an event pair around every kernel launch of the synthesis calls; afs_kernel_times
  * returns their summed durations (measurement only: a few microseconds per launch). */
