@@ -48,6 +48,16 @@ bool is_device_ptr(const void *p) {
   return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
 }
 
+// Lanes per utterance of the tree kernel for a batch of B: forced by AFS_LANES_16 / AFS_LANES_64,
+// else the voice kernel (64 lanes, one utterance per wave: fewer instructions per sample on the
+// chain) while the batch leaves SIMDs idle with 16 lanes per utterance (B <= the GPU's SIMDs), the
+// throughput kernel (16 lanes, four utterances per wave) above.
+int lanes_for(const afs_ctx *c, int64_t B) {
+  if (c->cfg.flags & AFS_LANES_16) return TREE_W;
+  if (c->cfg.flags & AFS_LANES_64) return TREE_VOICE_W;
+  return B <= c->simds ? TREE_VOICE_W : TREE_W;
+}
+
 afs_status ensure(afs_ctx *c, void **buf, size_t *cap, size_t bytes) {
   if (bytes <= *cap) return AFS_OK;
   if (*buf) (void)hipFree(*buf);
@@ -63,6 +73,7 @@ afs_status ensure(afs_ctx *c, void **buf, size_t *cap, size_t bytes) {
 using afs::ensure;
 using afs::fail;
 using afs::is_device_ptr;
+using afs::lanes_for;
 
 namespace {
 
@@ -73,15 +84,6 @@ bool solver_ok(int32_t s) { return s == AFS_SOLVER_CHOLESKY || s == AFS_SOLVER_T
 // the cooperative kernel (noise-source plans from K5)
 bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE; }
 
-// Lanes per utterance of the tree kernel for a batch of B: forced by AFS_LANES_16 / AFS_LANES_64,
-// else the voice kernel (64 lanes, one utterance per wave: fewer instructions per sample on the
-// chain) while the batch leaves SIMDs idle with 16 lanes per utterance (B <= the GPU's SIMDs), the
-// throughput kernel (16 lanes, four utterances per wave) above.
-int lanes_for(const afs_ctx *c, int64_t B) {
-  if (c->cfg.flags & AFS_LANES_16) return afs::TREE_W;
-  if (c->cfg.flags & AFS_LANES_64) return afs::TREE_VOICE_W;
-  return B <= c->simds ? afs::TREE_VOICE_W : afs::TREE_W;
-}
 
 // Bytes of noise-source plans one call may hold (afs_ctx::plan_budget: 4 GiB, or
 // AFS_PLAN_BUDGET_MB).  Hop mode keeps the hop records of the whole call and the dense records
@@ -231,15 +233,26 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     // chunk k - 1 has read that buffer, K1 of chunk k waits for its plans.  K5 (80 VGPRs, 4 KB of
     // LDS per block) fits beside K1's wave, but the measured gain (+1.4 %) came with runs where K1
     // slowed by 9 % beside it, so the default is sequential.
-    const int64_t per = std::max<int64_t>(1, std::min<int64_t>({S, c->launch_cap, c->plan_budget / ((int64_t)rows * afs::PLAN_RECORD_BYTES)}));
+    // Dense records: `per` samples per row.  Hop mode: the compact dense records of the chunk's
+    // listed hops, slot e of the work list holding `hop` records, and every hop the chunk spans may
+    // be listed -- rows x hstride slots of hop records, hstride = the chunk's hop slots + 1 (a chunk
+    // may start inside a hop).  Chunks of whole hops are sized so that this worst case fits the
+    // budget (at least one hop per chunk: past that the budget is exceeded, not the buffer).
+    int64_t per = std::min<int64_t>(S, c->launch_cap);
+    if (hops) {
+      const int64_t slots_fit = c->plan_budget / ((int64_t)rows * hop * afs::PLAN_RECORD_BYTES) - 1;
+      per = std::min<int64_t>(per, std::max<int64_t>(1, slots_fit) * hop);
+    } else {
+      per = std::min<int64_t>(per, c->plan_budget / ((int64_t)rows * afs::PLAN_RECORD_BYTES));
+    }
+    per = std::max<int64_t>(1, per);
     const int64_t nch = (S + per - 1) / per;
-    // (hop mode: compact dense records, at most every hop the chunk touches: rows x (per + hop))
-    const size_t pbytes = (size_t)rows * (size_t)(per + (hops ? hop : 0)) * afs::PLAN_RECORD_BYTES;
+    const int64_t hstride = afs::plan_hop_slots(0, per, hop) + 1;
+    const size_t pbytes = (size_t)rows * (size_t)(hops ? hstride * hop : per) * afs::PLAN_RECORD_BYTES;
     if ((st = ensure(c, &c->plan, &c->plan_bytes, pbytes)) != AFS_OK) return st;
     const bool ov = c->overlap && nch > 1;
     if (ov && (st = ensure(c, &c->plan2, &c->plan2_bytes, pbytes)) != AFS_OK) return st;
     void *buf[2] = {c->plan, ov ? c->plan2 : c->plan};
-    const int64_t hstride = afs::plan_hop_slots(0, per, hop) + 1;  // (a chunk may start inside a hop)
     afs::tree::PlanHop *hbuf[2] = {nullptr, nullptr};
     if (hops) {
       const size_t hbytes = (size_t)rows * (size_t)hstride * sizeof(afs::tree::PlanHop);
@@ -504,7 +517,7 @@ afs_status afs_synchronize(afs_ctx *c) {
 static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstride, int B, int width,
                               const int32_t **dord) {
   *dord = nullptr;
-  const int upb = 4 * afs::TREE_WPB;
+  const int upb = afs::TREE_UPB;
   if (!tree(c) || !c->shape_order || width == afs::TREE_VOICE_W || B <= upb) return AFS_OK;
   const int nb = (B + upb - 1) / upb;
   const size_t kbytes = (size_t)B * sizeof(uint64_t), obytes = (size_t)nb * upb * sizeof(int32_t);
@@ -528,7 +541,8 @@ static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstr
 
 // afs_synthesize; force_async: leave the stream running unless a host buffer needs a wait
 static afs_status synth_core(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B, int32_t F,
-                             int32_t hop, double *out, uint8_t *nonfinite, afs_report *rep, bool force_async) {
+                             int32_t hop, double *out, uint8_t *nonfinite, afs_report *rep, bool force_async,
+                             int lanes = 0) {
   if (!frames || !out || B <= 0 || F < 2 || hop < 1)
     return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_synthesize: need frames, out, batch>0, num_frames>=2, hop>=1");
   HIP_TRY(c, hipSetDevice(c->cfg.device));
@@ -556,7 +570,7 @@ static afs_status synth_core(afs_ctx *c, const afs_frame *frames, const uint32_t
     dout = (double *)c->stage_out;
   }
   // state
-  const int width = lanes_for(c, B);
+  const int width = lanes > 0 ? lanes : lanes_for(c, B);
   if ((s = ensure(c, &c->ws, &c->ws_bytes, ws_bytes_for(c, bp))) != AFS_OK) return s;
   if ((s = ensure(c, (void **)&c->rng, &c->rng_bytes, (size_t)(32 * bp) * sizeof(int32_t))) != AFS_OK) return s;
   if (tree(c) && (s = ensure(c, &c->tree_lanes, &c->tree_lanes_bytes, lanes_bytes_for(c, bp, width))) != AFS_OK)
@@ -587,8 +601,10 @@ static afs_status synth_core(afs_ctx *c, const afs_frame *frames, const uint32_t
 }
 
 afs_status afs::synthesize_async(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B, int32_t F,
-                                 int32_t hop, double *out, uint8_t *nonfinite) {
-  return synth_core(c, frames, seeds, B, F, hop, out, nonfinite, nullptr, true);
+                                 int32_t hop, double *out, uint8_t *nonfinite, int lanes) {
+  if (lanes != 0 && lanes != afs::TREE_W && lanes != afs::TREE_VOICE_W)
+    return fail(c, AFS_ERR_INVALID_ARGUMENT, "synthesize: %d lanes per utterance", lanes);
+  return synth_core(c, frames, seeds, B, F, hop, out, nonfinite, nullptr, true, lanes);
 }
 
 extern "C" {
@@ -1031,7 +1047,7 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
   // tree solver: the XCD-aware slot order of the utterances by trajectory (xcd_order)
   std::vector<int32_t> order;
   if (tree(c) && c->xcd_order) {
-    const int upb = width == afs::TREE_VOICE_W ? 1 : 4 * afs::TREE_WPB;
+    const int upb = width == afs::TREE_VOICE_W ? 1 : afs::TREE_UPB;
     // blocks the GPU holds at once: the voice kernel one wave (block) per SIMD, the throughput
     // kernel one wave per SIMD in blocks of TREE_WPB waves (4 / TREE_WPB blocks per CU, its LDS)
     const int conc = width == afs::TREE_VOICE_W ? c->simds : c->simds / afs::TREE_WPB;

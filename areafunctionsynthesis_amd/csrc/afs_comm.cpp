@@ -357,6 +357,10 @@ afs_status afs_multi_synthesize(afs_ctx *const *ctxs, afs_comm *const *comms, in
     seeds = gseeds.data();
   }
   afs_status s;
+  // one kernel width for every shard, chosen for the whole batch: the two widths agree within the
+  // parity tolerances but not bit for bit, so a width chosen per shard would make the audio depend
+  // on the GPU count
+  const int lanes = c0->cfg.solver == AFS_SOLVER_TREE ? afs::lanes_for(c0, B) : 0;
   std::vector<int64_t> first((size_t)n), cnt((size_t)n);
   for (int i = 0; i < n; ++i) {
     afs_ctx *c = ctxs[i];
@@ -370,7 +374,7 @@ afs_status afs_multi_synthesize(afs_ctx *const *ctxs, afs_comm *const *comms, in
     if ((s = afs::ensure(c, &c->m_nf, &c->m_nf_bytes, (size_t)b)) != AFS_OK) return s;
     // (queued on this device's stream; the host moves on to the next device)
     if ((s = afs::synthesize_async(c, frames + first[(size_t)i] * F, seeds + first[(size_t)i], (int32_t)b, F, hop,
-                                   (double *)c->m_out, (uint8_t *)c->m_nf)) != AFS_OK)
+                                   (double *)c->m_out, (uint8_t *)c->m_nf, lanes)) != AFS_OK)
       return s;
     HIP_TRY(c, afs::launch_to_int16((const double *)c->m_out, (int16_t *)c->m_pcm, b * T, c->stream));
   }

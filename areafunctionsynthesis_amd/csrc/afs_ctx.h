@@ -91,10 +91,13 @@ namespace afs {
 afs_status fail(afs_ctx *c, afs_status s, const char *fmt, ...);
 bool is_device_ptr(const void *p);
 afs_status ensure(afs_ctx *c, void **buf, size_t *cap, size_t bytes);
-// afs_synthesize with the call's synchronisation left to the caller (no host wait unless a
-// host buffer needs it)
+// afs_synthesize queued without a host wait (unless host buffers need one), with the tree solver's
+// lanes per utterance fixed by the caller (lanes > 0; afs_multi_synthesize: the global batch's, so
+// that a shard's audio does not depend on the GPU count) or chosen for B (lanes = 0)
 afs_status synthesize_async(afs_ctx *c, const afs_frame *frames, const uint32_t *seeds, int32_t B, int32_t F,
-                            int32_t hop, double *out, uint8_t *nonfinite);
+                            int32_t hop, double *out, uint8_t *nonfinite, int lanes = 0);
+// the lanes per utterance of the tree kernel for a batch of B (AFS_LANES_* or the library's choice)
+int lanes_for(const afs_ctx *c, int64_t B);
 
 }  // namespace afs
 

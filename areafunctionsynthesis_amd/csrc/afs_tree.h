@@ -81,6 +81,7 @@ inline int64_t plan_work_bytes(int64_t rows, int64_t slots) { return (rows * slo
 constexpr int TREE_W = AFS_TREE_W;      // lanes per utterance of the throughput kernel (16)
 constexpr int TREE_WPB = AFS_TREE_WPB;  // its waves per block
 constexpr int TREE_VOICE_W = 64;        // lanes per utterance of the voice kernel (one utterance per wave)
+constexpr int TREE_UPB = (64 / TREE_W) * TREE_WPB;  // utterances per block of the throughput kernel
 // Lanes per utterance: TREE_W or TREE_VOICE_W (the per-lane state layout, Lane<lanes>, differs).
 int64_t tree_lane_bytes(int lanes);
 int64_t tree_lds_doubles();

@@ -41,6 +41,7 @@ struct Geom {
 constexpr int UPW = Geom<TW>::UPW;
 constexpr int WPB = Geom<TW>::WPB;
 constexpr int UPB = Geom<TW>::UPB;
+static_assert(UPB == TREE_UPB, "afs_tree.h TREE_UPB: the host's slot orders group utterances by block");
 
 template <bool PROF, int W = TW>
 struct GpuExec {

@@ -144,8 +144,11 @@ def check_gathered(rows, world: int, per_rank: int, reference: Callable[[Sequenc
     ``rows[i]`` is the gathered row of the i-th entry of :func:`edge_utterances` (``[n, T]``
     int16, any array type with ``numpy()`` or an ndarray); ``reference(us)`` synthesizes the
     global utterances ``us`` (frames of index u, seed u + 1) in one call on rank 0 and returns their
-    int16 audio ``[len(us), T]``.  Bit-for-bit comparison: the shards' audio does not depend on
-    the GPU count, so any difference is a gather (or sharding) fault."""
+    int16 audio ``[len(us), T]`` -- with the lane width the shards ran (the tree kernel's 16- and
+    64-lane builds agree within the parity tolerances, not bit for bit; bench.py passes the
+    shard's width, afs_multi_synthesize fixes one width for the whole batch).  At that width an
+    utterance's audio does not depend on its batch-mates or slot, so any difference in the
+    bit-for-bit comparison is a gather (or sharding) fault."""
     import numpy as np
     edges = edge_utterances(world, per_rank)
     got = rows.numpy() if hasattr(rows, "numpy") else np.asarray(rows)

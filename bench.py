@@ -2,7 +2,9 @@
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--seconds S] [--fs HZ]
                 [--workload static|fricatives|vcv]
-For N > 1 launch with torch.distributed.run (one rank per GPU).
+For N > 1 either run `python bench.py --gpus N` (it starts the N ranks itself: a child
+torch.distributed.run, one rank per GPU) or launch it under torch.distributed.run with --gpus
+equal to WORLD_SIZE (anything else is refused).
 
 One *step* = one pass of the hot path over this rank's shard of the BASELINE config-4 batch:
 B static-vowel utterances (default 8192 per GPU; 65536 at 8 GPUs) of S seconds at fs Hz, from
@@ -383,7 +385,9 @@ def cpu_leg(args, m: Measured, n: int):
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node; default: WORLD_SIZE, else 1.  Without WORLD_SIZE, "
+                         "--gpus N > 1 starts the N ranks itself (torch.distributed.run as a child process)")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=8192, help="utterances per GPU")
@@ -407,19 +411,51 @@ def main() -> None:
     ap.add_argument("--one-device", action="store_true",
                     help="N > 1: every rank on device 0 (test of the multi-process path on a one-GPU box)")
     ap.add_argument("--sub-cpu-utterances", type=int, default=16)
+    ap.add_argument("--pg-timeout", type=float, default=300.0,
+                    help="N > 1: seconds a rank waits in a control-plane collective before failing")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="N > 1 test option: start the ranks and the process group, print the world, no GPU work")
+    ap.add_argument("--fail-rank", type=int, default=None,
+                    help="N > 1 test option: this rank raises after the process group is up")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        # `python bench.py --gpus N`: start the N ranks ourselves, as a child torch.distributed.run,
+        # before this process makes any GPU call (none follows either)
+        sys.exit(_launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import datetime
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=args.pg_timeout))
+        if args.fail_rank == rank:
+            raise RuntimeError(f"bench.py: rank {rank} fails on request (--fail-rank)")
+        if args.launch_check:
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            if rank == 0:
+                print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_reporting": int(t.item())}),
+                      flush=True)
+            dist.barrier()
+            dist.destroy_process_group()
+            return
     if args.one_device:
         local = 0
+    elif torch.cuda.device_count() < world:  # (counting devices initialises no GPU)
+        print(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPUs", file=sys.stderr)
+        sys.exit(3)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -516,6 +552,25 @@ def main() -> None:
         comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _launch_ranks(n: int) -> int:
+    """Run this command as N ranks: `python -m torch.distributed.run --nproc-per-node N bench.py
+    <the same arguments>` in a child process (never an exec: this process stays GPU-free), rank 0's
+    JSON line reaching our stdout through the inherited descriptor.  torch.distributed.run ends
+    every rank when one fails, so a failing rank makes the whole command exit non-zero; the
+    return code is the child's."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, env=env)
+    return r.returncode
 
 
 class _NoGather:

@@ -201,6 +201,42 @@ def test_launch_split_is_bitwise(oracle, solver, monkeypatch):
     assert np.isfinite(ys[0]).all()
 
 
+def test_plan_budget_chunked_hop_mode(oracle, monkeypatch):
+    """The hop-mode fallback for calls whose plans exceed the budget (AFS_PLAN_BUDGET_MB): launches
+    of whole hops, each with its own K5 pass and the compact dense records of its listed hops sized
+    for the worst case (every hop of the chunk listed).  Frame-rate VCV trajectories list and mix
+    many hops.  Chunks of whole hops decide every hop exactly as the single call does: bit for bit
+    equal.  Chunks that start inside hops (AFS_LAUNCH_SAMPLES=300 with hop 441) decide partial hops,
+    so a hop mixed in the whole call may be uniform in a part (hop-record words instead of dense
+    records: a few ulps), checked against the single call within 1e-7 (as hop vs dense records)."""
+    from areafunctionsynthesis_amd.synthesizer import Context
+    from areafunctionsynthesis_amd.workloads import build_frames, vcv
+    w = vcv(64, fs=44100.0)
+    ys = {}
+    for label, env in (("single", {}), ("chunks", {"AFS_PLAN_BUDGET_MB": "1"}),
+                       ("straddle", {"AFS_PLAN_BUDGET_MB": "1", "AFS_LAUNCH_SAMPLES": "300"})):
+        for k in ("AFS_PLAN_BUDGET_MB", "AFS_LAUNCH_SAMPLES"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        ctx = Context(44100.0, solver="tree", lanes=16, profile=True)
+        try:
+            frames = build_frames(w, ctx.af_to_frames)
+            if label == "single":
+                hops, _ = ctx.noise_plan_hops(frames, w.hop)
+                mixed = int(np.count_nonzero(hops[..., 528:532].view(np.uint32)))
+                assert mixed > 0
+            ys[label] = ctx.synthesize(frames, w.hop, seeds=w.seeds)
+            kt = ctx.kernel_times()
+        finally:
+            ctx.close()
+        T = (w.num_frames - 1) * w.hop
+        assert kt["synth_launches"] == {"single": 1, "chunks": T // w.hop, "straddle": -(-T // 300)}[label]
+    assert np.isfinite(ys["single"]).all()
+    assert np.array_equal(ys["chunks"], ys["single"])
+    assert np.abs(ys["straddle"] - ys["single"]).max() < 1e-7
+
+
 def test_slot_order_is_invisible(oracle, monkeypatch):
     """afs_synthesize places a batch's utterances in the 16-lane kernel's slots sorted by the shape
     of their first frame (afs_capi.cpp shape_order); each utterance's audio is the same wherever it

@@ -83,25 +83,44 @@ def test_multi_synthesize_equals_single_device(oracle):
     ctx.close()
 
 
+def test_multi_synthesize_lane_width_of_the_whole_batch(oracle):
+    """afs_multi_synthesize runs every shard at the lane width chosen for the whole batch (the two
+    widths agree within the tolerances, not bit for bit, so a per-shard choice would make the audio
+    depend on the GPU count): a batch above the SIMD count gives the 16-lane kernel's audio, one
+    below it the 64-lane kernel's, bit for bit."""
+    from areafunctionsynthesis_amd.synthesizer import Context, Node
+    F, hop = 3, 64
+    node = Node(44100.0, [0])
+    try:
+        for B, lanes in ((1030, 16), (9, 64)):
+            frames = _frames(oracle, B, F)
+            ctx = Context(44100.0, solver="tree", lanes=lanes)
+            try:
+                assert ctx.lanes_per_utterance(B) == lanes
+                ref = ctx.to_int16(ctx.synthesize(frames, hop))
+            finally:
+                ctx.close()
+            assert np.array_equal(node.synthesize(frames, hop), ref)
+    finally:
+        node.close()
+
+
 def test_bench_world2_gather_check_one_device():
-    """bench.py's multi-process path end to end at world size 2 (torch.distributed.run, both ranks
-    on this box's one GPU, the int16 blocks through gloo instead of RCCL): shards, the max-over-ranks
-    timing, and the self-check of the exchange -- rank 0 re-synthesizes the first and last utterance
-    of both blocks alone and finds the gathered rows bit for bit equal."""
+    """bench.py's multi-process path end to end at world size 2, started as the driver starts it
+    (`python bench.py --gpus 2 ...`, no torch.distributed.run in the command: bench.py starts the
+    ranks), both ranks on this box's one GPU, the int16 blocks through gloo instead of RCCL: shards,
+    the max-over-ranks timing, and the self-check of the exchange -- rank 0 re-synthesizes the first
+    and last utterance of both blocks alone and finds the gathered rows bit for bit equal."""
     import json
     import os
-    import socket
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+    cmd = [sys.executable, os.path.join(root, "bench.py"),
            "--gpus", "2", "--steps", "1", "--warmup", "1", "--batch", "24", "--seconds", "0.05",
            "--no-cpu-baseline", "--gather-transport", "gloo", "--one-device"]
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
