@@ -94,6 +94,9 @@ bool tree(const afs_ctx *c) { return c->cfg.solver == AFS_SOLVER_TREE; }
 // launches; round 4's compact hop-mode plans make the one launch +0.1..0.5 %,
 // profiles/r04h_launch_ab.txt.)
 constexpr int64_t PLAN_BUDGET_DEFAULT = (int64_t)4 << 30;
+// Hop mode: calls whose dense records fit this many bytes even with every hop listed skip the
+// read-back of K5's work-list length (run_chunks).
+constexpr int64_t SMALL_CALL_DENSE_BYTES = (int64_t)64 << 20;
 
 // Launch the synthesis of frame transitions 1 .. ntrans (frames[row * fstride + k], k = 0 the
 // latched frame) in chunks that keep each kernel well below a second; state is carried
@@ -204,9 +207,16 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, 0, S, nullptr, 0, two, uo, hbuf, hstride, work, true};
       hipEvent_t e0 = prof_event(c);
       HIP_TRY(c, afs::launch_plan_hops_iv(pa, c->stream));
-      HIP_TRY(c, hipMemcpyAsync(c->hcount, work, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(c, hipStreamSynchronize(c->stream));  // (the list's length sizes the dense records)
-      const int64_t listed = (int64_t)(uint32_t)*c->hcount;
+      // The list's length sizes the dense records.  When every hop of the call fits them (small
+      // calls: real-time sessions, short batches) they are sized for that worst case and the call
+      // runs without a host wait; otherwise the host reads the length back, waiting for the work
+      // queued so far on the stream (the previous call's kernels included).
+      int64_t listed = (int64_t)rows * call_hops;
+      if (listed * hop * afs::PLAN_RECORD_BYTES > std::min<int64_t>(c->plan_budget, SMALL_CALL_DENSE_BYTES)) {
+        HIP_TRY(c, hipMemcpyAsync(c->hcount, work, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        listed = (int64_t)(uint32_t)*c->hcount;
+      }
       const int64_t dense_bytes = listed * hop * afs::PLAN_RECORD_BYTES;
       if (dense_bytes <= c->plan_budget) {
         if (dense_bytes > 0 && (st = ensure(c, &c->plan, &c->plan_bytes, (size_t)dense_bytes)) != AFS_OK) return st;
@@ -432,6 +442,11 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
     return bail(AFS_ERR_OUT_OF_MEMORY);
   *ctx->hcount = 0;
   if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return bail(AFS_ERR_HIP);
+  // the code objects of the kernels a synthesis call launches, loaded now rather than at their
+  // first launch (which cost a real-time caller's first buffer ~35 ms)
+  if (afs::preload_tree_kernels() != hipSuccess || afs::preload_plan_kernels() != hipSuccess ||
+      afs::preload_audio_kernels() != hipSuccess)
+    return bail(AFS_ERR_HIP);
   if (const char *e = std::getenv("AFS_PLAN_OVERLAP")) ctx->overlap = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_PLAN_DENSE")) ctx->plan_dense = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_XCD_ORDER")) ctx->xcd_order = std::atoi(e) != 0;
@@ -812,6 +827,8 @@ afs_status afs_session_create(afs_ctx *c, int32_t B, const uint32_t *seeds, afs_
   if (tree(c) && (e = hipMalloc(&s->tree_lanes, lanes_bytes_for(c, s->bp, s->lanes))) != hipSuccess) return bail(e);
   if ((e = hipMalloc((void **)&s->pair, (size_t)B * 2 * sizeof(afs_frame))) != hipSuccess) return bail(e);
   if ((e = hipMalloc((void **)&s->seeds, (size_t)B * sizeof(uint32_t))) != hipSuccess) return bail(e);
+  if ((e = hipHostMalloc((void **)&s->hframes, (size_t)B * sizeof(afs_frame), hipHostMallocDefault)) != hipSuccess)
+    return bail(e);
   *out = s;
   afs_status st = afs_session_reset(s, seeds);
   if (st != AFS_OK) {
@@ -844,6 +861,8 @@ void afs_session_destroy(afs_session *s) {
   if (s->tree_lanes) (void)hipFree(s->tree_lanes);
   if (s->pair) (void)hipFree(s->pair);
   if (s->seeds) (void)hipFree(s->seeds);
+  if (s->hframes) (void)hipHostFree(s->hframes);
+  if (s->hout) (void)hipHostFree(s->hout);
   delete s;
 }
 
@@ -853,10 +872,21 @@ afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32
   afs_ctx *c = s->ctx;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   const int B = s->B;
-  hipMemcpyKind k = is_device_ptr(frames) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  // (the kinds of the caller's pointers are probed once per new pointer: a real-time caller
+  // passes the same buffers every call)
+  if (frames != s->last_in) {
+    s->last_in = frames;
+    s->last_in_dev = is_device_ptr(frames);
+  }
+  const afs_frame *src = frames;
+  if (!s->last_in_dev) {  // host frames: through the session's pinned buffer
+    std::memcpy(s->hframes, frames, (size_t)B * sizeof(afs_frame));
+    src = s->hframes;
+  }
+  const hipMemcpyKind k = s->last_in_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   // frames[u] -> pair[u][slot]
   const int slot = s->latched ? 1 : 0;
-  HIP_TRY(c, hipMemcpy2DAsync(s->pair + slot, 2 * sizeof(afs_frame), frames, sizeof(afs_frame),
+  HIP_TRY(c, hipMemcpy2DAsync(s->pair + slot, 2 * sizeof(afs_frame), src, sizeof(afs_frame),
                               sizeof(afs_frame), B, k, c->stream));
   if (!s->latched) {  // Synthesizer.cpp:522-532
     s->latched = true;
@@ -867,12 +897,24 @@ afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32
   }
   if (!out) return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_session_synthesize: out is NULL");
   if (n < 1) n = 1;  // Synthesizer.cpp:543-546
+  if (out != s->last_out) {
+    s->last_out = out;
+    s->last_out_dev = is_device_ptr(out);
+  }
   double *dout = out;
-  const bool host_out = !is_device_ptr(out);
+  const bool host_out = !s->last_out_dev;
+  const size_t nout = (size_t)B * (size_t)n;
   afs_status st;
   if (host_out) {
-    if ((st = ensure(c, &c->stage_out, &c->stage_out_bytes, (size_t)B * n * sizeof(double))) != AFS_OK) return st;
+    if ((st = ensure(c, &c->stage_out, &c->stage_out_bytes, nout * sizeof(double))) != AFS_OK) return st;
     dout = (double *)c->stage_out;
+    if (nout > s->hout_cap) {
+      if (s->hout) (void)hipHostFree(s->hout);
+      s->hout = nullptr;
+      s->hout_cap = 0;
+      HIP_TRY(c, hipHostMalloc((void **)&s->hout, nout * sizeof(double), hipHostMallocDefault));
+      s->hout_cap = nout;
+    }
   }
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
   if ((st = run_chunks(c, s->pair, 2, B, 1, n, dout, n, s->ws, s->rng, s->tree_lanes, s->bp, B, s->lanes)) != AFS_OK)
@@ -883,8 +925,9 @@ afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32
                               sizeof(afs_frame), B, hipMemcpyDeviceToDevice, c->stream));
   bool nf_sync = false;
   if ((st = nonfinite_report(c, s->ws, s->bp, B, nonfinite, rep != nullptr, &nf_sync)) != AFS_OK) return st;
-  if (host_out) HIP_TRY(c, hipMemcpyAsync(out, dout, (size_t)B * n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (host_out) HIP_TRY(c, hipMemcpyAsync(s->hout, dout, nout * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (host_out) std::memcpy(out, s->hout, nout * sizeof(double));
   if (produced) *produced = n;
   if (rep) {
     float ms = 0.f;

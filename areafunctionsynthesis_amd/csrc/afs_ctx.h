@@ -84,6 +84,13 @@ struct afs_session {
   afs_frame *pair = nullptr;   // [B][2]: previous frame, new frame
   uint32_t *seeds = nullptr;   // device copy
   bool latched = false;
+  // pinned staging of host frames and host output (a real-time caller's per-call copies go
+  // through these instead of pageable memory) and the kinds of the caller's last pointers
+  afs_frame *hframes = nullptr;
+  double *hout = nullptr;
+  size_t hout_cap = 0;  // doubles
+  const void *last_in = nullptr, *last_out = nullptr;
+  bool last_in_dev = false, last_out_dev = false;
 };
 
 namespace afs {

@@ -93,6 +93,10 @@ hipError_t launch_tree_synth(const TreeArgs &a, int lanes, hipStream_t st);
 // (out[u * out_stride + s - s_begin], replaced by the audio).
 hipError_t launch_tree_output(const Tables *tab, double *lds_state, double *out, int64_t out_stride, int64_t n, int B,
                               const double *p25, int64_t p25_stride, int skin, hipStream_t st);
+// Load the tree kernels' and K5's code objects on the current device (afs_create: no code-object
+// load inside the first synthesis call).
+hipError_t preload_tree_kernels();
+hipError_t preload_plan_kernels();
 hipError_t launch_tree_nonfinite(const double *lds_state, int B, int32_t *count, uint8_t *flags, hipStream_t st);
 hipError_t launch_tree_draws(const double *lds_state, int B, int64_t *draws, hipStream_t st);
 hipError_t launch_plan(const PlanArgs &a, hipStream_t st);

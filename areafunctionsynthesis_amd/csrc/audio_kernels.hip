@@ -51,4 +51,10 @@ hipError_t launch_to_int16(const double *in, int16_t *out, int64_t n, hipStream_
   return hipGetLastError();
 }
 
+// (see preload_tree_kernels, tds_tree.hip)
+hipError_t preload_audio_kernels() {
+  hipFuncAttributes at;
+  return hipFuncGetAttributes(&at, reinterpret_cast<const void *>(to_int16_kernel));
+}
+
 }  // namespace afs

@@ -221,4 +221,13 @@ hipError_t launch_plan(const PlanArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// (see preload_tree_kernels, tds_tree.hip)
+hipError_t preload_plan_kernels() {
+  hipFuncAttributes at;
+  hipError_t e = hipFuncGetAttributes(&at, reinterpret_cast<const void *>(plan_kernel));
+  if (e == hipSuccess) e = hipFuncGetAttributes(&at, reinterpret_cast<const void *>(plan_hop_iv_kernel));
+  if (e == hipSuccess) e = hipFuncGetAttributes(&at, reinterpret_cast<const void *>(plan_hop_wave_kernel));
+  return e;
+}
+
 }  // namespace afs

@@ -169,4 +169,28 @@ hipError_t launch_tree_draws(const double *lds_state, int B, int64_t *draws, hip
   return hipGetLastError();
 }
 
+// Loads this file's code object on the context's device now (HIP loads a code object at the first
+// launch of one of its kernels otherwise: tens of milliseconds inside a real-time caller's first
+// buffer).
+template <class K> static hipError_t preload_one(K k) {
+  hipFuncAttributes at;
+  return hipFuncGetAttributes(&at, reinterpret_cast<const void *>(k));
+}
+hipError_t preload_tree_kernels() {
+  hipError_t e = hipSuccess;
+  for (hipError_t x : {preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, TW>),
+                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false, TW>),
+                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, 64>),
+                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false, 64>),
+                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true, TW>),
+                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, false, TW>),
+                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true, 64>),
+                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, false, 64>),
+                       preload_one(tree_output_kernel), preload_one(tree_reset_kernel<TW>),
+                       preload_one(tree_reset_kernel<64>), preload_one(tree_nonfinite_kernel),
+                       preload_one(tree_draws_kernel)})
+    if (e == hipSuccess) e = x;
+  return e;
+}
+
 }  // namespace afs

@@ -22,7 +22,10 @@ the CPU baseline (the reference's own sources, oracle/_ref, timed on this host's
 bounded sample, plus the single-core config-1 figure).  On one GPU the line also carries
 "configs": config 5 (8192 fricatives, velum 1.0 cm^2) and config 3 (8192 VCV utterances through
 playTargetSequence), each timed over a few steps with its own launch times, roofline, fp64
-object, reference CPU rate and error against the reference build (--no-sub-configs skips them).
+object, reference CPU rate and error against the reference build, and "config4_full": the
+metric's whole 64k-utterance batch in one call on this GPU (one step; its first rows checked bit
+for bit against the shard's, its first utterances against the reference build; --full-batch 0 or
+--no-sub-configs skips them).
 PMC-derived figures are quoted only when profiles/pmc_*.json hold a pass of this build's kernel
 sources (areafunctionsynthesis_amd.build.kernel_digest).
 """
@@ -406,6 +409,9 @@ def main() -> None:
                     help="tree solver: force 16 (throughput kernel) or 64 (voice kernel) lanes per utterance; "
                          "default: the library's choice for the batch")
     ap.add_argument("--sub-steps", type=int, default=2)
+    ap.add_argument("--full-batch", type=int, default=65536,
+                    help="one GPU: also time the metric's whole batch (65536 utterances) in one call, one step "
+                         "(0: skip)")
     ap.add_argument("--gather-transport", choices=("rccl", "gloo"), default="rccl",
                     help="N > 1: rccl (the library's afs_gather_pcm; default) or gloo through the host (test only)")
     ap.add_argument("--one-device", action="store_true",
@@ -481,6 +487,14 @@ def main() -> None:
     if world == 1 and args.workload == "static" and not args.no_sub_configs:
         for wl, label in (("fricatives", "config5"), ("vcv", "config3")):
             subs.append((label, measure(args, ctx, dev, stream, wl, B, first, world, rank, None, args.sub_steps, 1)))
+    # one GPU: the metric's own 64k-utterance batch in one call (BASELINE config 4 without the sharding)
+    full = None
+    if world == 1 and args.workload == "static" and args.full_batch > 0 and not args.no_sub_configs:
+        full = measure(args, ctx, dev, stream, "static", args.full_batch, 0, 1, 0, None, 1, 1)
+        n = min(B, args.full_batch)
+        # batch independence: the full batch's first utterances are the shard's, bit for bit
+        full.same_as_shard = bool(torch.equal(full.out_dev[:n], m.out_dev[:n])) if first == 0 else None
+        full.same_rows = n
 
     if rank == 0:
         d = describe(args, m, world, digest)
@@ -547,11 +561,43 @@ def main() -> None:
                     o["max_abs_err_vs_cpu_ref"] = max_abs
                     o["max_rms_err_vs_cpu_ref"] = max_rms
                 result["configs"][label] = o
+        if full is not None:
+            df = describe(args, full, 1, digest)
+            o = {
+                "workload": f"BASELINE config 4's whole batch on one GPU: {full.B} static-vowel utterances x "
+                            f"{args.seconds:g} s @ {args.fs:g} Hz in one afs_synthesize call",
+                "batch": full.B, "value": df["value"], "unit": "samples/s", "steps": full.steps,
+                "warmup": full.warmup, "ms_per_step": df["ms_per_step"],
+                "avg_launch_ms": df["roofline"]["avg_launch_ms"],
+                "launches_per_step": df["roofline"]["launches_per_step"],
+                "lanes_per_utterance": ctx.lanes_per_utterance(full.B),
+                "plan_path": _plan_path(full.B, full.T, full.hop),
+                "ratio_to_shard_value": df["value"] / d["value"],
+                "roofline": df["roofline"], "fp64": df["fp64"],
+                "first_rows_bitwise_equal_to_shard": full.same_as_shard, "rows_compared": full.same_rows,
+            }
+            if not args.no_cpu_baseline:
+                _, max_abs, max_rms = cpu_leg(args, full, 8)
+                o["max_abs_err_vs_cpu_ref"] = max_abs
+                o["max_rms_err_vs_cpu_ref"] = max_rms
+                o["cpu_ref_utterances"] = 8
+            result.setdefault("configs", {})["config4_full"] = o
         print(json.dumps(result), flush=True)
     if comm is not None:
         comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _plan_path(B: int, T: int, hop: int) -> str:
+    """Which noise-plan path afs_synthesize takes for this call (afs_capi.cpp run_chunks)."""
+    hops = -(-T // hop)
+    rec = B * hops * 544
+    budget = 4 << 30
+    if hop >= 32 and rec <= budget:
+        return (f"hop mode, one call: {rec / 1e9:.2f} GB of hop records within the 4 GiB plan budget "
+                "(plus the mixed hops' dense records)")
+    return "chunked launches (plans past the 4 GiB budget)"
 
 
 def _launch_ranks(n: int) -> int:

@@ -3,7 +3,8 @@
 //   adapter_main frames <file>        print afs_frame fields of a mock tube (CPU)
 //   adapter_main nodevice             create a context on a missing device -> afs::Error (CPU)
 //   adapter_main synth <in> <out>     run TdsVoices (batch 1) over frames read from <in> (GPU)
-//   adapter_main latency <in> <out>   the same, writing the wall time of every call (ms) to <out>
+//   adapter_main latency <in> <out>   the same, writing per call (ms): wall time, tube conversion,
+//                                     K5, K1, K6 device times (AFS_PROFILE events) to <out>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -84,18 +85,34 @@ int main(int argc, char **argv) {
     if (std::fread(fr.data(), sizeof(afs_frame), (size_t)F, fi) != (size_t)F) return 3;
     std::fclose(fi);
     (void)argv[4];
-    afs::Context ctx(fs, 0);
+    afs_config cfg;
+    afs_config_default(&cfg);
+    cfg.sampling_rate_hz = fs;
+    if (latency) cfg.flags |= AFS_PROFILE;  // (per-call kernel times, read after each call's clock)
+    afs::Context ctx(cfg);
     afs::TdsVoices<MockTube> voice(ctx, 1, &seed);
     std::vector<double> out, ms;
     std::vector<double> buf((size_t)hop);
+    using clk = std::chrono::steady_clock;
+    auto msec = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     for (int k = 0; k < F; ++k) {
       MockTube t;
       fill(t, fr[(size_t)k]);
+      // the host's tube conversion alone (the call below repeats it)
+      const auto c0 = clk::now();
+      volatile afs_frame probe = afs::frame_from_tube(t, fr[(size_t)k].glottis);
+      (void)probe;
+      const auto c1 = clk::now();
       // (one call as SynthesisThread makes it: tube + glottis in, hop samples back in host memory)
-      const auto t0 = std::chrono::steady_clock::now();
+      const auto t0 = clk::now();
       int n = voice.synthesizeSignalTds(&t, fr[(size_t)k].glottis, hop, buf.data());
-      const auto t1 = std::chrono::steady_clock::now();
-      ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+      const auto t1 = clk::now();
+      if (latency) {
+        // per call: wall, tube conversion, K5, K1, K6 device times (HIP events around each launch)
+        afs_kernel_timing kt{};
+        afs::check(afs_kernel_times_ex(ctx.get(), &kt), ctx.get(), "afs_kernel_times_ex");
+        for (double v : {msec(t0, t1), msec(c0, c1), kt.plan_ms, kt.synth_ms, kt.output_ms}) ms.push_back(v);
+      }
       out.insert(out.end(), buf.begin(), buf.begin() + n);
     }
     if (latency) out = ms;
