@@ -31,6 +31,8 @@ hipError_t launch_target_frames(const double *seq, int Q, const TargetPlan &plan
 
 // keys[u] = the shape key of utterance u's first frame frames[u * fstride] (how narrow its tube is
 // and where), for the slot order of the tree kernel (afs_capi.cpp shape_order).
-hipError_t launch_utterance_keys(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, hipStream_t st);
+// (noise_class: the noise class as the key's first field, af_kernels.hip)
+hipError_t launch_utterance_keys(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, bool noise_class,
+                                 hipStream_t st);
 
 }  // namespace afs

@@ -163,6 +163,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     // (stride and base congruent to the output's modulo 16 doubles): K1 stores both through one
     // line-aligned window (tree_kernel.h).
     auto p25_for = [&](int64_t per, int64_t *stride) -> afs_status {
+      if (!AFS_TONE_K6) return AFS_OK;  // (the tone filter in K1: no pressures stored)
       *stride = per + ((ostride - per) % 16 + 16) % 16;
       return ensure(c, &c->p25, &c->p25_bytes, ((size_t)B * (size_t)*stride + 32) * sizeof(double));
     };
@@ -175,25 +176,28 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     auto synth = [&](int64_t s0, int64_t s1, const uint64_t *plan, int64_t plan_stride, const afs::tree::PlanHop *hops,
                      int64_t hop_stride, int64_t p25_stride) -> afs_status {
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride, plan, plan_stride, lanes,
-                      (double *)ws, B, c->host_tab.uni, hops, hop_stride, p25_row0(s0), p25_stride, order};
+                      (double *)ws, B, c->host_tab.uni, hops, hop_stride, p25_row0(s0), p25_stride, order,
+                      c->noise_variants ? 1 : 0};
       hipEvent_t e1 = prof_event(c);
       HIP_TRY(c, afs::launch_tree_synth(a, width, c->stream));
       hipEvent_t e2 = prof_event(c);
       prof_pair(c, e1, e2, 0);
       // K6: the glottal-tone filter and the output stage of the launch's samples
-      HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B, p25_row0(s0),
-                                         p25_stride, c->cfg.options.radiation_from_skin, c->stream));
+      HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B,
+                                         AFS_TONE_K6 ? p25_row0(s0) : nullptr, p25_stride,
+                                         c->cfg.options.radiation_from_skin, c->stream));
       prof_pair(c, e2, prof_event(c), 2);
       return AFS_OK;
     };
     // Hop mode (tree solver, hops >= PLAN_HOP_MIN): K5 decides every hop of the call first -- one
-    // record per (row, hop), the hops it cannot decide at once listed -- the host reads the list's
-    // length, and K5's second stage writes the dense records of the listed hops whose samples
-    // differ (mixed) into a compact array (slot = list entry).  K1 then runs the call in launches
-    // of up to 65536 samples, each hop's words evaluated from its record (or read from its dense
-    // slot).  One K1 launch per second of 44.1 kHz audio instead of one per 4096 samples: no
-    // state save / restore and launch tail in between (+0.6 %, profiles/r04c_store_launch_ab.txt).
-    // A list whose dense records would exceed the plan budget falls back to the chunked path.
+    // record per (row, hop), the hops it cannot decide at once listed -- and K5's second stage
+    // decides the listed hops sample by sample, writing the dense records of the mixed ones (whose
+    // samples differ) into a compact array (one hop-long slot each, claimed from a counter).  K1
+    // then runs the call in launches of up to 65536 samples, each hop's words evaluated from its
+    // record (or read from its dense slot).  One K1 launch per second of 44.1 kHz audio instead of
+    // one per 4096 samples: no state save / restore and launch tail in between (+0.6 %,
+    // profiles/r04c_store_launch_ab.txt).  A call whose mixed hops' records would exceed the plan
+    // budget falls back to the chunked path.
     const bool hops = !c->plan_dense && hop >= afs::tree::PLAN_HOP_MIN;
     const int64_t call_hops = afs::plan_hop_slots(0, S, hop);
     if (hops && (int64_t)rows * call_hops * (int64_t)sizeof(afs::tree::PlanHop) <= c->plan_budget) {
@@ -207,22 +211,34 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, 0, S, nullptr, 0, two, uo, hbuf, hstride, work, true};
       hipEvent_t e0 = prof_event(c);
       HIP_TRY(c, afs::launch_plan_hops_iv(pa, c->stream));
-      // The list's length sizes the dense records.  When every hop of the call fits them (small
-      // calls: real-time sessions, short batches) they are sized for that worst case and the call
-      // runs without a host wait; otherwise the host reads the length back, waiting for the work
-      // queued so far on the stream (the previous call's kernels included).
-      int64_t listed = (int64_t)rows * call_hops;
-      if (listed * hop * afs::PLAN_RECORD_BYTES > std::min<int64_t>(c->plan_budget, SMALL_CALL_DENSE_BYTES)) {
+      // Slots for the mixed hops.  When every hop of the call fits them (small calls: real-time
+      // sessions, short batches) they are sized for that worst case and the call runs without a
+      // host wait.  Otherwise the host reads the list's length back (waiting for the work queued so
+      // far on the stream, the previous call's kernels included) and offers min(listed, budget)
+      // slots; only when the list is longer than the budget's slots does it read back how many the
+      // mixed hops claimed (most listed hops are not mixed: near-ties decided alike by every sample).
+      const int64_t slot_bytes = (int64_t)hop * afs::PLAN_RECORD_BYTES;
+      int64_t cap = (int64_t)rows * call_hops;
+      bool check = false;
+      if (cap * slot_bytes > std::min<int64_t>(c->plan_budget, SMALL_CALL_DENSE_BYTES)) {
         HIP_TRY(c, hipMemcpyAsync(c->hcount, work, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        listed = (int64_t)(uint32_t)*c->hcount;
+        const int64_t listed = (int64_t)(uint32_t)*c->hcount;
+        cap = std::min<int64_t>(listed, c->plan_budget / slot_bytes);
+        check = cap < listed;
       }
-      const int64_t dense_bytes = listed * hop * afs::PLAN_RECORD_BYTES;
-      if (dense_bytes <= c->plan_budget) {
-        if (dense_bytes > 0 && (st = ensure(c, &c->plan, &c->plan_bytes, (size_t)dense_bytes)) != AFS_OK) return st;
-        pa.plan = (uint64_t *)c->plan;
-        HIP_TRY(c, afs::launch_plan_hops_wave(pa, c->stream));
-        prof_pair(c, e0, prof_event(c), 1);
+      if (cap > 0 && (st = ensure(c, &c->plan, &c->plan_bytes, (size_t)(cap * slot_bytes))) != AFS_OK) return st;
+      pa.plan = (uint64_t *)c->plan;
+      pa.dense_cap = cap;
+      HIP_TRY(c, afs::launch_plan_hops_wave(pa, c->stream));
+      bool fits = true;
+      if (check) {
+        HIP_TRY(c, hipMemcpyAsync(c->hcount, work + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        fits = (int64_t)(uint32_t)*c->hcount <= cap;
+      }
+      prof_pair(c, e0, prof_event(c), 1);
+      if (fits) {
         const int64_t per = std::min<int64_t>(S, c->launch_cap);
         int64_t p25_stride = 0;
         if ((st = p25_for(per, &p25_stride)) != AFS_OK) return st;
@@ -234,7 +250,6 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
         }
         return AFS_OK;
       }
-      prof_pair(c, e0, prof_event(c), 1);
     }
     // Chunked path: launches of `per` samples, each K5 (the chunk's plans: dense records, or in
     // hop mode the chunk's hop records with sample-indexed dense records) and then K1.  With
@@ -280,7 +295,8 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     auto plan_chunk = [&](int64_t k) -> afs_status {
       const int64_t s0 = k * per, s1 = std::min(S, s0 + per);
       afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, s0, s1, (uint64_t *)buf[k & 1], per, two, uo,
-                       hbuf[k & 1], hstride, hops ? (uint32_t *)c->plan_work[ov ? (k & 1) : 0] : nullptr, hops};
+                       hbuf[k & 1], hstride, hops ? (uint32_t *)c->plan_work[ov ? (k & 1) : 0] : nullptr, hops,
+                       (int64_t)rows * hstride};  // (hop mode: a slot for every hop of the chunk)
       hipEvent_t e0 = prof_event(c, ps);
       HIP_TRY(c, hops ? afs::launch_plan_hops(pa, ps) : afs::launch_plan(pa, ps));
       prof_pair(c, e0, prof_event(c, ps), 1);
@@ -451,6 +467,8 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   if (const char *e = std::getenv("AFS_PLAN_DENSE")) ctx->plan_dense = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_XCD_ORDER")) ctx->xcd_order = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_SHAPE_ORDER")) ctx->shape_order = std::atoi(e) != 0;
+  if (const char *e = std::getenv("AFS_NOISE_VARIANTS")) ctx->noise_variants = std::atoi(e) != 0;
+  if (const char *e = std::getenv("AFS_CLASS_ORDER")) ctx->class_order = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_LAUNCH_SAMPLES")) {  // (A/B and latency studies: samples per K1 launch)
     const long long v = std::atoll(e);
     if (v > 0) ctx->launch_cap = std::min<int64_t>(v, 65536);
@@ -540,7 +558,7 @@ static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstr
   if ((s = ensure(c, &c->keys, &c->keys_bytes, kbytes + obytes)) != AFS_OK) return s;
   uint64_t *dkeys = (uint64_t *)c->keys;
   int32_t *dorder = (int32_t *)((char *)c->keys + kbytes);
-  HIP_TRY(c, afs::launch_utterance_keys(dframes, fstride, B, dkeys, c->stream));
+  HIP_TRY(c, afs::launch_utterance_keys(dframes, fstride, B, dkeys, c->noise_variants && c->class_order, c->stream));
   c->hkeys.resize((size_t)B);
   HIP_TRY(c, hipMemcpyAsync(c->hkeys.data(), dkeys, kbytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));

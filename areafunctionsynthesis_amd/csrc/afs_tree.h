@@ -38,6 +38,9 @@ struct TreeArgs {
   // padding slots); shared trajectories (frame_row) order the utterances by row so that the blocks
   // one XCD runs at a time play few rows (afs_capi.cpp xcd_order)
   const int32_t *order = nullptr;
+  // hop mode: run each wave's launch in the lightest noise-phase variant its hop records allow
+  // (tree_kernel.h noise_variant; 0: always the full phases -- AFS_NOISE_VARIANTS=0, A/B and tests)
+  int noise_variants = 1;
 };
 // K5: the noise-source plans of samples [s_begin, s_end) of `rows` frame rows.
 struct PlanArgs {
@@ -53,21 +56,28 @@ struct PlanArgs {
                             // smoothed flows (tab->consts.sec)
   tree::PlanHop *hops = nullptr;  // hop mode (launch_plan_hops): as TreeArgs::hops
   int64_t hop_stride = 0;
-  uint32_t *work = nullptr;  // hop mode: a counter and rows * hop slots entries (the hops decided
-                             // sample by sample)
-  // hop mode: the dense records of a mixed hop go to slot e of a compact array (e: its work-list
-  // entry; plan[(e * hop + i) * 16 + w] for the hop's sample i; PlanHop::dense = e) instead of
-  // sample-indexed rows (the diagnostics' layout)
+  uint32_t *work = nullptr;  // hop mode: work[0] the hops listed (decided sample by sample), work[1]
+                             // the compact slots claimed, then rows * hop slots list entries
+  // hop mode: the dense records of a mixed hop go to the next free slot e of a compact array
+  // (plan[(e * hop + i) * 16 + w] for the hop's sample i; PlanHop::dense = e; e < dense_cap, else
+  // nothing is written and the host, which reads work[1] back, falls back to shorter launches)
+  // instead of sample-indexed rows (the diagnostics' layout)
   bool compact = false;
+  int64_t dense_cap = 0;
 };
 constexpr int64_t PLAN_RECORD_BYTES = 128;
 // Hop slots a launch of samples [s0, s1) spans.
 inline int64_t plan_hop_slots(int64_t s0, int64_t s1, int hop) { return (s1 - 1) / hop - s0 / hop + 1; }
 // Bytes of the hop-mode work list of a launch.
-inline int64_t plan_work_bytes(int64_t rows, int64_t slots) { return (rows * slots + 1) * 4; }
+inline int64_t plan_work_bytes(int64_t rows, int64_t slots) { return (rows * slots + 2) * 4; }
 
 #ifndef AFS_TREE_W
 #define AFS_TREE_W 16
+#endif
+#ifndef AFS_TONE_K6
+// 1: K1 stores section 25's pressure per sample and K6 runs the glottal-tone filter over it
+// (+0.5 % end to end in round 3, profiles/r03ai_ab.txt); 0: K1 runs the filter itself (A/B builds)
+#define AFS_TONE_K6 1
 #endif
 #ifndef AFS_TREE_WPB
 // waves per block of the throughput kernel: 2 (8 utterances, 78 KB of LDS: two blocks per CU).  With

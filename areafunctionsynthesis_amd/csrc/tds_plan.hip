@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(HOP_IV_BLOCK) plan_hop_iv_kernel(PlanArgs a, i
     h = PlanHop{};
     ok = plan_hop_inputs(k, fl, fr, a.uo, a.two_mass != 0, h);
   }
-  if (!ok) a.work[1 + atomicAdd(a.work, 1u)] = (uint32_t)id;
+  if (!ok) a.work[2 + atomicAdd(a.work, 1u)] = (uint32_t)id;
 }
 
 __global__ void __launch_bounds__(HOP_WAVE) plan_hop_wave_kernel(PlanArgs a, int64_t slots) {
@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(HOP_WAVE) plan_hop_wave_kernel(PlanArgs a, int
   const int lane = threadIdx.x;
   const uint32_t nwork = a.work[0];
   for (uint32_t e = blockIdx.x; e < nwork; e += gridDim.x) {
-    const uint32_t id = a.work[1 + e];
+    const uint32_t id = a.work[2 + e];
     const int64_t row = id / slots, slot = id % slots;
     const HopRange r = hop_range(a, slot);
     const int64_t h = r.h;
@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(HOP_WAVE) plan_hop_wave_kernel(PlanArgs a, int
     const afs_frame *fl = (const afs_frame *)fr_lds[0], *fr = (const afs_frame *)fr_lds[1];
     const int i0 = r.i0, i1 = r.i1;
     PlanKey k0{};
-    uint64_t q0[2] = {0, 0};
+    uint64_t q0[2] = {0, 0}, noise = 0;
     bool diff = false;
     for (int i = i0 + lane, it = 0; it == 0 || i < i1; i += HOP_WAVE, ++it) {
       uint64_t q[2] = {0, 0};
@@ -148,6 +148,7 @@ __global__ void __launch_bounds__(HOP_WAVE) plan_hop_wave_kernel(PlanArgs a, int
         double obst[4], po[4];
         plan_decide(g, k, obst, po);
         plan_key_pack(k, q);
+        noise |= plan_key_noise(k);
       }
       if (it == 0) {  // (the hop's first sample is lane 0's first)
         k0 = k;
@@ -157,22 +158,29 @@ __global__ void __launch_bounds__(HOP_WAVE) plan_hop_wave_kernel(PlanArgs a, int
       if (i < i1) diff = diff || q[0] != q0[0] || q[1] != q0[1];
     }
     bool mixed = __ballot(diff) != 0;
+#pragma unroll
+    for (int o = HOP_WAVE / 2; o >= 1; o /= 2) noise |= __shfl_xor(noise, o, HOP_WAVE);
     if (lane == 0) {
       PlanHop &hl = *reinterpret_cast<PlanHop *>(hop_lds);
       hl = PlanHop{};
       const bool ok = plan_hop_inputs(k0, fl, fr, a.uo, a.two_mass != 0, hl);
       hl.mixed = (mixed || !ok) ? 1u : 0u;
-      hl.dense = a.compact ? e : 0u;
+      // (compact: the next free slot, claimed by mixed hops only -- the listed hops whose samples
+      // share one decision, most of them, need none)
+      hl.dense = (a.compact && hl.mixed) ? atomicAdd(a.work + 1, 1u) : 0u;
+      hl.noise = noise;  // (every sample's, not only the first's)
     }
     __syncthreads();
     mixed = reinterpret_cast<const PlanHop *>(hop_lds)->mixed != 0;
+    const uint32_t slot_e = reinterpret_cast<const PlanHop *>(hop_lds)->dense;
+    if (a.compact && (int64_t)slot_e >= a.dense_cap) mixed = false;  // (no room: the host falls back)
     uint64_t *dst = reinterpret_cast<uint64_t *>(a.hops + row * a.hop_stride + slot);
     for (int w = lane; w < HOP_WORDS; w += HOP_WAVE) dst[w] = hop_lds[w];
     if (mixed) {  // the decisions change within the hop: the samples' dense records
       for (int i = i0 + lane; i < i1; i += HOP_WAVE) {
         uint64_t w[PLAN_WORDS];
         plan_sample<true>(fl, fr, (double)i / (double)a.hop, a.uo, a.two_mass != 0, w);
-        const int64_t rec = a.compact ? (int64_t)e * a.hop + i : row * a.plan_stride + (h * a.hop + i - a.s_begin);
+        const int64_t rec = a.compact ? (int64_t)slot_e * a.hop + i : row * a.plan_stride + (h * a.hop + i - a.s_begin);
         ulonglong2 *o = (ulonglong2 *)(a.plan + rec * PLAN_WORDS);
 #pragma unroll
         for (int q = 0; q < PLAN_WORDS / 2; ++q) o[q] = make_ulonglong2(w[2 * q], w[2 * q + 1]);
@@ -190,7 +198,7 @@ hipError_t launch_plan_hops_iv(const PlanArgs &a, hipStream_t st) {
   if (!a.hops || a.hop < PLAN_HOP_MIN) return hipErrorInvalidValue;
   if (!a.work) return hipErrorInvalidValue;
   const int64_t slots = plan_hop_slots(a.s_begin, a.s_end, a.hop), n_hops = (int64_t)a.rows * slots;
-  hipError_t e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), st);
+  hipError_t e = hipMemsetAsync(a.work, 0, 2 * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(plan_hop_iv_kernel, dim3((unsigned)((n_hops + HOP_IV_BLOCK - 1) / HOP_IV_BLOCK)),
                      dim3(HOP_IV_BLOCK), 0, st, a, slots);

@@ -1019,6 +1019,32 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
 // ---------------------------------------------------------------------------
 struct Target { uint32_t up; double tup, tdn, fc; bool on; };
 
+// Noise-phase variants.  On most utterances only some constrictions ever exist and only some
+// dipole sources are ever targeted -- static vowels: the glottis source alone (dipoles 2-4) on a
+// third of them, the glottis and one tongue constriction below dipole 32 on another third -- yet
+// the full phases evaluate all four constrictions and smooth, count and filter all NDP dipole
+// slots of every lane at every sample.  A variant NZ evaluates the first NC constrictions (glottis,
+// tongue 1, tongue 2, lip) and processes the first NS slots; K1 runs a launch's time loop for a
+// wave in the lightest variant whose constrictions and dipole slots cover everything the launch's
+// hop records say any of its samples may target (PlanHop::noise) and whose skipped slots hold no
+// amplitude (damp == 0, so their smoother, filter and dipole samples stay exactly as they are: 0).
+// The variants compute exactly the full phases' values (tree_kernel.h).  Ceiling measured with
+// every wave forced into a variant, 8192 static vowels (profiles/r05b_noise_variant_ceiling_ab.txt):
+// NZ 1 +4.8 %, NZ 2 +13 %.
+enum : int { NZ_FULL = 0, NZ_TONGUE1 = 1, NZ_GLOTTIS = 2, NZ_COUNT = 3 };
+template <int W, int NZ>
+struct NoiseV {
+  static constexpr int NC = NZ == NZ_FULL ? 4 : (NZ == NZ_TONGUE1 ? 2 : 1);
+  static constexpr int NS_ = NZ == NZ_FULL ? Shape<W>::NDP : (NZ == NZ_TONGUE1 ? 2 : 1);
+  static constexpr int NS = NS_ < Shape<W>::NDP ? NS_ : Shape<W>::NDP;
+  // PlanHop::noise bits this variant serves: constrictions 0 .. NC-1, dipoles below NS * W
+  static constexpr uint64_t SERVES = (((1ull << NC) - 1) << NOISE_CON0) |
+                                     (NS * W >= 64 ? ((1ull << NOISE_CON0) - 1) : ((1ull << (NS * W)) - 1));
+};
+static_assert(NoiseV<16, NZ_GLOTTIS>::SERVES == NOISE_SERVES16_GLOTTIS &&
+                  NoiseV<16, NZ_TONGUE1>::SERVES == NOISE_SERVES16_TONGUE1,
+              "tree_plan.h plan_noise_class16: the slot order's classes are the 16-lane variants");
+
 AFS_HD inline double narrow_flow(const double *X, uint32_t o0, uint32_t o1) {
   double flow = 0.0;
   flow += xat(X, o0);  // (an absent output reads the zero slot)
@@ -1030,9 +1056,9 @@ AFS_HD inline double clamp_fc(double fc) {
   return at_most(at_least(fc, 50.0), 2000.0);
 }
 
-template <int W, class Xc>
+template <int W, int NZ, class Xc>
 AFS_HD inline void phase_targets(Xc &x, int gl, Lane<W> &R, const double *X, const Consts &C, double a_glot_up) {
-  using S = Shape<W>;
+  using V = NoiseV<W, NZ>;
   const uint64_t hdr = x.template rec<PW_HDR>(), uo = x.template rec<PW_UO>(), uol = x.template rec<PW_UOL>();
   const uint32_t fl = (uint32_t)hdr & 0xffu;
   Target t[4];
@@ -1045,7 +1071,7 @@ AFS_HD inline void phase_targets(Xc &x, int gl, Lane<W> &R, const double *X, con
     t[0] = Target{(uint32_t)(hdr >> 8) & 0xffu, (1.0 - fdn) * full, fdn * full, 2000.0, (fl & PF_G) != 0};
   }
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {  // tongue constrictions: "normal" fricatives (:1547-1563)
+  for (int c = 0; c < V::NC - 1 && c < 2; ++c) {  // tongue constrictions: "normal" fricatives (:1547-1563)
     const uint32_t o = (uint32_t)(uo >> (32 * c));
     const double invA = plan_double(c ? x.template rec<PW_T2 + 0>() : x.template rec<PW_T1 + 0>());
     const double sqA = plan_double(c ? x.template rec<PW_T2 + 1>() : x.template rec<PW_T1 + 1>());
@@ -1059,7 +1085,7 @@ AFS_HD inline void phase_targets(Xc &x, int gl, Lane<W> &R, const double *X, con
     t[1 + c] = Target{(uint32_t)(hdr >> (16 + 8 * c)) & 0xffu, (1.0 - fdn) * full, fdn * full, clamp_fc(fc),
                       (fl & (c ? PF_T2 : PF_T1)) != 0};
   }
-  {  // lower lip: flat spectrum, gain 2e-7 (:1523-1529)
+  if constexpr (V::NC >= 4) {  // lower lip: flat spectrum, gain 2e-7 (:1523-1529)
     const double v = narrow_flow(X, (uint32_t)uol & 0xffffu, (uint32_t)(uol >> 16) & 0xffffu) *
                      plan_double(x.template rec<PW_L + 0>());
     const double full = 2.0e-7 * fabs(v) * v * v * plan_double(x.template rec<PW_L + 1>());
@@ -1069,11 +1095,11 @@ AFS_HD inline void phase_targets(Xc &x, int gl, Lane<W> &R, const double *X, con
   // the owned dipoles: targets in store order, then the 40 Hz amplitude smoother
   // (branch-free over the slots; a slot past the 41 dipoles is never targeted and never active)
 #pragma unroll
-  for (int k = 0; k < S::NDP; ++k) {
+  for (int k = 0; k < V::NS; ++k) {
     const uint32_t d = (uint32_t)(gl + k * W);
     double tgt = 0.0, cut = 0.0;  // targetAmp reset (:1203-1208); cut 0: not targeted
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < V::NC; ++c) {
       const uint32_t dn = t[c].up < (uint32_t)(NPM - 1) ? t[c].up + 1 : (uint32_t)DIP_LIPS;
       const bool hu = t[c].on && t[c].up == d, hd = t[c].on && dn == d;
       tgt = hu ? t[c].tup : tgt;
@@ -1139,19 +1165,19 @@ AFS_HD inline void rng_block(Xc &x, uint32_t *g, uint32_t *sink, int head, bool 
 // difference of two output prefix sums.  Then the one-pole shaping filter of the owned
 // active dipoles.  The values come from the ones generated ahead (rng_ahead, at least
 // RNG_BLOCK pending); a sample that needs more generates further blocks here.
-template <int W, class Xc>
+template <int W, int NZ, class Xc>
 AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) {
-  using S = Shape<W>;
+  using V = NoiseV<W, NZ>;
   x.mark(PH_N_AMP);
   uint64_t act = 0;
 #pragma unroll
-  for (int k = 0; k < S::NDP; ++k)
+  for (int k = 0; k < V::NS; ++k)
     act |= x.ballot([&](int gl, Lane<W> &R) { return gl + k * W < NDIP && !(R.damp[k] < THR); }) << (k * W);
   if (act == 0) {
     x.par([&](int gl, Lane<W> &R) {
       (void)R;
 #pragma unroll
-      for (int k = 0; k < S::NDP; ++k)
+      for (int k = 0; k < V::NS; ++k)
         if (gl + k * W < NDIP) X[X_SMP + gl + k * W] = 0.0;
     });
     return;
@@ -1165,7 +1191,7 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
   auto consume = [&](int lo, int hi) {
     x.par([&](int gl, Lane<W> &R) {
 #pragma unroll
-      for (int k = 0; k < S::NDP; ++k) {
+      for (int k = 0; k < V::NS; ++k) {
         const int d = gl + k * W;  // < 64
         const bool on = d < NDIP && ((act >> d) & 1);
         const int q0 = 12 * __builtin_popcountll(act & ((1ull << d) - 1));
@@ -1201,7 +1227,7 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
   });
   x.par([&](int gl, Lane<W> &R) {
 #pragma unroll
-    for (int k = 0; k < S::NDP; ++k) {
+    for (int k = 0; k < V::NS; ++k) {
       const int d = gl + k * W;
       const bool on = d < NDIP && ((act >> d) & 1);
       double xi = (double)(int32_t)R.racc[k];
@@ -1912,7 +1938,7 @@ AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, doub
 // One audio sample.  Xc: execution policy (par / one / lanes / sync).
 // ---------------------------------------------------------------------------
 
-template <int W, int MODEL, bool VARLOSS, class Xc>
+template <int W, int MODEL, bool VARLOSS, int NZ, class Xc>
 AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
   // the glottis of this sample: its loads first, its stores (displacements, interpolated
   // controls) at the end of the block, so that the network and the targets need not wait for
@@ -1932,14 +1958,14 @@ AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts
   x.dyn_neighbors();
   x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS>(gl, R, X, U, C, g.go); });
   x.mark(PH_NETWORK);
-  x.par([&](int gl, Lane<W> &R) { phase_targets<W>(x, gl, R, X, C, g.go.a1); });
+  x.par([&](int gl, Lane<W> &R) { phase_targets<W, NZ>(x, gl, R, X, C, g.go.a1); });
   x.par_uniform([&](int gl, Lane<W> &R) { (void)gl; (void)R; },
                 [&](Lane<W> &R) { (void)R; glottis_commit(X, g); });
 }
 
 // One audio sample at `ratio` with glottis model MODEL (one kernel per model: a kernel holding
-// both models' code needs more registers than the SIMD has).
-template <int W, int MODEL, class Xc>
+// both models' code needs more registers than the SIMD has) and noise-phase variant NZ.
+template <int W, int MODEL, int NZ = NZ_FULL, class Xc>
 AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio, bool defer_out) {
   static_assert(W >= TREE_CHAINS, "every solver lane needs a lane of the utterance");
   // geometry and network in one block (no LDS round trip between them): the interpolated
@@ -1947,12 +1973,12 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   // lane-uniform
   // (one instantiation per glottis model and entrance-loss kind: no option branch in the block)
   const bool varloss = U.opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE;
-  if (varloss) geometry_network<W, MODEL, true>(x, X, U, C, ratio);
-  else geometry_network<W, MODEL, false>(x, X, U, C, ratio);
+  if (varloss) geometry_network<W, MODEL, true, NZ>(x, X, U, C, ratio);
+  else geometry_network<W, MODEL, false, NZ>(x, X, U, C, ratio);
   x.sync();
   x.mark(PH_TARGETS);
   if (U.opt.generate_noise_sources) {
-    phase_noise<W>(x, X, U, C);
+    phase_noise<W, NZ>(x, X, U, C);
   } else {
     x.par([&](int gl, Lane<W> &R) {
       (void)R;

@@ -45,7 +45,7 @@ static_assert(UPB == TREE_UPB, "afs_tree.h TREE_UPB: the host's slot orders grou
 
 template <bool PROF, int W = TW>
 struct GpuExec {
-  static constexpr bool kToneOut = true;        // the tone filter in K6 from the stored p[25] (+0.5 %, r03ai_ab.txt)
+  static constexpr bool kToneOut = AFS_TONE_K6 != 0;  // the tone filter in K6 from the stored p[25] (afs_tree.h)
   static constexpr bool kGlottisSplit = true;   // the glottis' masses on the two lane halves (+1.1 %, r03ag_ab.txt)
   int gl;
   Lane<W> *R;
@@ -176,12 +176,43 @@ struct WaveLdsT {
 };
 using WaveLds = WaveLdsT<TW>;
 
+// The noise-phase variant a wave runs a launch in (tree_core.h NoiseV): the lightest one that
+// serves every dipole and constriction any sample of the launch may target -- the or of its
+// utterances' hop records (PlanHop::noise, every sample's decisions) -- and every dipole slot that
+// still holds amplitude (damp != 0 in the saved lane state: its smoother must keep running).
+// Wave-uniform.  Decided before the body loads any state, so that each variant's body (a whole
+// copy: tree_synth_body) has live ranges of its own: with the branch between time loops instead,
+// the register allocator spilled 160-250 VGPRs of the persistent state to scratch.
+template <int W>
+__device__ __forceinline__ int noise_variant(const TreeArgs &a) {
+  constexpr int UPB_ = Geom<W>::UPB;
+  const int lane = threadIdx.x, g = lane / W, gl = lane % W;
+  const int slot = blockIdx.x * UPB_ + g;
+  const int u = a.order ? a.order[slot] : slot;
+  const int ue = u < a.B ? u : 0;  // (a padding slot runs utterance 0's data and stores nothing)
+  const int64_t row = a.frame_row ? a.frame_row[ue] : ue;
+  const int64_t nh = (a.s_end - 1) / a.hop - a.s_begin / a.hop + 1;
+  const PlanHop *h0 = a.hops + row * a.hop_stride;
+  uint64_t m = 0;
+  for (int64_t q = gl; q < nh; q += W) m |= h0[q].noise;
+  const Lane<W> &L = ((const Lane<W> *)a.lane_state)[(int64_t)ue * W + gl];
+#pragma unroll
+  for (int k = 0; k < Shape<W>::NDP; ++k)
+    if (L.damp[k] != 0.0 && gl + k * W < NDIP) m |= 1ull << (gl + k * W);
+#pragma unroll
+  for (int o = 32; o >= 1; o /= 2) m |= __shfl_xor(m, o, 64);
+  int nz = NZ_FULL;
+  if ((m & ~NoiseV<W, NZ_TONGUE1>::SERVES) == 0) nz = NZ_TONGUE1;
+  if ((m & ~NoiseV<W, NZ_GLOTTIS>::SERVES) == 0) nz = NZ_GLOTTIS;
+  return __builtin_amdgcn_readfirstlane(a.noise_variants ? nz : (int)NZ_FULL);
+}
+
 // prof (PROF only): per wave, PH_COUNT cycle sums (s_memtime) over the launch.
 // HOPS: the plan words come from hop records (a.hops, tree_plan.h PlanHop): lane gl keeps word
 // gl's kind and inputs for the hop and evaluates the word at every sample; a mixed hop's samples
 // read their dense records as without HOPS.
-template <bool PROF, int MODEL, bool HOPS = false, int W = TW>
-__device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &lds, uint64_t *prof) {
+template <bool PROF, int MODEL, bool HOPS, int W, int NZ>
+__device__ __forceinline__ void tree_synth_run(const TreeArgs &a, WaveLdsT<W> &lds, uint64_t *prof) {
   constexpr int UPB_ = Geom<W>::UPB, WPB_ = Geom<W>::WPB;
   const int lane = threadIdx.x;  // 0 .. 64 WPB - 1
   const int g = lane / W, gl = lane % W;
@@ -268,7 +299,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
       next = pl[tn * PLAN_WORDS];  // the next sample's word, a sample ahead
       if (i + 1 == hop && t + 1 < n) nf.load(gl, fu + k + 1);
     }
-    sample_step<W, MODEL>(ex, X, a.uni, C, ratio, true);
+    sample_step<W, MODEL, NZ>(ex, X, a.uni, C, ratio, true);
     {
       const int j = (o_line + (int)t) & 15;  // the sample's position in its line
       const double p25v = GpuExec<PROF, W>::template dpp<0x152>(R.p[0]);  // lane 2's p[25] to its row
@@ -278,7 +309,7 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
       // lane gl stores window entry gl, sample t - j + gl, if it belongs to this launch
       if (valid && (j == 15 || t + 1 == n) && gl <= j && t - j + gl >= 0) {
         o[t - j + gl] = wo;
-        p25o[t - j + gl] = wp;
+        if constexpr (AFS_TONE_K6 != 0) p25o[t - j + gl] = wp;
       }
     }
     if (++i == hop) {
@@ -315,6 +346,21 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
     if (lane % 64 == 0)
       for (int p = 0; p < PH_COUNT; ++p)
         prof[((int64_t)blockIdx.x * WPB_ + lane / 64) * PH_COUNT + p] = ex.acc[p];
+  }
+}
+
+// The kernel body: in hop mode each wave picks its noise-phase variant for the launch
+// (noise_variant) and runs the whole body compiled for it.  (The waves of a block may take
+// different variants: each reaches the one __syncthreads of the table staging in its own copy.)
+template <bool PROF, int MODEL, bool HOPS = false, int W = TW>
+__device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &lds, uint64_t *prof) {
+  if constexpr (HOPS) {
+    const int nz = noise_variant<W>(a);
+    if (nz == NZ_GLOTTIS) tree_synth_run<PROF, MODEL, HOPS, W, NZ_GLOTTIS>(a, lds, prof);
+    else if (nz == NZ_TONGUE1) tree_synth_run<PROF, MODEL, HOPS, W, NZ_TONGUE1>(a, lds, prof);
+    else tree_synth_run<PROF, MODEL, HOPS, W, NZ_FULL>(a, lds, prof);
+  } else {
+    tree_synth_run<PROF, MODEL, HOPS, W, NZ_FULL>(a, lds, prof);
   }
 }
 

@@ -254,6 +254,30 @@ struct PlanKey {
   bool tb1, tb2;    // the tongue obstacle is the teeth (:1283-1299)
   uint32_t flags;   // PF_*
 };
+// The dipole sources a sample's decisions target -- bit d for dipole d (0..40: the up- and
+// downstream source of every constriction present, TdsModel.cpp:1590-1604; a lateral tongue
+// constriction targets its sources with amplitude 0) -- and, bits NOISE_CON0 + c, the
+// constrictions present (PF_G, PF_T1, PF_T2, PF_L).
+constexpr int NOISE_CON0 = 48;
+AFS_HD inline uint64_t plan_key_noise(const PlanKey &k) {
+  uint64_t m = 0;
+  for (int c = 0; c < 4; ++c)
+    if (k.flags & (1u << c)) {
+      const int up = k.mo[c], dn = up < NPM - 1 ? up + 1 : DIP_LIPS;
+      m |= (1ull << up) | (1ull << dn) | (1ull << (NOISE_CON0 + c));
+    }
+  return m;
+}
+// The noise-phase variant classes of the 16-lane synthesis kernel (tree_core.h NoiseV): the
+// plan_key_noise bits the glottis-only variant serves (the glottis constriction, dipoles 0-15: its
+// lanes' first slot) and the glottis + first tongue constriction variant (dipoles 0-31).  Class 2,
+// 1 or 0 (the full phases) of a mask; the slot order groups utterances by the class of their first
+// frame (afs_capi.cpp shape_order).
+constexpr uint64_t NOISE_SERVES16_GLOTTIS = (1ull << NOISE_CON0) | 0xFFFFull;
+constexpr uint64_t NOISE_SERVES16_TONGUE1 = (3ull << NOISE_CON0) | 0xFFFFFFFFull;
+AFS_HD inline int plan_noise_class16(uint64_t m) {
+  return (m & ~NOISE_SERVES16_GLOTTIS) == 0 ? 2 : ((m & ~NOISE_SERVES16_TONGUE1) == 0 ? 1 : 0);
+}
 // Two 64-bit words that are equal iff the keys are.
 AFS_HD inline void plan_key_pack(const PlanKey &k, uint64_t *q) {
   auto b6 = [](int v) { return (uint64_t)(uint32_t)(v + 1) & 63u; };  // -1 .. 62
@@ -464,7 +488,8 @@ struct PlanHop {
   uint8_t kind[PLAN_WORDS];
   uint32_t mixed;           // 1: the hop's samples use the dense records
   uint32_t dense;           // compact dense records (PlanArgs::compact): the mixed hop's slot
-  uint32_t pad[2];
+  uint64_t noise;           // plan_key_noise of every sample of the hop, or-ed (K1 picks its noise
+                            // phases' variant for a launch from these, tree_kernel.h)
 };
 static_assert(sizeof(PlanHop) == 544, "hop record layout (K1 loads p[w] as two 16-byte words)");
 constexpr int PLAN_HOP_MIN = 32;  // shorter hops (target sequences: hop 1) keep dense records
@@ -545,6 +570,7 @@ AFS_HD inline bool plan_hop_inputs(const PlanKey &k, const afs_frame *fl, const 
       h.p[base[c] + j][1] = plan_clampA(fr->area_cm2[na[c]]);
     }
   }
+  h.noise = plan_key_noise(k);
   // glottis gain: constant over the hop
   const double g0 = two_mass ? GLOTTIS_DEFAULT_ASPIRATION_DB : fl->glottis[5];
   h.p[PW_GAIN_G][0] = plan_gain(g0);
@@ -567,7 +593,7 @@ AFS_HD inline bool plan_hop_decide_iv(const afs_frame *fl, const afs_frame *fr, 
 // (ratios i / hop); the words of a mixed hop's samples come from plan_sample.
 inline void plan_hop_host(const afs_frame *fl, const afs_frame *fr, int hop, int i0, int i1, const SecRec *sec,
                           bool two_mass, PlanHop &h) {
-  uint64_t q0[2] = {0, 0};
+  uint64_t q0[2] = {0, 0}, noise = 0;
   PlanKey k0{};
   bool mixed = false;
   for (int i = i0; i < i1; ++i) {
@@ -578,6 +604,7 @@ inline void plan_hop_host(const afs_frame *fl, const afs_frame *fr, int hop, int
     plan_decide(g, k, obst, po);
     uint64_t q[2];
     plan_key_pack(k, q);
+    noise |= plan_key_noise(k);
     if (i == i0) {
       k0 = k;
       q0[0] = q[0];
@@ -589,6 +616,7 @@ inline void plan_hop_host(const afs_frame *fl, const afs_frame *fr, int hop, int
   h = PlanHop{};
   if (!plan_hop_inputs(k0, fl, fr, sec, two_mass, h)) mixed = true;
   h.mixed = mixed ? 1u : 0u;
+  h.noise = noise;
 }
 
 }  // namespace tree

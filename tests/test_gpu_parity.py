@@ -237,6 +237,40 @@ def test_plan_budget_chunked_hop_mode(oracle, monkeypatch):
     assert np.abs(ys["straddle"] - ys["single"]).max() < 1e-7
 
 
+@pytest.mark.parametrize("solver", TREE_SOLVERS)
+def test_noise_variants_are_bitwise(oracle, solver, monkeypatch):
+    """K1 runs each wave's launch in the lightest noise-phase variant its hop records allow
+    (tree_core.h NoiseV: the glottis source alone, glottis + first tongue constriction below dipole
+    32, or all).  The variants compute the full phases' values: the audio and the rand() call counts
+    equal those of the full phases (AFS_NOISE_VARIANTS=0) bit for bit -- static vowels (most waves
+    in a light variant), fricatives with their tongue and lip sources, frame-rate VCV trajectories
+    (constrictions forming within a launch), and launches of 1000 samples (a dipole's amplitude
+    decaying across a launch boundary keeps its slot in the heavier variant)."""
+    from areafunctionsynthesis_amd.synthesizer import Context
+    from areafunctionsynthesis_amd.workloads import build_frames, fricatives, static_vowels, vcv
+    cases = [("static", static_vowels(48, seconds=0.25)), ("fricatives", fricatives(40, seconds=0.25, velum_cm2=1.0)),
+             ("vcv", vcv(32))]
+    for label, w in cases:
+        for launch in (None, "1000"):
+            ys, draws = [], []
+            for env in ("0", "1"):
+                monkeypatch.setenv("AFS_NOISE_VARIANTS", env)
+                if launch is None:
+                    monkeypatch.delenv("AFS_LAUNCH_SAMPLES", raising=False)
+                else:
+                    monkeypatch.setenv("AFS_LAUNCH_SAMPLES", launch)
+                ctx = Context(44100.0, solver="tree", lanes=LANES[solver])
+                try:
+                    frames = build_frames(w, ctx.af_to_frames)
+                    ys.append(ctx.synthesize(frames, w.hop, seeds=w.seeds))
+                    draws.append(ctx.rng_draws(w.batch))
+                finally:
+                    ctx.close()
+            assert np.isfinite(ys[0]).all(), label
+            assert np.array_equal(ys[0], ys[1]), (label, launch)
+            assert np.array_equal(draws[0], draws[1]), (label, launch)
+
+
 def test_slot_order_is_invisible(oracle, monkeypatch):
     """afs_synthesize places a batch's utterances in the 16-lane kernel's slots sorted by the shape
     of their first frame (afs_capi.cpp shape_order); each utterance's audio is the same wherever it

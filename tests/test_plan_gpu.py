@@ -180,7 +180,7 @@ def test_k1_interpolation_equals_k5_geometry(oracle):
 # mixed hops' samples against plan_sample.
 # ---------------------------------------------------------------------------
 HOP_DTYPE = np.dtype([("p", "<u8", (PLAN_WORDS, 4)), ("kind", "u1", (PLAN_WORDS,)), ("mixed", "<u4"),
-                      ("pad", "<u4", (3,))])
+                      ("dense", "<u4"), ("noise", "<u8")])
 assert HOP_DTYPE.itemsize == 544
 
 
@@ -208,6 +208,7 @@ def _compare_hops(ctx, host_hops, host_plans, frames, hop, s0, s1, fs, two_mass,
     hh = host_hops(frames, hop, s0, s1, fs, two_mass)
     assert np.array_equal(gh["mixed"], hh["mixed"]), label
     assert np.array_equal(gh["kind"], hh["kind"]), label
+    assert np.array_equal(gh["noise"], hh["noise"]), label  # (the dipoles and constrictions of every sample)
     gw, hw = gh["p"].copy(), hh["p"].copy()
     # the glottis gain (a constant word: p[15][0]) comes from the device pow: 1 ulp
     ulps = np.abs(gw[..., 15, 0].view(np.int64) - hw[..., 15, 0].view(np.int64))

@@ -20,7 +20,7 @@ from areafunctionsynthesis_amd.params import default_shapes
 EMU = os.path.join(os.path.dirname(os.path.abspath(__file__)), "emu")
 PLAN_WORDS = 16
 HOP_DTYPE = np.dtype([("p", "<f8", (PLAN_WORDS, 4)), ("kind", "u1", (PLAN_WORDS,)), ("mixed", "<u4"),
-                      ("pad", "<u4", (3,))])
+                      ("dense", "<u4"), ("noise", "<u8")])
 PW_FDN, PW_GAIN_G = 3, 15
 
 
@@ -114,3 +114,34 @@ def test_hop_record_words_equal_dense_records(lib, oracle):
                     assert np.all(np.abs(gw - gd) <= 1e-13 * np.abs(gd)), (label, r, q, i, gw, gd)
                     checked += 1
         assert checked > 0, label
+
+
+def _header_noise(hdr):
+    """plan_key_noise from dense records' header words (tree_plan.h PW_HDR: flags, then the
+    upstream dipole of glottis / tongue 1 / tongue 2 / lip)."""
+    hdr = hdr.astype(np.uint64)
+    m = np.zeros(hdr.shape, dtype=np.uint64)
+    for c in range(4):
+        on = ((hdr >> np.uint64(c)) & np.uint64(1)).astype(bool)
+        up = ((hdr >> np.uint64(8 * (c + 1))) & np.uint64(0xFF)).astype(np.int64)
+        dn = np.where(up < 39, up + 1, 40)
+        bits = (np.uint64(1) << up.astype(np.uint64)) | (np.uint64(1) << dn.astype(np.uint64)) | \
+            (np.uint64(1) << np.uint64(48 + c))
+        m |= np.where(on, bits, np.uint64(0))
+    return m
+
+
+def test_hop_noise_mask_covers_every_sample(lib, oracle):
+    """A hop record's noise mask (K1's choice of its noise phases' variant) is the union over the
+    hop's samples of the dipoles their decisions target and the constrictions present, as the
+    per-sample records' headers give them -- for decided and for mixed hops."""
+    for label, frames, hop in _cases(oracle):
+        rows, F = frames.shape
+        n = (F - 1) * hop
+        hops = np.zeros((rows, F - 1), dtype=HOP_DTYPE)
+        assert lib.emu_plan_hops(frames.ctypes.data, rows, F, hop, 0, n, 44100.0, 0, hops.ctypes.data) == 0
+        dense = np.zeros((rows, n, PLAN_WORDS), dtype=np.uint64)
+        assert lib.emu_plan_records(frames.ctypes.data, rows, F, hop, 0, n, 44100.0, 0, dense.ctypes.data) == 0
+        want = np.bitwise_or.reduce(_header_noise(dense[..., 0]).reshape(rows, F - 1, hop), axis=2)
+        assert np.array_equal(hops["noise"], want), label
+        assert (hops["noise"] >> np.uint64(48) & np.uint64(1)).all(), label  # the glottis source is always present
