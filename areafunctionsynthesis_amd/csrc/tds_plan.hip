@@ -97,18 +97,54 @@ __device__ __forceinline__ HopRange hop_range(const PlanArgs &a, int64_t slot) {
   return HopRange{h, (int)(s_lo - h * a.hop), (int)(s_hi - h * a.hop)};
 }
 
+// The block's frames -- consecutive (row, hop) ids read a contiguous run of frames when the rows'
+// hops are their whole trajectories (frame_stride = slots + 1: every frame-driven call) -- are
+// staged in LDS with coalesced loads and their areas clamped once: each thread's decisions read
+// its two frames' sections several times over (four scans), and from global memory, one 1072-B
+// record per lane, those reads missed the caches -- 9.9 GB of fetch per step of 8192 x 1 s for
+// 0.89 GB of frames (profiles/pmc_traffic.json r04ad).  Blocks whose frames are not one short
+// run (chunked launches) read them from global memory as before.
+constexpr int HOP_IV_STAGE = HOP_IV_BLOCK + 2;  // frames: one more than the block's hops, + a row step
+
 __global__ void __launch_bounds__(HOP_IV_BLOCK) plan_hop_iv_kernel(PlanArgs a, int64_t slots) {
-  const int64_t id = (int64_t)blockIdx.x * HOP_IV_BLOCK + threadIdx.x;
-  if (id >= (int64_t)a.rows * slots) return;
+  __shared__ uint64_t fr_lds[HOP_IV_STAGE][FRAME_WORDS];
+  const int64_t n_ids = (int64_t)a.rows * slots;
+  const int64_t id0 = (int64_t)blockIdx.x * HOP_IV_BLOCK, id = id0 + threadIdx.x;
+  const int64_t idl = (id0 + HOP_IV_BLOCK < n_ids ? id0 + HOP_IV_BLOCK : n_ids) - 1;
+  // the frame index (into a.frames) of an id's left frame
+  auto left = [&](int64_t q) { return (q / slots) * a.frame_stride + a.s_begin / a.hop + q % slots; };
+  const int64_t f0 = left(id0), f1 = left(idl) + 1;  // the run the block's frames lie in
+  const bool staged = f1 - f0 + 1 <= HOP_IV_STAGE;  // (uniform over the block)
+  if (staged) {
+    const uint64_t *src = (const uint64_t *)(a.frames + f0);
+    const int words = (int)(f1 - f0 + 1) * FRAME_WORDS;
+    for (int w = threadIdx.x; w < words; w += HOP_IV_BLOCK) (&fr_lds[0][0])[w] = src[w];
+    __syncthreads();
+    for (int q = threadIdx.x; q < (int)(f1 - f0 + 1) * NPM; q += HOP_IV_BLOCK) {
+      double *ar = ((afs_frame *)fr_lds[q / NPM])->area_cm2 + q % NPM;
+      *ar = plan_clampA(*ar);
+    }
+    __syncthreads();
+  }
+  if (id >= n_ids) return;
   const int64_t row = id / slots, slot = id % slots;
   const HopRange r = hop_range(a, slot);
-  const afs_frame *fl = a.frames + row * a.frame_stride + r.h, *fr = fl + 1;
   PlanKey k;
-  bool ok = plan_hop_decide_iv<false>(fl, fr, a.hop, r.i0, r.i1, k);
+  bool ok;
+  const afs_frame *fl, *fr;
+  if (staged) {  // (two instantiations of the scans: LDS frames, areas clamped, and global frames)
+    fl = (const afs_frame *)fr_lds[left(id) - f0];
+    fr = fl + 1;
+    ok = plan_hop_decide_iv<true>(fl, fr, a.hop, r.i0, r.i1, k);
+  } else {
+    fl = a.frames + left(id);
+    fr = fl + 1;
+    ok = plan_hop_decide_iv<false>(fl, fr, a.hop, r.i0, r.i1, k);
+  }
   if (ok) {
     PlanHop &h = a.hops[row * a.hop_stride + slot];
     h = PlanHop{};
-    ok = plan_hop_inputs(k, fl, fr, a.uo, a.two_mass != 0, h);
+    ok = plan_hop_inputs(k, fl, fr, a.uo, a.two_mass != 0, h);  // (clampA is idempotent on staged areas)
   }
   if (!ok) a.work[2 + atomicAdd(a.work, 1u)] = (uint32_t)id;
 }

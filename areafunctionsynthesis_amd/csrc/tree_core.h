@@ -1031,18 +1031,23 @@ struct Target { uint32_t up; double tup, tdn, fc; bool on; };
 // The variants compute exactly the full phases' values (tree_kernel.h).  Ceiling measured with
 // every wave forced into a variant, 8192 static vowels (profiles/r05b_noise_variant_ceiling_ab.txt):
 // NZ 1 +4.8 %, NZ 2 +13 %.
-enum : int { NZ_FULL = 0, NZ_TONGUE1 = 1, NZ_GLOTTIS = 2, NZ_COUNT = 3 };
+// (heaviest first: the slot order's classes, tree_plan.h plan_noise_class16, use these values)
+enum : int { NZ_FULL = 0, NZ_T1ALL = 1, NZ_TONGUE1 = 2, NZ_GLOTTIS = 3, NZ_COUNT = 4 };
+#ifndef AFS_NZ_T1ALL
+#define AFS_NZ_T1ALL 0  // 1: also the variant of the glottis + first tongue constriction over all slots
+#endif
 template <int W, int NZ>
 struct NoiseV {
-  static constexpr int NC = NZ == NZ_FULL ? 4 : (NZ == NZ_TONGUE1 ? 2 : 1);
-  static constexpr int NS_ = NZ == NZ_FULL ? Shape<W>::NDP : (NZ == NZ_TONGUE1 ? 2 : 1);
+  static constexpr int NC = NZ == NZ_FULL ? 4 : (NZ == NZ_GLOTTIS ? 1 : 2);
+  static constexpr int NS_ = (NZ == NZ_FULL || NZ == NZ_T1ALL) ? Shape<W>::NDP : (NZ == NZ_TONGUE1 ? 2 : 1);
   static constexpr int NS = NS_ < Shape<W>::NDP ? NS_ : Shape<W>::NDP;
   // PlanHop::noise bits this variant serves: constrictions 0 .. NC-1, dipoles below NS * W
   static constexpr uint64_t SERVES = (((1ull << NC) - 1) << NOISE_CON0) |
                                      (NS * W >= 64 ? ((1ull << NOISE_CON0) - 1) : ((1ull << (NS * W)) - 1));
 };
 static_assert(NoiseV<16, NZ_GLOTTIS>::SERVES == NOISE_SERVES16_GLOTTIS &&
-                  NoiseV<16, NZ_TONGUE1>::SERVES == NOISE_SERVES16_TONGUE1,
+                  NoiseV<16, NZ_TONGUE1>::SERVES == NOISE_SERVES16_TONGUE1 &&
+                  NoiseV<16, NZ_T1ALL>::SERVES == NOISE_SERVES16_T1ALL,
               "tree_plan.h plan_noise_class16: the slot order's classes are the 16-lane variants");
 
 AFS_HD inline double narrow_flow(const double *X, uint32_t o0, uint32_t o1) {

@@ -275,8 +275,11 @@ AFS_HD inline uint64_t plan_key_noise(const PlanKey &k) {
 // frame (afs_capi.cpp shape_order).
 constexpr uint64_t NOISE_SERVES16_GLOTTIS = (1ull << NOISE_CON0) | 0xFFFFull;
 constexpr uint64_t NOISE_SERVES16_TONGUE1 = (3ull << NOISE_CON0) | 0xFFFFFFFFull;
-AFS_HD inline int plan_noise_class16(uint64_t m) {
-  return (m & ~NOISE_SERVES16_GLOTTIS) == 0 ? 2 : ((m & ~NOISE_SERVES16_TONGUE1) == 0 ? 1 : 0);
+constexpr uint64_t NOISE_SERVES16_T1ALL = (3ull << NOISE_CON0) | ((1ull << NOISE_CON0) - 1);
+AFS_HD inline int plan_noise_class16(uint64_t m, bool t1all) {
+  if ((m & ~NOISE_SERVES16_GLOTTIS) == 0) return 3;
+  if ((m & ~NOISE_SERVES16_TONGUE1) == 0) return 2;
+  return (t1all && (m & ~NOISE_SERVES16_T1ALL) == 0) ? 1 : 0;
 }
 // Two 64-bit words that are equal iff the keys are.
 AFS_HD inline void plan_key_pack(const PlanKey &k, uint64_t *q) {

@@ -84,6 +84,34 @@ long g_hops = 0, g_mixed_hops = 0;
 // 2's slot 0 (section 25's new pressure) is stored per sample, and tone_output_run adds the tone to the
 // hop's flows before the output filter -- as tree_kernel.h + tree_output_kernel.  Off by default.
 int g_tone_k6 = 0;
+// Noise-phase variants (the device's hop-mode default, tree_kernel.h noise_variant): each hop runs
+// in the lightest variant (tree_core.h NoiseV) that serves its record's noise mask and the dipole
+// slots still holding amplitude, the hop playing the part of a launch.  Off by default; counts of
+// the hops run in each variant since the last emu_tree_variant_counts.
+int g_noise_variants = 0;
+long g_variant_hops[NZ_COUNT] = {};
+
+template <int W>
+int emu_noise_variant(uint64_t m, const Lane<W> *R) {
+  for (int gl = 0; gl < W; ++gl)
+    for (int k = 0; k < Shape<W>::NDP; ++k)
+      if (R[gl].damp[k] != 0.0 && gl + k * W < NDIP) m |= 1ull << (gl + k * W);
+  int nz = NZ_FULL;
+  if ((m & ~NoiseV<W, NZ_T1ALL>::SERVES) == 0) nz = NZ_T1ALL;  // (every variant is emulated)
+  if ((m & ~NoiseV<W, NZ_TONGUE1>::SERVES) == 0) nz = NZ_TONGUE1;
+  if ((m & ~NoiseV<W, NZ_GLOTTIS>::SERVES) == 0) nz = NZ_GLOTTIS;
+  return nz;
+}
+
+template <int W, int MODEL, class Xc>
+void step_nz(int nz, Xc &ex, double *X, const Tables &T, double ratio, bool defer) {
+  switch (nz) {
+    case NZ_GLOTTIS: sample_step<W, MODEL, NZ_GLOTTIS>(ex, X, T.uni, T.consts, ratio, defer); break;
+    case NZ_TONGUE1: sample_step<W, MODEL, NZ_TONGUE1>(ex, X, T.uni, T.consts, ratio, defer); break;
+    case NZ_T1ALL: sample_step<W, MODEL, NZ_T1ALL>(ex, X, T.uni, T.consts, ratio, defer); break;
+    default: sample_step<W, MODEL, NZ_FULL>(ex, X, T.uni, T.consts, ratio, defer); break;
+  }
+}
 
 template <int W, bool TONE>
 long run_impl(const afs_frame *frames, int F, int hop, unsigned seed, double fs, const afs_options &opt,
@@ -111,6 +139,8 @@ long run_impl(const afs_frame *frames, int F, int hop, unsigned seed, double fs,
       g_mixed_hops += H.mixed ? 1 : 0;
     }
     const long t0 = t;
+    const int nz = (hops && g_noise_variants) ? emu_noise_variant<W>(H.noise, R.data()) : (int)NZ_FULL;
+    if (hops && g_noise_variants) ++g_variant_hops[nz];
     for (int i = 0; i < hop; ++i) {
       double ratio = (double)i / (double)hop;
       uint64_t w[PLAN_WORDS];  // K5's record of this sample (tree_plan.h)
@@ -120,9 +150,9 @@ long run_impl(const afs_frame *frames, int F, int hop, unsigned seed, double fs,
         plan_sample(frames + k - 1, frames + k, ratio, T.consts.sec, two, w);
       for (int gl = 0; gl < W; ++gl) R[gl].planw = w[gl % PLAN_WORDS];
       if (opt.glottis_model == AFS_GLOTTIS_TWO_MASS)
-        sample_step<W, AFS_GLOTTIS_TWO_MASS>(ex, X.data(), T.uni, T.consts, ratio, defer);
+        step_nz<W, AFS_GLOTTIS_TWO_MASS>(nz, ex, X.data(), T, ratio, defer);
       else
-        sample_step<W, AFS_GLOTTIS_TRIANGULAR>(ex, X.data(), T.uni, T.consts, ratio, defer);
+        step_nz<W, AFS_GLOTTIS_TRIANGULAR>(nz, ex, X.data(), T, ratio, defer);
       out[t] = R[0].sample;
       if constexpr (TONE) p25[i] = R[2].p[0];
       if (t < ndump) {
@@ -181,6 +211,14 @@ extern "C" long emu_tree_utterance_opt(const afs_frame *frames, int F, int hop, 
 
 extern "C" void emu_tree_set_hop_mode(int on) { g_hop_mode = on; }
 extern "C" void emu_tree_set_tone_k6(int on) { g_tone_k6 = on; }
+extern "C" void emu_tree_set_noise_variants(int on) { g_noise_variants = on; }
+// hops run in each noise-phase variant (NZ_FULL, NZ_T1ALL, NZ_TONGUE1, NZ_GLOTTIS) since the last call
+extern "C" void emu_tree_variant_counts(long *counts) {
+  for (int v = 0; v < NZ_COUNT; ++v) {
+    counts[v] = g_variant_hops[v];
+    g_variant_hops[v] = 0;
+  }
+}
 // hops run in hop mode since the last call, and how many of them were mixed
 extern "C" void emu_tree_hop_counts(long *hops, long *mixed) {
   *hops = g_hops;

@@ -240,3 +240,47 @@ def test_tone_in_k6_vs_in_step(emu, oracle, hop, skin):
         assert np.array_equal(x, y)
     z = oracle.utterance(frames, hop, 7, 22050.0, opt=opt)
     assert np.abs(x - z).max() <= TOL
+
+
+@pytest.mark.parametrize("W", [16, 64])
+def test_noise_variants_bitwise(emu, oracle, hop_mode, W):
+    """The noise-phase variants (tree_core.h NoiseV: the glottis source alone, glottis + first
+    tongue constriction below dipole 32, ...) chosen per hop from the hop record's noise mask and
+    the slots still holding amplitude, as the device chooses them per launch: the audio is the
+    full phases' bit for bit -- vowels (light variants), fricatives, and transitions between all
+    shapes (constrictions appearing and dying away across hops, a decaying amplitude keeping its
+    slot in the heavier variant)."""
+    from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS
+    from areafunctionsynthesis_amd.params import default_shapes
+    lib = emu.lib
+    lib.emu_tree_set_noise_variants.argtypes = [ctypes.c_int]
+    lib.emu_tree_variant_counts.argtypes = [ctypes.c_void_p]
+    sh = default_shapes()
+    names = sorted(sh)
+    rng = np.random.default_rng(21)
+    cases = []
+    for seq in (["a:"] * 4, ["i:"] * 4, ["s"] * 4, ["u:", "S", "a:", "f"], ["(a)b(a):", "i:", "l", "u:"]):
+        cases.append(seq)
+    for k in range(0, len(names), 5):
+        cases.append([names[(k + j) % len(names)] for j in range(4)])
+    used = np.zeros(4, dtype=np.int64)
+    for n, seq in enumerate(cases):
+        frames = np.stack([oracle.af_to_frame(sh[x]) for x in seq] + [oracle.af_to_frame(sh[seq[-1]])])
+        frames["glottis"] = DEFAULT_GLOTTIS
+        frames["glottis"][:, 0] = 100.0 + 10.0 * rng.random(5)
+        frames["velum_opening_cm2"] = rng.random(5) * (n % 2)
+        ys = []
+        for on in (0, 1):
+            lib.emu_tree_set_noise_variants(on)
+            try:
+                ys.append(emu(frames, 97, n + 1, 44100.0, W=W))
+            finally:
+                lib.emu_tree_set_noise_variants(0)
+            c = np.zeros(4, dtype=np.int64)
+            lib.emu_tree_variant_counts(c.ctypes.data)
+            used += c
+        assert np.array_equal(ys[0], ys[1]), (seq, W)
+    assert used[0] > 0 and used[3] > 0, used  # (the full phases and the glottis-only variant both ran)
+    if W == 16:
+        assert used[1] > 0 and used[2] > 0, used  # (and both tongue variants)
+    hop_mode()
