@@ -12,8 +12,8 @@
 #include "afs_model.h"
 #include "tree_plan.h"
 
-#ifndef AFS_NZ_T1ALL
-#define AFS_NZ_T1ALL 0  // (tree_core.h)
+#ifndef AFS_NZ_SET
+#define AFS_NZ_SET 3  // (tree_core.h)
 #endif
 
 namespace afs {
@@ -174,7 +174,7 @@ __global__ void utterance_key_kernel(const afs_frame *frames, int64_t fstride, i
   tree::PlanKey k;
   double obst[4], po[4];
   plan_decide(tree::PlanGeomT<false>{f, f, 1.0, 0.0}, k, obst, po);  // (the first frame's decisions)
-  const uint64_t cls = noise_class ? (uint64_t)tree::plan_noise_class16(tree::plan_key_noise(k), AFS_NZ_T1ALL) : 0;
+  const uint64_t cls = noise_class ? (uint64_t)tree::plan_noise_class16(tree::plan_key_noise(k), AFS_NZ_SET) : 0;
   keys[u] = (cls << 48) | ((uint64_t)bucket << 40) | ((uint64_t)imin << 32) | (uint64_t)__float_as_uint(af);
 }
 

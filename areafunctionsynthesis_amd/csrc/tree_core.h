@@ -1033,9 +1033,14 @@ struct Target { uint32_t up; double tup, tdn, fc; bool on; };
 // NZ 1 +4.8 %, NZ 2 +13 %.
 // (heaviest first: the slot order's classes, tree_plan.h plan_noise_class16, use these values)
 enum : int { NZ_FULL = 0, NZ_T1ALL = 1, NZ_TONGUE1 = 2, NZ_GLOTTIS = 3, NZ_COUNT = 4 };
-#ifndef AFS_NZ_T1ALL
-#define AFS_NZ_T1ALL 0  // 1: also the variant of the glottis + first tongue constriction over all slots
+// The variants compiled into the hop-mode kernel, a bit mask: 1 NZ_TONGUE1, 2 NZ_GLOTTIS,
+// 4 NZ_T1ALL (each a whole copy of the kernel body: the instruction cache, shared by a CU pair,
+// holds about one, so every variant costs the waves of the other variants on the same CUs;
+// profiles/r05c_variants_ab.txt, r05d_variants_ab.txt)
+#ifndef AFS_NZ_SET
+#define AFS_NZ_SET 3
 #endif
+#define AFS_NZ_T1ALL ((AFS_NZ_SET & 4) != 0)
 template <int W, int NZ>
 struct NoiseV {
   static constexpr int NC = NZ == NZ_FULL ? 4 : (NZ == NZ_GLOTTIS ? 1 : 2);

@@ -202,9 +202,9 @@ __device__ __forceinline__ int noise_variant(const TreeArgs &a) {
 #pragma unroll
   for (int o = 32; o >= 1; o /= 2) m |= __shfl_xor(m, o, 64);
   int nz = NZ_FULL;
-  if (AFS_NZ_T1ALL && (m & ~NoiseV<W, NZ_T1ALL>::SERVES) == 0) nz = NZ_T1ALL;
-  if ((m & ~NoiseV<W, NZ_TONGUE1>::SERVES) == 0) nz = NZ_TONGUE1;
-  if ((m & ~NoiseV<W, NZ_GLOTTIS>::SERVES) == 0) nz = NZ_GLOTTIS;
+  if ((AFS_NZ_SET & 4) && (m & ~NoiseV<W, NZ_T1ALL>::SERVES) == 0) nz = NZ_T1ALL;
+  if ((AFS_NZ_SET & 1) && (m & ~NoiseV<W, NZ_TONGUE1>::SERVES) == 0) nz = NZ_TONGUE1;
+  if ((AFS_NZ_SET & 2) && (m & ~NoiseV<W, NZ_GLOTTIS>::SERVES) == 0) nz = NZ_GLOTTIS;
   return __builtin_amdgcn_readfirstlane(a.noise_variants ? nz : (int)NZ_FULL);
 }
 
@@ -357,12 +357,22 @@ template <bool PROF, int MODEL, bool HOPS = false, int W = TW>
 __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &lds, uint64_t *prof) {
   if constexpr (HOPS) {
     const int nz = noise_variant<W>(a);
-    if (nz == NZ_GLOTTIS) tree_synth_run<PROF, MODEL, HOPS, W, NZ_GLOTTIS>(a, lds, prof);
-    else if (nz == NZ_TONGUE1) tree_synth_run<PROF, MODEL, HOPS, W, NZ_TONGUE1>(a, lds, prof);
-#if AFS_NZ_T1ALL
-    else if (nz == NZ_T1ALL) tree_synth_run<PROF, MODEL, HOPS, W, NZ_T1ALL>(a, lds, prof);
+    if (false) {
+#if AFS_NZ_SET & 2
+    } else if (nz == NZ_GLOTTIS) {
+      tree_synth_run<PROF, MODEL, HOPS, W, NZ_GLOTTIS>(a, lds, prof);
 #endif
-    else tree_synth_run<PROF, MODEL, HOPS, W, NZ_FULL>(a, lds, prof);
+#if AFS_NZ_SET & 1
+    } else if (nz == NZ_TONGUE1) {
+      tree_synth_run<PROF, MODEL, HOPS, W, NZ_TONGUE1>(a, lds, prof);
+#endif
+#if AFS_NZ_SET & 4
+    } else if (nz == NZ_T1ALL) {
+      tree_synth_run<PROF, MODEL, HOPS, W, NZ_T1ALL>(a, lds, prof);
+#endif
+    } else {
+      tree_synth_run<PROF, MODEL, HOPS, W, NZ_FULL>(a, lds, prof);
+    }
   } else {
     tree_synth_run<PROF, MODEL, HOPS, W, NZ_FULL>(a, lds, prof);
   }

@@ -276,10 +276,10 @@ AFS_HD inline uint64_t plan_key_noise(const PlanKey &k) {
 constexpr uint64_t NOISE_SERVES16_GLOTTIS = (1ull << NOISE_CON0) | 0xFFFFull;
 constexpr uint64_t NOISE_SERVES16_TONGUE1 = (3ull << NOISE_CON0) | 0xFFFFFFFFull;
 constexpr uint64_t NOISE_SERVES16_T1ALL = (3ull << NOISE_CON0) | ((1ull << NOISE_CON0) - 1);
-AFS_HD inline int plan_noise_class16(uint64_t m, bool t1all) {
-  if ((m & ~NOISE_SERVES16_GLOTTIS) == 0) return 3;
-  if ((m & ~NOISE_SERVES16_TONGUE1) == 0) return 2;
-  return (t1all && (m & ~NOISE_SERVES16_T1ALL) == 0) ? 1 : 0;
+AFS_HD inline int plan_noise_class16(uint64_t m, int set) {  // set: the variants compiled (AFS_NZ_SET)
+  if ((set & 2) && (m & ~NOISE_SERVES16_GLOTTIS) == 0) return 3;
+  if ((set & 1) && (m & ~NOISE_SERVES16_TONGUE1) == 0) return 2;
+  return ((set & 4) && (m & ~NOISE_SERVES16_T1ALL) == 0) ? 1 : 0;
 }
 // Two 64-bit words that are equal iff the keys are.
 AFS_HD inline void plan_key_pack(const PlanKey &k, uint64_t *q) {
