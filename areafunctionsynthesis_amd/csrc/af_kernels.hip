@@ -150,16 +150,17 @@ __global__ void target_frames_kernel(const double *seq, int Q, TargetPlan t, int
   for (int j = 0; j < 6; ++j) fr->glottis[j] = gp[j];
 }
 
-// The shape key of utterance u (shape_order, afs_capi.cpp), from its first frame: the noise
-// class of its decisions (tree_plan.h plan_noise_class16: the synthesis kernel's noise-phase
-// variant -- the full phases first, the lightest last, so that a wave's four utterances share
-// one variant and the heavy blocks start first), then how narrow the tube is at its narrowest (in
-// half-octave buckets of the area), then where (section index), then the area itself (a float's
-// bits: positive floats order as their bits).  Ascending, the narrowest constrictions -- the
-// utterances with turbulence noise, the heaviest -- come first and alike shapes sit together.
-// (Measured against the section-major key: +0.8 % static vowels, equal on fricatives; descending:
-// -1.3 %; profiles/r04v_shape_key_ab.txt.)  A NaN area counts as wide.
-__global__ void utterance_key_kernel(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, bool noise_class) {
+// The shape key of utterance u (shape_order, afs_capi.cpp), from its first frame: how narrow the
+// tube is at its narrowest (in half-octave buckets of the area), then the noise class of its
+// decisions (tree_plan.h plan_noise_class16: the synthesis kernel's noise-phase variant, the full
+// phases first, so that a wave's four utterances share one variant), then where (section index),
+// then the area itself (a float's bits: positive floats order as their bits).  Ascending, the
+// narrowest constrictions -- the utterances with turbulence noise, the heaviest -- come first and
+// alike shapes sit together.  (Measured against the section-major key: +0.8 % static vowels, equal
+// on fricatives; descending: -1.3 %; profiles/r04v_shape_key_ab.txt.  The class as the first key
+// instead of the second: within 0.2 %, profiles/r05g_class_key_ab.txt; no class key with the
+// variants: -5 %, r05c_variants_ab.txt.)  A NaN area counts as wide.
+__global__ void utterance_key_kernel(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, int noise_class) {
   const int u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= B) return;
   const afs_frame *f = frames + (int64_t)u * fstride;
@@ -175,12 +176,14 @@ __global__ void utterance_key_kernel(const afs_frame *frames, int64_t fstride, i
   double obst[4], po[4];
   plan_decide(tree::PlanGeomT<false>{f, f, 1.0, 0.0}, k, obst, po);  // (the first frame's decisions)
   const uint64_t cls = noise_class ? (uint64_t)tree::plan_noise_class16(tree::plan_key_noise(k), AFS_NZ_SET) : 0;
-  keys[u] = (cls << 48) | ((uint64_t)bucket << 40) | ((uint64_t)imin << 32) | (uint64_t)__float_as_uint(af);
+  keys[u] = noise_class == 2  // (the class after the narrowness bucket)
+                ? ((uint64_t)bucket << 48) | (cls << 40) | ((uint64_t)imin << 32) | (uint64_t)__float_as_uint(af)
+                : (cls << 48) | ((uint64_t)bucket << 40) | ((uint64_t)imin << 32) | (uint64_t)__float_as_uint(af);
 }
 
 }  // namespace
 
-hipError_t launch_utterance_keys(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, bool noise_class,
+hipError_t launch_utterance_keys(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, int noise_class,
                                  hipStream_t st) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(utterance_key_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, frames, fstride, B,

@@ -31,8 +31,9 @@ hipError_t launch_target_frames(const double *seq, int Q, const TargetPlan &plan
 
 // keys[u] = the shape key of utterance u's first frame frames[u * fstride] (how narrow its tube is
 // and where), for the slot order of the tree kernel (afs_capi.cpp shape_order).
-// (noise_class: the noise class as the key's first field, af_kernels.hip)
-hipError_t launch_utterance_keys(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, bool noise_class,
+// (noise_class: 1 the noise class as the key's first field, 2 after the narrowness bucket, 0 not
+// in the key; af_kernels.hip)
+hipError_t launch_utterance_keys(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, int noise_class,
                                  hipStream_t st);
 
 }  // namespace afs

@@ -468,7 +468,7 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   if (const char *e = std::getenv("AFS_XCD_ORDER")) ctx->xcd_order = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_SHAPE_ORDER")) ctx->shape_order = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_NOISE_VARIANTS")) ctx->noise_variants = std::atoi(e) != 0;
-  if (const char *e = std::getenv("AFS_CLASS_ORDER")) ctx->class_order = std::atoi(e) != 0;
+  if (const char *e = std::getenv("AFS_CLASS_ORDER")) ctx->class_order = std::atoi(e);
   if (const char *e = std::getenv("AFS_LAUNCH_SAMPLES")) {  // (A/B and latency studies: samples per K1 launch)
     const long long v = std::atoll(e);
     if (v > 0) ctx->launch_cap = std::min<int64_t>(v, 65536);
@@ -558,7 +558,7 @@ static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstr
   if ((s = ensure(c, &c->keys, &c->keys_bytes, kbytes + obytes)) != AFS_OK) return s;
   uint64_t *dkeys = (uint64_t *)c->keys;
   int32_t *dorder = (int32_t *)((char *)c->keys + kbytes);
-  HIP_TRY(c, afs::launch_utterance_keys(dframes, fstride, B, dkeys, c->noise_variants && c->class_order, c->stream));
+  HIP_TRY(c, afs::launch_utterance_keys(dframes, fstride, B, dkeys, c->class_order, c->stream));
   c->hkeys.resize((size_t)B);
   HIP_TRY(c, hipMemcpyAsync(c->hkeys.data(), dkeys, kbytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -47,7 +47,7 @@ struct afs_ctx {
   int64_t launch_cap = 65536;          // samples per K1 launch at most (AFS_LAUNCH_SAMPLES lowers it)
   bool shape_order = true;             // AFS_SHAPE_ORDER=0: afs_synthesize's utterances in call order
   bool noise_variants = true;          // AFS_NOISE_VARIANTS=0: K1 always runs the full noise phases
-  bool class_order = true;             // AFS_CLASS_ORDER=0: the slot order ignores the noise classes (A/B)
+  int class_order = 2;                 // AFS_CLASS_ORDER: the slot order's noise-class key (af_kernels.hip; A/B)
   void *keys = nullptr;                // shape keys (device) and the slot order built from them
   size_t keys_bytes = 0;
   std::vector<uint64_t> hkeys;

@@ -1032,7 +1032,8 @@ struct Target { uint32_t up; double tup, tdn, fc; bool on; };
 // every wave forced into a variant, 8192 static vowels (profiles/r05b_noise_variant_ceiling_ab.txt):
 // NZ 1 +4.8 %, NZ 2 +13 %.
 // (heaviest first: the slot order's classes, tree_plan.h plan_noise_class16, use these values)
-enum : int { NZ_FULL = 0, NZ_T1ALL = 1, NZ_TONGUE1 = 2, NZ_GLOTTIS = 3, NZ_COUNT = 4 };
+enum : int { NZ_FULL = 0, NZ_T1ALL = 1, NZ_TONGUE1 = 2, NZ_GLOTTIS = 3, NZ_COUNT = 4,
+             NZ_DYN = -1 };  // NZ_DYN: the variant chosen at run time, in a phase of its own (sample_step)
 // The variants compiled into the hop-mode kernel, a bit mask: 1 NZ_TONGUE1, 2 NZ_GLOTTIS,
 // 4 NZ_T1ALL (each a whole copy of the kernel body: the instruction cache, shared by a CU pair,
 // holds about one, so every variant costs the waves of the other variants on the same CUs;
@@ -1949,7 +1950,7 @@ AFS_HD inline double phase_output(double *X, const Uni &U, const Consts &C, doub
 // ---------------------------------------------------------------------------
 
 template <int W, int MODEL, bool VARLOSS, int NZ, class Xc>
-AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
+AFS_HD inline double geometry_network(Xc &x, double *X, const Uni &U, const Consts &C, double ratio) {
   // the glottis of this sample: its loads first, its stores (displacements, interpolated
   // controls) at the end of the block, so that the network and the targets need not wait for
   // the glottis chain before they load
@@ -1968,25 +1969,19 @@ AFS_HD inline void geometry_network(Xc &x, double *X, const Uni &U, const Consts
   x.dyn_neighbors();
   x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS>(gl, R, X, U, C, g.go); });
   x.mark(PH_NETWORK);
-  x.par([&](int gl, Lane<W> &R) { phase_targets<W, NZ>(x, gl, R, X, C, g.go.a1); });
+  // (NZ_DYN: the targets run after the block, in the variant's noise phase)
+  if constexpr (NZ != NZ_DYN) x.par([&](int gl, Lane<W> &R) { phase_targets<W, NZ>(x, gl, R, X, C, g.go.a1); });
   x.par_uniform([&](int gl, Lane<W> &R) { (void)gl; (void)R; },
                 [&](Lane<W> &R) { (void)R; glottis_commit(X, g); });
+  return g.go.a1;
 }
 
-// One audio sample at `ratio` with glottis model MODEL (one kernel per model: a kernel holding
-// both models' code needs more registers than the SIMD has) and noise-phase variant NZ.
-template <int W, int MODEL, int NZ = NZ_FULL, class Xc>
-AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio, bool defer_out) {
-  static_assert(W >= TREE_CHAINS, "every solver lane needs a lane of the utterance");
-  // geometry and network in one block (no LDS round trip between them): the interpolated
-  // areas stay in the lanes, the neighbours' come by lane exchange, the glottis values are
-  // lane-uniform
-  // (one instantiation per glottis model and entrance-loss kind: no option branch in the block)
-  const bool varloss = U.opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE;
-  if (varloss) geometry_network<W, MODEL, true, NZ>(x, X, U, C, ratio);
-  else geometry_network<W, MODEL, false, NZ>(x, X, U, C, ratio);
-  x.sync();
-  x.mark(PH_TARGETS);
+// The targets and noise phases of variant NZ (NZ_DYN: sample_step), after the geometry / network
+// block: a phase of their own between two wave fences, so that the variants' branch splits no
+// block the scheduler interleaves.
+template <int W, int NZ, class Xc>
+AFS_HD inline void targets_noise(Xc &x, double *X, const Uni &U, const Consts &C, double a_glot_up) {
+  x.par([&](int gl, Lane<W> &R) { phase_targets<W, NZ>(x, gl, R, X, C, a_glot_up); });
   if (U.opt.generate_noise_sources) {
     phase_noise<W, NZ>(x, X, U, C);
   } else {
@@ -1994,6 +1989,45 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
       (void)R;
       for (int d = gl; d < NDIP; d += W) X[X_SMP + d] = 0.0;
     });
+  }
+}
+
+// One audio sample at `ratio` with glottis model MODEL (one kernel per model: a kernel holding
+// both models' code needs more registers than the SIMD has) and noise-phase variant NZ.
+// NZ = NZ_DYN: the noise-phase variant nz (wave-uniform) is chosen at run time in the phase after
+// the geometry / network block (one copy of everything else); any other NZ: that variant, the
+// targets inside the block.
+template <int W, int MODEL, int NZ = NZ_FULL, class Xc>
+AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, double ratio, bool defer_out,
+                               int nz = NZ_FULL) {
+  static_assert(W >= TREE_CHAINS, "every solver lane needs a lane of the utterance");
+  // geometry and network in one block (no LDS round trip between them): the interpolated
+  // areas stay in the lanes, the neighbours' come by lane exchange, the glottis values are
+  // lane-uniform
+  // (one instantiation per glottis model and entrance-loss kind: no option branch in the block)
+  const bool varloss = U.opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE;
+  const double a_glot_up = varloss ? geometry_network<W, MODEL, true, NZ>(x, X, U, C, ratio)
+                                   : geometry_network<W, MODEL, false, NZ>(x, X, U, C, ratio);
+  x.sync();
+  x.mark(PH_TARGETS);
+  if constexpr (NZ == NZ_DYN) {
+    (void)nz;
+    // (only the variants of AFS_NZ_SET are compiled; the CPU emulator compiles them all)
+    if ((AFS_NZ_SET & 2) && nz == NZ_GLOTTIS) targets_noise<W, NZ_GLOTTIS>(x, X, U, C, a_glot_up);
+    else if ((AFS_NZ_SET & 1) && nz == NZ_TONGUE1) targets_noise<W, NZ_TONGUE1>(x, X, U, C, a_glot_up);
+    else if ((AFS_NZ_SET & 4) && nz == NZ_T1ALL) targets_noise<W, NZ_T1ALL>(x, X, U, C, a_glot_up);
+    else targets_noise<W, NZ_FULL>(x, X, U, C, a_glot_up);
+  } else {
+    (void)a_glot_up;
+    (void)nz;
+    if (U.opt.generate_noise_sources) {
+      phase_noise<W, NZ>(x, X, U, C);
+    } else {
+      x.par([&](int gl, Lane<W> &R) {
+        (void)R;
+        for (int d = gl; d < NDIP; d += W) X[X_SMP + d] = 0.0;
+      });
+    }
   }
   x.sync();
   x.mark(PH_NOISE);

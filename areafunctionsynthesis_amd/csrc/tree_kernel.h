@@ -213,7 +213,8 @@ __device__ __forceinline__ int noise_variant(const TreeArgs &a) {
 // gl's kind and inputs for the hop and evaluates the word at every sample; a mixed hop's samples
 // read their dense records as without HOPS.
 template <bool PROF, int MODEL, bool HOPS, int W, int NZ>
-__device__ __forceinline__ void tree_synth_run(const TreeArgs &a, WaveLdsT<W> &lds, uint64_t *prof) {
+__device__ __forceinline__ void tree_synth_run(const TreeArgs &a, WaveLdsT<W> &lds, uint64_t *prof,
+                                               int nz = NZ_FULL) {
   constexpr int UPB_ = Geom<W>::UPB, WPB_ = Geom<W>::WPB;
   const int lane = threadIdx.x;  // 0 .. 64 WPB - 1
   const int g = lane / W, gl = lane % W;
@@ -300,7 +301,7 @@ __device__ __forceinline__ void tree_synth_run(const TreeArgs &a, WaveLdsT<W> &l
       next = pl[tn * PLAN_WORDS];  // the next sample's word, a sample ahead
       if (i + 1 == hop && t + 1 < n) nf.load(gl, fu + k + 1);
     }
-    sample_step<W, MODEL, NZ>(ex, X, a.uni, C, ratio, true);
+    sample_step<W, MODEL, NZ>(ex, X, a.uni, C, ratio, true, nz);
     {
       const int j = (o_line + (int)t) & 15;  // the sample's position in its line
       const double p25v = GpuExec<PROF, W>::template dpp<0x152>(R.p[0]);  // lane 2's p[25] to its row
@@ -353,9 +354,14 @@ __device__ __forceinline__ void tree_synth_run(const TreeArgs &a, WaveLdsT<W> &l
 // The kernel body: in hop mode each wave picks its noise-phase variant for the launch
 // (noise_variant) and runs the whole body compiled for it.  (The waves of a block may take
 // different variants: each reaches the one __syncthreads of the table staging in its own copy.)
+#ifndef AFS_NZ_INNER
+#define AFS_NZ_INNER 0  // 1: one body, the variant switched in the noise phase (NZ_DYN); 0: a body per variant
+#endif
 template <bool PROF, int MODEL, bool HOPS = false, int W = TW>
 __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &lds, uint64_t *prof) {
-  if constexpr (HOPS) {
+  if constexpr (HOPS && AFS_NZ_INNER) {
+    tree_synth_run<PROF, MODEL, HOPS, W, NZ_DYN>(a, lds, prof, noise_variant<W>(a));
+  } else if constexpr (HOPS) {
     const int nz = noise_variant<W>(a);
     if (false) {
 #if AFS_NZ_SET & 2

@@ -103,14 +103,12 @@ int emu_noise_variant(uint64_t m, const Lane<W> *R) {
   return nz;
 }
 
+// (variants on: the device's arrangement, the variant switched at run time in the phase after the
+// geometry / network block, NZ_DYN; off: the full phases with the targets inside the block)
 template <int W, int MODEL, class Xc>
 void step_nz(int nz, Xc &ex, double *X, const Tables &T, double ratio, bool defer) {
-  switch (nz) {
-    case NZ_GLOTTIS: sample_step<W, MODEL, NZ_GLOTTIS>(ex, X, T.uni, T.consts, ratio, defer); break;
-    case NZ_TONGUE1: sample_step<W, MODEL, NZ_TONGUE1>(ex, X, T.uni, T.consts, ratio, defer); break;
-    case NZ_T1ALL: sample_step<W, MODEL, NZ_T1ALL>(ex, X, T.uni, T.consts, ratio, defer); break;
-    default: sample_step<W, MODEL, NZ_FULL>(ex, X, T.uni, T.consts, ratio, defer); break;
-  }
+  if (g_noise_variants) sample_step<W, MODEL, NZ_DYN>(ex, X, T.uni, T.consts, ratio, defer, nz);
+  else sample_step<W, MODEL, NZ_FULL>(ex, X, T.uni, T.consts, ratio, defer);
 }
 
 template <int W, bool TONE>
