@@ -152,7 +152,7 @@ std::vector<int32_t> xcd_order(const std::vector<int32_t> &row, int B, int upb, 
 
 afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int rows, int ntrans, int hop,
                       double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B,
-                      int width, const int32_t *frame_row = nullptr, const int32_t *order = nullptr) {
+                      int width, const int32_t *frame_row = nullptr, const int32_t *order = nullptr, int grid = 0) {
   if (tree(c)) {
     const int64_t S = (int64_t)ntrans * hop;
     const int two = c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0;
@@ -177,7 +177,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
                      int64_t hop_stride, int64_t p25_stride) -> afs_status {
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride, plan, plan_stride, lanes,
                       (double *)ws, B, c->host_tab.uni, hops, hop_stride, p25_row0(s0), p25_stride, order,
-                      c->noise_variants ? 1 : 0};
+                      c->noise_variants ? 1 : 0, grid};
       hipEvent_t e1 = prof_event(c);
       HIP_TRY(c, afs::launch_tree_synth(a, width, c->stream));
       hipEvent_t e2 = prof_event(c);
@@ -500,6 +500,7 @@ void afs_destroy(afs_ctx *c) {
   if (c->stage_seeds) (void)hipFree(c->stage_seeds);
   if (c->tgt) (void)hipFree(c->tgt);
   if (c->keys) (void)hipFree(c->keys);
+  if (c->order_buf) (void)hipFree(c->order_buf);
   if (c->plan_stream) (void)hipStreamSynchronize(c->plan_stream);
   if (c->plan) (void)hipFree(c->plan);
   if (c->plan2) (void)hipFree(c->plan2);
@@ -548,27 +549,73 @@ afs_status afs_synchronize(afs_ctx *c) {
 // a host sort per call; off for the voice kernel (one utterance per wave), batches of one block and
 // AFS_SHAPE_ORDER=0.
 static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstride, int B, int width,
-                              const int32_t **dord) {
+                              const int32_t **dord, int *grid) {
   *dord = nullptr;
+  *grid = 0;
   const int upb = afs::TREE_UPB;
   if (!tree(c) || !c->shape_order || width == afs::TREE_VOICE_W || B <= upb) return AFS_OK;
   const int nb = (B + upb - 1) / upb;
-  const size_t kbytes = (size_t)B * sizeof(uint64_t), obytes = (size_t)nb * upb * sizeof(int32_t);
+  const bool by_xcd = c->class_order == 3 && c->noise_variants;
   afs_status s;
-  if ((s = ensure(c, &c->keys, &c->keys_bytes, kbytes + obytes)) != AFS_OK) return s;
+  if ((s = ensure(c, &c->keys, &c->keys_bytes, (size_t)B * sizeof(uint64_t))) != AFS_OK) return s;
   uint64_t *dkeys = (uint64_t *)c->keys;
-  int32_t *dorder = (int32_t *)((char *)c->keys + kbytes);
-  HIP_TRY(c, afs::launch_utterance_keys(dframes, fstride, B, dkeys, c->class_order, c->stream));
+  HIP_TRY(c, afs::launch_utterance_keys(dframes, fstride, B, dkeys, by_xcd ? 1 : (c->class_order == 3 ? 0 : c->class_order),
+                                        c->stream));
   c->hkeys.resize((size_t)B);
-  HIP_TRY(c, hipMemcpyAsync(c->hkeys.data(), dkeys, kbytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->hkeys.data(), dkeys, (size_t)B * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   std::vector<int32_t> idx((size_t)B);
   for (int u = 0; u < B; ++u) idx[(size_t)u] = u;
   std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) { return c->hkeys[(size_t)a] < c->hkeys[(size_t)b]; });
-  c->horder.assign((size_t)nb * upb, B);
-  for (int q = 0; q < B; ++q) c->horder[(size_t)q] = idx[(size_t)q];
-  HIP_TRY(c, hipMemcpyAsync(dorder, c->horder.data(), obytes, hipMemcpyHostToDevice, c->stream));
-  *dord = dorder;
+  int nblocks = nb;
+  if (!by_xcd) {
+    c->horder.assign((size_t)nb * upb, B);
+    for (int q = 0; q < B; ++q) c->horder[(size_t)q] = idx[(size_t)q];
+  } else {
+    // The blocks of the class-major order (the full noise phases first) dealt to the 8 XCDs in
+    // contiguous runs of equal expected cost, so that the blocks one XCD runs -- whose waves share
+    // its CUs' instruction caches -- run one noise-phase variant (at most one change per XCD): a
+    // CU pair holds about one copy of the kernel body, and waves of different variants on it
+    // slowed each other (profiles/r05i_fricatives_variants_ab.txt).  Blocks are dealt to XCDs
+    // round-robin (block b runs on XCD b % 8, MI355X_MICROARCH.md), so run x occupies grid
+    // blocks x, x + 8, ...; the shorter runs end in empty blocks, which exit at once.  Expected
+    // cost of a block: that of its heaviest utterance's variant, from the ceilings measured with
+    // every wave in one variant (profiles/r05b_noise_variant_ceiling_ab.txt).
+    constexpr int XCDS = 8;
+    static const double cost[4] = {1.0, 0.976, 0.954, 0.885};  // NZ_FULL, NZ_T1ALL, NZ_TONGUE1, NZ_GLOTTIS
+    std::vector<double> bc((size_t)nb, 0.0);
+    double total = 0.0;
+    for (int b = 0; b < nb; ++b) {
+      double w = 0.0;
+      for (int g = 0; g < upb && b * upb + g < B; ++g)
+        w = std::max(w, cost[(c->hkeys[(size_t)idx[(size_t)(b * upb + g)]] >> 48) & 3]);
+      bc[(size_t)b] = w;
+      total += w;
+    }
+    std::vector<int> first(XCDS + 1, nb);
+    first[0] = 0;
+    double acc = 0.0;
+    int x = 1;
+    for (int b = 0; b < nb && x < XCDS; ++b) {
+      acc += bc[(size_t)b];
+      if (acc >= total * x / XCDS) first[(size_t)x++] = b + 1;
+    }
+    for (; x < XCDS; ++x) first[(size_t)x] = nb;
+    int len = 0;
+    for (int q = 0; q < XCDS; ++q) len = std::max(len, first[(size_t)q + 1] - first[(size_t)q]);
+    nblocks = XCDS * len;
+    c->horder.assign((size_t)nblocks * upb, B);
+    for (int q = 0; q < XCDS; ++q)
+      for (int b = first[(size_t)q]; b < first[(size_t)q + 1]; ++b) {
+        const int slot = (q + XCDS * (b - first[(size_t)q])) * upb;
+        for (int g = 0; g < upb && b * upb + g < B; ++g) c->horder[(size_t)(slot + g)] = idx[(size_t)(b * upb + g)];
+      }
+  }
+  const size_t obytes = c->horder.size() * sizeof(int32_t);
+  if ((s = ensure(c, &c->order_buf, &c->order_bytes, obytes)) != AFS_OK) return s;
+  HIP_TRY(c, hipMemcpyAsync(c->order_buf, c->horder.data(), obytes, hipMemcpyHostToDevice, c->stream));
+  *dord = (const int32_t *)c->order_buf;
+  *grid = nblocks;
   return AFS_OK;
 }
 
@@ -611,9 +658,10 @@ static afs_status synth_core(afs_ctx *c, const afs_frame *frames, const uint32_t
   if ((s = reset_state(c, c->ws, c->rng, c->tree_lanes, bp, B, dseeds, width)) != AFS_OK) return s;
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
   const int32_t *dord = nullptr;
-  if ((s = shape_order(c, dframes, F, B, width, &dord)) != AFS_OK) return s;
+  int grid = 0;
+  if ((s = shape_order(c, dframes, F, B, width, &dord, &grid)) != AFS_OK) return s;
   if ((s = run_chunks(c, dframes, F, B, F - 1, hop, dout, T, c->ws, c->rng, c->tree_lanes, bp, B, width, nullptr,
-                      dord)) != AFS_OK)
+                      dord, grid)) != AFS_OK)
     return s;
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   c->last_B = B;

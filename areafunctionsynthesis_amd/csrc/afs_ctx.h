@@ -48,8 +48,10 @@ struct afs_ctx {
   bool shape_order = true;             // AFS_SHAPE_ORDER=0: afs_synthesize's utterances in call order
   bool noise_variants = true;          // AFS_NOISE_VARIANTS=0: K1 always runs the full noise phases
   int class_order = 2;                 // AFS_CLASS_ORDER: the slot order's noise-class key (af_kernels.hip; A/B)
-  void *keys = nullptr;                // shape keys (device) and the slot order built from them
+  void *keys = nullptr;                // shape keys (device)
   size_t keys_bytes = 0;
+  void *order_buf = nullptr;           // the slot order built from them (device)
+  size_t order_bytes = 0;
   std::vector<uint64_t> hkeys;
   std::vector<int32_t> horder;
   hipStream_t plan_stream = nullptr;  // K5 of the next launch, beside K1 of this one (overlap)

@@ -41,6 +41,9 @@ struct TreeArgs {
   // hop mode: run each wave's launch in the lightest noise-phase variant its hop records allow
   // (tree_kernel.h noise_variant; 0: always the full phases -- AFS_NOISE_VARIANTS=0, A/B and tests)
   int noise_variants = 1;
+  // blocks of the launch (0: enough for B utterances); with `order`, blocks whose slots are all
+  // padding exit at once (the XCD-dealt slot order of afs_capi.cpp shape_order)
+  int grid_blocks = 0;
 };
 // K5: the noise-source plans of samples [s_begin, s_end) of `rows` frame rows.
 struct PlanArgs {

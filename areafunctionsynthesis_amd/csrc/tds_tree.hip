@@ -139,7 +139,7 @@ hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const u
 template <int W>
 static void launch_synth_w(const TreeArgs &a, hipStream_t st) {
   constexpr int UPB_ = Geom<W>::UPB;
-  const dim3 grid((a.B + UPB_ - 1) / UPB_), block(64 * Geom<W>::WPB);
+  const dim3 grid(a.grid_blocks > 0 ? a.grid_blocks : (a.B + UPB_ - 1) / UPB_), block(64 * Geom<W>::WPB);
   const bool two = a.uni.opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
   if (a.hops) {
     if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true, W>), grid, block, 0, st, a);

@@ -359,6 +359,12 @@ __device__ __forceinline__ void tree_synth_run(const TreeArgs &a, WaveLdsT<W> &l
 #endif
 template <bool PROF, int MODEL, bool HOPS = false, int W = TW>
 __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &lds, uint64_t *prof) {
+  if (a.order) {  // a block of padding slots only (the XCD-dealt slot order) has nothing to do
+    bool any = false;
+#pragma unroll
+    for (int g = 0; g < Geom<W>::UPB; ++g) any |= a.order[blockIdx.x * Geom<W>::UPB + g] < a.B;
+    if (!any) return;
+  }
   if constexpr (HOPS && AFS_NZ_INNER) {
     tree_synth_run<PROF, MODEL, HOPS, W, NZ_DYN>(a, lds, prof, noise_variant<W>(a));
   } else if constexpr (HOPS) {

@@ -204,11 +204,16 @@ def vcv_targets(B: int, first_utterance: int = 0, seed: int = BUILD_SEED + 3):
 def build_frames(w: Workload, af_to_frames) -> np.ndarray:
     """Frames[B, F] from a workload; ``af_to_frames(params[N,16]) -> frames[N]``."""
     B, F = w.batch, w.num_frames
-    flat = w.params.reshape(B * F, 16)
-    # static utterances repeat one parameter row: convert unique rows only
-    uniq, inv = np.unique(flat, axis=0, return_inverse=True)
-    fu = af_to_frames(uniq)
-    frames = fu[inv.reshape(-1)].reshape(B, F).copy()
+    if (w.params == w.params[:, :1, :]).all():
+        # static utterances: one parameter row each (the 64k batch: 65536 rows to sort, not 6.6 M)
+        uniq, inv = np.unique(w.params[:, 0, :], axis=0, return_inverse=True)
+        fu = af_to_frames(uniq)
+        frames = np.repeat(fu[inv.reshape(-1)][:, None], F, axis=1)
+    else:
+        # convert unique rows only
+        uniq, inv = np.unique(w.params.reshape(B * F, 16), axis=0, return_inverse=True)
+        fu = af_to_frames(uniq)
+        frames = fu[inv.reshape(-1)].reshape(B, F).copy()
     frames["velum_opening_cm2"] = w.velum
     frames["glottis"] = w.glottis
     return frames

@@ -6,13 +6,13 @@ For N > 1 either run `python bench.py --gpus N` (it starts the N ranks itself: a
 torch.distributed.run, one rank per GPU) or launch it under torch.distributed.run with --gpus
 equal to WORLD_SIZE (anything else is refused).
 
-One *step* = one pass of the hot path over this rank's shard of the BASELINE config-4 batch:
-B static-vowel utterances (default 8192 per GPU; 65536 at 8 GPUs) of S seconds at fs Hz, from
-frames already resident in HBM to fp64 audio in HBM, converted on the GPU to the reference's
-int16 output format and (N > 1) gathered to rank 0 by the library's RCCL gather
-(afs_gather_pcm, xGMI) while the next step synthesizes.  Scaling is weak: per-GPU work is
-fixed.  torch.distributed (gloo) only carries the control plane: the RCCL id, barriers and the
-max-over-ranks time.
+One *step* = one pass of the hot path over this rank's shard of the metric's batch (BASELINE
+config 4: 65536 static-vowel utterances of S seconds at fs Hz, split over the N GPUs -- strong
+scaling: 65536 on one GPU, 8192 per GPU at 8; --batch B instead fixes B per GPU, weak scaling),
+from frames already resident in HBM to fp64 audio in HBM, converted on the GPU to the reference's
+int16 output format and (N > 1) gathered to rank 0 by the library's RCCL gather (afs_gather_pcm,
+xGMI) while the next step synthesizes.  torch.distributed (gloo) only carries the control plane:
+the RCCL id, barriers and the max-over-ranks time.
 
 Printed (rank 0): one JSON line with the BASELINE metric (whole-node samples/s), the roofline
 object of the dominant kernel (HBM, as the north star asks, with the kernel's own launch times
@@ -22,10 +22,9 @@ the CPU baseline (the reference's own sources, oracle/_ref, timed on this host's
 bounded sample, plus the single-core config-1 figure).  On one GPU the line also carries
 "configs": config 5 (8192 fricatives, velum 1.0 cm^2) and config 3 (8192 VCV utterances through
 playTargetSequence), each timed over a few steps with its own launch times, roofline, fp64
-object, reference CPU rate and error against the reference build, and "config4_full": the
-metric's whole 64k-utterance batch in one call on this GPU (one step; its first rows checked bit
-for bit against the shard's, its first utterances against the reference build; --full-batch 0 or
---no-sub-configs skips them).
+object, reference CPU rate and error against the reference build, and "config4_shard": config 4's
+per-GPU shard at 8 GPUs (8192 utterances; the headline of rounds 1-4), its rows checked bit for
+bit against the batch's first rows (--no-sub-configs skips them).
 PMC-derived figures are quoted only when profiles/pmc_*.json hold a pass of this build's kernel
 sources (areafunctionsynthesis_amd.build.kernel_digest).
 """
@@ -159,10 +158,10 @@ def config1_frames(fs: float):
 
 
 WORKLOAD_TEXT = {
-    "static": "BASELINE config 4 shard: {B} static-vowel utterances/GPU x {sec:g} s @ {fs:g} Hz ({B8} at 8 GPUs), "
+    "static": "BASELINE config 4: {G} static-vowel utterances x {sec:g} s @ {fs:g} Hz over {N} GPU(s), {B} per GPU, "
               "frames resident in HBM",
-    "fricatives": "BASELINE config 5: {B} fricative utterances (s f z S Z x C R v) + velum 1.0 cm^2/GPU x {sec:g} s "
-                  "@ {fs:g} Hz, frames resident in HBM",
+    "fricatives": "BASELINE config 5: {B} fricative utterances (s f z S Z x C R v) + velum 1.0 cm^2 per GPU x "
+                  "{sec:g} s @ {fs:g} Hz, frames resident in HBM",
     "vcv": "BASELINE config 3 (fp64 state): {B} VCV utterances/GPU through playTargetSequence ({T} samples @ "
            "{fs:g} Hz, per-sample area-function tubes built on the GPU)",
 }
@@ -393,7 +392,14 @@ def main() -> None:
                          "--gpus N > 1 starts the N ranks itself (torch.distributed.run as a child process)")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=8192, help="utterances per GPU")
+    ap.add_argument("--global-batch", type=int, default=65536,
+                    help="the metric's batch (BASELINE config 4: 65536 utterances), split over the GPUs (strong "
+                         "scaling: 65536 on one GPU, 8192 per GPU at 8)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="utterances per GPU instead (weak scaling; the global batch is then batch x GPUs)")
+    ap.add_argument("--sub-batch", type=int, default=8192,
+                    help="one GPU: utterances of the config-5 / config-3 sub-objects (BASELINE: 8192) and of the "
+                         "config-4 per-GPU shard sub-object")
     ap.add_argument("--seconds", type=float, default=1.0)
     ap.add_argument("--fs", type=float, default=44100.0)
     ap.add_argument("--solver", default=os.environ.get("AFS_SOLVER", "tree"))
@@ -409,9 +415,6 @@ def main() -> None:
                     help="tree solver: force 16 (throughput kernel) or 64 (voice kernel) lanes per utterance; "
                          "default: the library's choice for the batch")
     ap.add_argument("--sub-steps", type=int, default=2)
-    ap.add_argument("--full-batch", type=int, default=65536,
-                    help="one GPU: also time the metric's whole batch (65536 utterances) in one call, one step "
-                         "(0: skip)")
     ap.add_argument("--gather-transport", choices=("rccl", "gloo"), default="rccl",
                     help="N > 1: rccl (the library's afs_gather_pcm; default) or gloo through the host (test only)")
     ap.add_argument("--one-device", action="store_true",
@@ -470,7 +473,15 @@ def main() -> None:
     from areafunctionsynthesis_amd.synthesizer import Comm, Context, comm_unique_id
 
     digest = kernel_digest()
-    B = args.batch
+    if args.batch is None and args.workload != "static":  # (configs 5 and 3: 8192 utterances per GPU)
+        args.batch = args.sub_batch
+    if args.batch is None:  # strong scaling: the metric's batch over the GPUs
+        if args.global_batch % world:
+            print(f"bench.py: --global-batch {args.global_batch} does not split over {world} GPUs", file=sys.stderr)
+            sys.exit(2)
+        B, scaling = args.global_batch // world, "strong"
+    else:
+        B, scaling = args.batch, "weak"
     ctx = Context(args.fs, solver=args.solver, device=local, async_calls=True, profile=True, lanes=args.lanes)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
@@ -486,15 +497,16 @@ def main() -> None:
     subs = []
     if world == 1 and args.workload == "static" and not args.no_sub_configs:
         for wl, label in (("fricatives", "config5"), ("vcv", "config3")):
-            subs.append((label, measure(args, ctx, dev, stream, wl, B, first, world, rank, None, args.sub_steps, 1)))
-    # one GPU: the metric's own 64k-utterance batch in one call (BASELINE config 4 without the sharding)
-    full = None
-    if world == 1 and args.workload == "static" and args.full_batch > 0 and not args.no_sub_configs:
-        full = measure(args, ctx, dev, stream, "static", args.full_batch, 0, 1, 0, None, 1, 1)
-        n = min(B, args.full_batch)
-        # batch independence: the full batch's first utterances are the shard's, bit for bit
-        full.same_as_shard = bool(torch.equal(full.out_dev[:n], m.out_dev[:n])) if first == 0 else None
-        full.same_rows = n
+            subs.append((label, measure(args, ctx, dev, stream, wl, args.sub_batch, 0, world, rank, None,
+                                        args.sub_steps, 1)))
+    # one GPU: config 4's per-GPU shard at 8 GPUs (8192 utterances), the headline of rounds 1-4
+    shard = None
+    if world == 1 and args.workload == "static" and not args.no_sub_configs and args.sub_batch != B:
+        shard = measure(args, ctx, dev, stream, "static", args.sub_batch, 0, 1, 0, None, args.sub_steps, 1)
+        n = min(B, args.sub_batch)
+        # batch independence: the shard's utterances are the batch's first ones, bit for bit
+        shard.same_as_batch = bool(torch.equal(shard.out_dev[:n], m.out_dev[:n]))
+        shard.same_rows = n
 
     if rank == 0:
         d = describe(args, m, world, digest)
@@ -507,12 +519,13 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": d["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": WORKLOAD_TEXT[args.workload].format(B=B, B8=B * 8, sec=args.seconds, fs=args.fs, T=m.T),
+                "workload": WORKLOAD_TEXT[args.workload].format(B=B, G=B * world, N=world, sec=args.seconds,
+                                                                fs=args.fs, T=m.T),
                 "batch_per_gpu": B,
                 "global_batch": B * world,
                 "samples_per_utterance": m.T,
@@ -548,56 +561,43 @@ def main() -> None:
             for label, ms in subs:
                 ds = describe(args, ms, world, digest)
                 o = {
-                    "workload": WORKLOAD_TEXT[ms.workload].format(B=B, B8=B * 8, sec=args.seconds, fs=args.fs, T=ms.T),
+                    "workload": WORKLOAD_TEXT[ms.workload].format(B=ms.B, G=ms.B, N=1, sec=args.seconds, fs=args.fs,
+                                                                  T=ms.T),
+                    "batch": ms.B,
                     "value": ds["value"], "unit": "samples/s", "steps": ms.steps, "warmup": ms.warmup,
                     "ms_per_step": ds["ms_per_step"], "samples_per_utterance": ms.T, "hop": ms.hop,
                     "avg_launch_ms": ds["roofline"]["avg_launch_ms"], "roofline": ds["roofline"], "fp64": ds["fp64"],
                 }
                 if not args.no_cpu_baseline:
-                    cb, max_abs, max_rms = cpu_leg(args, ms, min(args.sub_cpu_utterances, B))
+                    cb, max_abs, max_rms = cpu_leg(args, ms, min(args.sub_cpu_utterances, ms.B))
                     o["cpu_reference_per_core_samples_per_s"] = cb["per_core_samples_per_s"]
                     o["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample",
                                                             "per_core_samples_per_s")}
                     o["max_abs_err_vs_cpu_ref"] = max_abs
                     o["max_rms_err_vs_cpu_ref"] = max_rms
                 result["configs"][label] = o
-        if full is not None:
-            df = describe(args, full, 1, digest)
-            o = {
-                "workload": f"BASELINE config 4's whole batch on one GPU: {full.B} static-vowel utterances x "
-                            f"{args.seconds:g} s @ {args.fs:g} Hz in one afs_synthesize call",
-                "batch": full.B, "value": df["value"], "unit": "samples/s", "steps": full.steps,
-                "warmup": full.warmup, "ms_per_step": df["ms_per_step"],
-                "avg_launch_ms": df["roofline"]["avg_launch_ms"],
-                "launches_per_step": df["roofline"]["launches_per_step"],
-                "lanes_per_utterance": ctx.lanes_per_utterance(full.B),
-                "plan_path": _plan_path(full.B, full.T, full.hop),
-                "ratio_to_shard_value": df["value"] / d["value"],
-                "roofline": df["roofline"], "fp64": df["fp64"],
-                "first_rows_bitwise_equal_to_shard": full.same_as_shard, "rows_compared": full.same_rows,
+        if shard is not None:
+            ds = describe(args, shard, 1, digest)
+            result.setdefault("configs", {})["config4_shard"] = {
+                "workload": f"BASELINE config 4's per-GPU shard at 8 GPUs: {shard.B} static-vowel utterances x "
+                            f"{args.seconds:g} s @ {args.fs:g} Hz on this GPU (the headline of rounds 1-4)",
+                "batch": shard.B, "value": ds["value"], "unit": "samples/s", "steps": shard.steps,
+                "warmup": shard.warmup, "ms_per_step": ds["ms_per_step"],
+                "avg_launch_ms": ds["roofline"]["avg_launch_ms"],
+                "launches_per_step": ds["roofline"]["launches_per_step"],
+                "ratio_to_value": ds["value"] / d["value"],
+                "roofline": ds["roofline"], "fp64": ds["fp64"],
+                "rows_bitwise_equal_to_the_batch": shard.same_as_batch, "rows_compared": shard.same_rows,
+                "why_slower": "8192 utterances fill the GPU's 1024 SIMDs (one wave of 4 utterances each) exactly "
+                              "twice: each SIMD runs two waves back to back, so lighter noise-phase variants "
+                              "(DESIGN.md 2.5) shorten a SIMD's time only when both of its waves are light; at "
+                              "65536 utterances each SIMD runs 16 waves and the light ones balance",
             }
-            if not args.no_cpu_baseline:
-                _, max_abs, max_rms = cpu_leg(args, full, 8)
-                o["max_abs_err_vs_cpu_ref"] = max_abs
-                o["max_rms_err_vs_cpu_ref"] = max_rms
-                o["cpu_ref_utterances"] = 8
-            result.setdefault("configs", {})["config4_full"] = o
         print(json.dumps(result), flush=True)
     if comm is not None:
         comm.close()
     if world > 1:
         dist.destroy_process_group()
-
-
-def _plan_path(B: int, T: int, hop: int) -> str:
-    """Which noise-plan path afs_synthesize takes for this call (afs_capi.cpp run_chunks)."""
-    hops = -(-T // hop)
-    rec = B * hops * 544
-    budget = 4 << 30
-    if hop >= 32 and rec <= budget:
-        return (f"hop mode, one call: {rec / 1e9:.2f} GB of hop records within the 4 GiB plan budget "
-                "(plus the mixed hops' dense records)")
-    return "chunked launches (plans past the 4 GiB budget)"
 
 
 def _launch_ranks(n: int) -> int:
