@@ -177,7 +177,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
                      int64_t hop_stride, int64_t p25_stride) -> afs_status {
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride, plan, plan_stride, lanes,
                       (double *)ws, B, c->host_tab.uni, hops, hop_stride, p25_row0(s0), p25_stride, order,
-                      c->noise_variants ? 1 : 0, grid};
+                      c->call_variants ? 1 : 0, grid};
       hipEvent_t e1 = prof_event(c);
       HIP_TRY(c, afs::launch_tree_synth(a, width, c->stream));
       hipEvent_t e2 = prof_event(c);
@@ -467,7 +467,7 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
   if (const char *e = std::getenv("AFS_PLAN_DENSE")) ctx->plan_dense = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_XCD_ORDER")) ctx->xcd_order = std::atoi(e) != 0;
   if (const char *e = std::getenv("AFS_SHAPE_ORDER")) ctx->shape_order = std::atoi(e) != 0;
-  if (const char *e = std::getenv("AFS_NOISE_VARIANTS")) ctx->noise_variants = std::atoi(e) != 0;
+  if (const char *e = std::getenv("AFS_NOISE_VARIANTS")) ctx->noise_variants = std::atoi(e);
   if (const char *e = std::getenv("AFS_CLASS_ORDER")) ctx->class_order = std::atoi(e);
   if (const char *e = std::getenv("AFS_LAUNCH_SAMPLES")) {  // (A/B and latency studies: samples per K1 launch)
     const long long v = std::atoll(e);
@@ -552,10 +552,11 @@ static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstr
                               const int32_t **dord, int *grid) {
   *dord = nullptr;
   *grid = 0;
+  c->call_variants = c->noise_variants != 0;  // (calls without a slot order: the voice kernel, small batches)
   const int upb = afs::TREE_UPB;
   if (!tree(c) || !c->shape_order || width == afs::TREE_VOICE_W || B <= upb) return AFS_OK;
   const int nb = (B + upb - 1) / upb;
-  const bool by_xcd = c->class_order == 3 && c->noise_variants;
+  const bool by_xcd = c->class_order == 3 && c->noise_variants != 0;
   afs_status s;
   if ((s = ensure(c, &c->keys, &c->keys_bytes, (size_t)B * sizeof(uint64_t))) != AFS_OK) return s;
   uint64_t *dkeys = (uint64_t *)c->keys;
@@ -564,9 +565,26 @@ static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstr
   c->hkeys.resize((size_t)B);
   HIP_TRY(c, hipMemcpyAsync(c->hkeys.data(), dkeys, (size_t)B * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  // The noise-phase variants pay when most waves are light: at 8192 static vowels (61 % light)
+  // +2.3 %, at 8192 fricatives (28 % light) -3 % -- the full-phase waves lose more to the light
+  // ones' copies of the kernel body in their CUs' instruction caches than the light ones gain
+  // (profiles/r05i_fricatives_variants_ab.txt, r05k_variant_rule_ab.txt).  Without them the class
+  // is left out of the sort (the class key alone measured -0.6 %, r05f_variant_order_ab.txt).
+  uint64_t class_mask = 0;
+  if (c->class_order == 1 || c->class_order == 3) class_mask = 3ull << 48;
+  if (c->class_order == 2) class_mask = 3ull << 40;
+  if (class_mask && c->noise_variants == 1) {
+    const int shift = class_mask == (3ull << 48) ? 48 : 40;
+    int64_t light = 0;
+    for (int u = 0; u < B; ++u) light += ((c->hkeys[(size_t)u] >> shift) & 3) != 0;
+    c->call_variants = 2 * light >= (int64_t)B;
+  }
+  const uint64_t sort_mask = c->call_variants ? ~0ull : ~class_mask;
   std::vector<int32_t> idx((size_t)B);
   for (int u = 0; u < B; ++u) idx[(size_t)u] = u;
-  std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) { return c->hkeys[(size_t)a] < c->hkeys[(size_t)b]; });
+  std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) {
+    return (c->hkeys[(size_t)a] & sort_mask) < (c->hkeys[(size_t)b] & sort_mask);
+  });
   int nblocks = nb;
   if (!by_xcd) {
     c->horder.assign((size_t)nb * upb, B);

@@ -46,7 +46,10 @@ struct afs_ctx {
   bool xcd_order = true;               // AFS_XCD_ORDER=0: shared trajectories in utterance order (A/B)
   int64_t launch_cap = 65536;          // samples per K1 launch at most (AFS_LAUNCH_SAMPLES lowers it)
   bool shape_order = true;             // AFS_SHAPE_ORDER=0: afs_synthesize's utterances in call order
-  bool noise_variants = true;          // AFS_NOISE_VARIANTS=0: K1 always runs the full noise phases
+  // AFS_NOISE_VARIANTS: 1 (default) K1's noise-phase variants for the calls whose slot order finds
+  // at least half of the utterances in a light class (shape_order), 2 for every call, 0 never
+  int noise_variants = 1;
+  bool call_variants = true;           // this call's choice (shape_order; run_chunks passes it to K1)
   int class_order = 2;                 // AFS_CLASS_ORDER: the slot order's noise-class key (af_kernels.hip; A/B)
   void *keys = nullptr;                // shape keys (device)
   size_t keys_bytes = 0;

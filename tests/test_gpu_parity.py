@@ -245,7 +245,8 @@ def test_noise_variants_are_bitwise(oracle, solver, monkeypatch):
     equal those of the full phases (AFS_NOISE_VARIANTS=0) bit for bit -- static vowels (most waves
     in a light variant), fricatives with their tongue and lip sources, frame-rate VCV trajectories
     (constrictions forming within a launch), and launches of 1000 samples (a dipole's amplitude
-    decaying across a launch boundary keeps its slot in the heavier variant)."""
+    decaying across a launch boundary keeps its slot in the heavier variant).  (AFS_NOISE_VARIANTS=2
+    forces the variants; by default a call uses them when most of its batch is light.)"""
     from areafunctionsynthesis_amd.synthesizer import Context
     from areafunctionsynthesis_amd.workloads import build_frames, fricatives, static_vowels, vcv
     cases = [("static", static_vowels(48, seconds=0.25)), ("fricatives", fricatives(40, seconds=0.25, velum_cm2=1.0)),
@@ -253,7 +254,7 @@ def test_noise_variants_are_bitwise(oracle, solver, monkeypatch):
     for label, w in cases:
         for launch in (None, "1000"):
             ys, draws = [], []
-            for env in ("0", "1"):
+            for env in ("0", "2"):  # (2: the variants for every call, whatever the batch's mix)
                 monkeypatch.setenv("AFS_NOISE_VARIANTS", env)
                 if launch is None:
                     monkeypatch.delenv("AFS_LAUNCH_SAMPLES", raising=False)
