@@ -67,6 +67,10 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--samples", type=int, default=44100)
     ap.add_argument("--hop", type=int, default=441)
+    ap.add_argument("--plan-fetch-factor", type=float, default=2.0,
+                    help="read bytes per FETCH_SIZE byte of K5's kernels (tools/microbench/fetch_calib rec1072)")
+    ap.add_argument("--plan-calibration", default="profiles/r05m_fetch_calib.txt",
+                    help="where --plan-fetch-factor was measured")
     a = ap.parse_args()
     a.dir = a.dir or os.path.join(ROOT, "gpurun_out", a.tag)
     fetch = per_launch(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"), a.kernel)
@@ -90,7 +94,19 @@ def main() -> None:
                       "KiB -> bytes",
     }
     if plan_f or plan_w:  # K5 (all its kernels), the noise-source plan producer of the same launches
-        entry["plan_kernel_traffic_bytes_per_launch"] = (2.0 * kib * plan_f + kib * plan_w) / len(fetch)
+        launches = len(fetch)
+        frames = a.batch * (a.samples // a.hop + 1) * 1072.0 / launches  # each frame once
+        records = a.batch * (-(-a.samples // a.hop)) * 544.0 / launches    # each hop record once
+        entry["plan_kernel_fetch_size_kib_per_launch"] = plan_f / launches
+        entry["plan_kernel_read_bytes_per_launch"] = a.plan_fetch_factor * kib * plan_f / launches
+        entry["plan_kernel_write_bytes_per_launch"] = kib * plan_w / launches
+        entry["plan_kernel_traffic_bytes_per_launch"] = (a.plan_fetch_factor * kib * plan_f + kib * plan_w) / launches
+        entry["plan_kernel_algorithmic_bytes_per_launch"] = frames + records
+        entry["plan_kernel_traffic_ratio"] = entry["plan_kernel_traffic_bytes_per_launch"] / (frames + records)
+        entry["plan_kernel_correction"] = (f"read = {a.plan_fetch_factor:g} x FETCH_SIZE, calibrated for K5's read "
+                                           f"pattern (each lane walking its own 1072-B frame: fetch_calib rec1072, "
+                                           f"{a.plan_calibration}); write = WRITE_SIZE; algorithmic = every frame "
+                                           "read once + every hop record written once")
     import sys
     sys.path.insert(0, ROOT)
     from areafunctionsynthesis_amd.build import kernel_digest
