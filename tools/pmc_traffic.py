@@ -68,7 +68,8 @@ def main() -> None:
     ap.add_argument("--samples", type=int, default=44100)
     ap.add_argument("--hop", type=int, default=441)
     ap.add_argument("--plan-fetch-factor", type=float, default=2.0,
-                    help="read bytes per FETCH_SIZE byte of K5's kernels (tools/microbench/fetch_calib rec1072)")
+                    help="read bytes per FETCH_SIZE byte of K5's kernels: 2 since K5 copies its block's frames "
+                         "to LDS with coalesced loads (fetch_calib b128 / b64_row16)")
     ap.add_argument("--plan-calibration", default="profiles/r05m_fetch_calib.txt",
                     help="where --plan-fetch-factor was measured")
     a = ap.parse_args()
@@ -103,10 +104,14 @@ def main() -> None:
         entry["plan_kernel_traffic_bytes_per_launch"] = (a.plan_fetch_factor * kib * plan_f + kib * plan_w) / launches
         entry["plan_kernel_algorithmic_bytes_per_launch"] = frames + records
         entry["plan_kernel_traffic_ratio"] = entry["plan_kernel_traffic_bytes_per_launch"] / (frames + records)
-        entry["plan_kernel_correction"] = (f"read = {a.plan_fetch_factor:g} x FETCH_SIZE, calibrated for K5's read "
-                                           f"pattern (each lane walking its own 1072-B frame: fetch_calib rec1072, "
-                                           f"{a.plan_calibration}); write = WRITE_SIZE; algorithmic = every frame "
-                                           "read once + every hop record written once")
+        entry["plan_kernel_traffic_ratio"] = entry["plan_kernel_traffic_bytes_per_launch"] / (frames + records)
+        entry["plan_kernel_correction"] = (f"read = {a.plan_fetch_factor:g} x FETCH_SIZE: K5 copies each block's "
+                                           "frames to LDS with coalesced loads, the pattern fetch_calib calibrates "
+                                           "at 2 (b128, b64_row16); the per-lane walk over 1072-B frames that K5 "
+                                           "used before (rec1072) reports 7.5x a coalesced read's FETCH_SIZE for "
+                                           f"the same bytes, i.e. it re-fetched lines ({a.plan_calibration}); "
+                                           "write = WRITE_SIZE; algorithmic = every frame read once + every hop "
+                                           "record written once")
     import sys
     sys.path.insert(0, ROOT)
     from areafunctionsynthesis_amd.build import kernel_digest
