@@ -565,11 +565,13 @@ static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstr
   c->hkeys.resize((size_t)B);
   HIP_TRY(c, hipMemcpyAsync(c->hkeys.data(), dkeys, (size_t)B * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  // The noise-phase variants pay when most waves are light: at 8192 static vowels (61 % light)
-  // +2.3 %, at 8192 fricatives (28 % light) -3 % -- the full-phase waves lose more to the light
-  // ones' copies of the kernel body in their CUs' instruction caches than the light ones gain
-  // (profiles/r05i_fricatives_variants_ab.txt, r05k_variant_rule_ab.txt).  Without them the class
-  // is left out of the sort (the class key alone measured -0.6 %, r05f_variant_order_ab.txt).
+  // The noise-phase variants pay when most waves are light, or when every SIMD runs many waves: at
+  // 8192 static vowels (61 % light, two waves per SIMD) +2.3 %, at 8192 fricatives (28 % light)
+  // -3 % -- the full-phase waves lose more to the light ones' copies of the kernel body in their
+  // CUs' instruction caches than the light ones gain -- but at 65536 fricatives (16 waves per SIMD,
+  // the classes in long runs of the slot order) +0.7 %, at 32768 (8 per SIMD) +0.05 %
+  // (profiles/r05i_fricatives_variants_ab.txt, r05k_variant_rule_ab.txt, r05r_variant_rule_ab.txt).  Without them the class is left out of the sort (the class key alone
+  // measured -0.6 %, r05f_variant_order_ab.txt).
   uint64_t class_mask = 0;
   if (c->class_order == 1 || c->class_order == 3) class_mask = 3ull << 48;
   if (c->class_order == 2) class_mask = 3ull << 40;
@@ -577,7 +579,8 @@ static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstr
     const int shift = class_mask == (3ull << 48) ? 48 : 40;
     int64_t light = 0;
     for (int u = 0; u < B; ++u) light += ((c->hkeys[(size_t)u] >> shift) & 3) != 0;
-    c->call_variants = 2 * light >= (int64_t)B;
+    const int64_t waves_per_simd = (int64_t)B / ((int64_t)(64 / afs::TREE_W) * std::max(1, c->simds));
+    c->call_variants = 2 * light >= (int64_t)B || waves_per_simd >= 16;
   }
   const uint64_t sort_mask = c->call_variants ? ~0ull : ~class_mask;
   std::vector<int32_t> idx((size_t)B);

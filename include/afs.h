@@ -174,7 +174,7 @@ int32_t afs_abi_version(void);
  *   AFS_NOISE_VARIANTS=0    the synthesis kernel always runs its full noise phases instead of the
  *                           lightest variant each launch's noise-source plans allow (same audio);
  *                           =2 the variants for every call (default: for calls whose batch is mostly
- *                           light: DESIGN.md 2.5)
+ *                           light or holds >= 16 waves per SIMD: DESIGN.md 2.5)
  *   AFS_PLAN_OVERLAP=1      chunked path: K5 of the next launch beside K1 of this one */
 afs_status afs_create(afs_ctx **ctx, const afs_config *cfg);
 void afs_destroy(afs_ctx *ctx);
