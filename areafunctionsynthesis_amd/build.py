@@ -105,11 +105,16 @@ def kernel_digest(source: str = "tds_tree.hip") -> str:
     includes, its compiler flags): the committed PMC summaries (profiles/pmc_*.json) are keyed
     by it, so bench.py quotes a counter figure only for the kernel it is timing."""
     import hashlib
+    import re
     h = hashlib.sha1()
     for f in [source] + KERNEL_HEADERS.get(source, HEADERS):
         h.update(f.encode())
-        with open(os.path.join(CSRC, f), "rb") as fh:
-            h.update(fh.read())
+        with open(os.path.join(CSRC, f), encoding="utf-8") as fh:
+            text = fh.read()
+        # (comments and blank space do not change the object: documentation edits keep the key)
+        text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+        text = re.sub(r"//[^\n]*", " ", text)
+        h.update(" ".join(text.split()).encode())
     h.update(repr((COMMON, PER_SOURCE.get(source, []))).encode())
     return h.hexdigest()[:12]
 

@@ -111,6 +111,10 @@ typedef struct afs_options {
   double flow_separation_area_ratio; /* 1.0 */
 } afs_options;
 
+/* Calls return once their work is queued on the context's stream, except where a call must read
+ * something back to order or size its launches (large tree batches: the slot order's shape keys,
+ * the length of K5's noise-plan work list); such a read-back waits for all work queued before it
+ * on the stream, the previous call's synthesis included. */
 #define AFS_ASYNC 0x1u
 /* Record an event pair around every kernel launch of the synthesis calls; afs_kernel_times
  * returns their summed durations (measurement only: a few microseconds per launch). */
