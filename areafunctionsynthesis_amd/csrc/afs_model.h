@@ -12,6 +12,7 @@
 // the kernels in one read-only `Tables` block.
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 
 #include "../../include/afs.h"
@@ -139,19 +140,28 @@ struct alignas(8) Topo {
 enum : uint16_t { SR_BIF = 1, SR_JUNCTION = 2, SR_RADIATION = 4 };
 // (The x_* fields are LDS byte offsets into the utterance block: the kernel adds them to the
 // block's address with one instruction, sub-dword operand select included.)
+// Fields grouped by the phase that reads them, each group at an offset aligned to its load width:
+// the compiler merges adjacent 16-bit fields into one wide LDS read, and a read that is not
+// aligned to its width stalls the LDS (SQ_LDS_UNALIGNED_STALL; the previous order had the row
+// phase's offsets in a 12-byte read at byte 30 of the record).
 struct alignas(16) SecRec {
-  double c_la, c_ra, c_ea;
-  uint16_t x_la, x_ra, x_ea, x_da, x_ub, x_urb, x_sx, x_e0, x_e1, x_e2;
-  uint16_t x_o0, x_o1, x_ur, x_un, x_p4;
+  uint16_t x_la, x_da, x_ub, x_urb, x_sx, x_e0, x_e1, x_e2;  // row phase (bytes 0-15)
+  double c_la, c_ra, c_ea;                                    // row phase (16-39)
   uint16_t flags;
   // constriction phase: the noise-smoothed flows of the section's outputs (X_UN, or zero)
   uint16_t x_uo0, x_uo1;
+  uint16_t x_ra;                                              // (unused by the kernel)
+  uint16_t x_o0, x_o1, x_ur, x_un, x_p4;                      // update phase (48-57)
+  uint16_t x_ea, pad0[2];                                     // (x_ea unused by the kernel)
   // radiation sections (SR_RADIATION): flow, d/dt and noise-smoothed flow of the two
-  // radiation currents (X_U + rc, X_U + lc, X_UR.., X_UR.., X_UN.., X_UN..)
+  // radiation currents (X_U + rc, X_U + lc, X_UR.., X_UR.., X_UN.., X_UN..) (64-75)
   uint16_t x_rad[6];
+  uint16_t pad1[2];
   // (80-byte stride: the 16 sections a 16-lane ds_read_b128 group reads start on 16 distinct
   // 16-byte bank slots; at 64 bytes, sections s and s+4 share banks: 4-way conflicts)
 };
+static_assert(offsetof(SecRec, c_la) == 16 && offsetof(SecRec, x_o0) == 48 && offsetof(SecRec, x_rad) == 64,
+              "SecRec: the phases' field groups at aligned offsets");
 static_assert(sizeof(SecRec) == 80, "SecRec: 80-byte stride");
 // Scalars of the time loop (copies of Tables fields; see build_tables).
 struct Hot {
