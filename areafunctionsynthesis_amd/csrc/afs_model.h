@@ -103,9 +103,11 @@ struct alignas(16) ArmRec {
   uint16_t ej;                // last lane of an arm: edge boundary - junction node
   uint8_t start;              // first real position (ARM_P: none)
   uint8_t idx, flags, pad0;   // position in the arm (0 = far end), ARM_IN / ARM_END
-  uint16_t pad[3];
+  uint16_t pad[11];
+  // (112-byte stride, 7 x 16: the 16 lanes of an utterance read records 0-15, which then start on
+  // 16 distinct 16-byte bank slots; at 96 bytes lanes k and k + 8 shared them, 2-way conflicts)
 };
-static_assert(sizeof(ArmRec) == 96, "ArmRec: 96 bytes");
+static_assert(sizeof(ArmRec) == 112, "ArmRec: 112 bytes");
 // the junction triangle: pivots of 40, 41, 65, edges 40-41, 40-65, 41-65, X_U of 40, 41, 65
 struct alignas(8) ArmJunction {
   uint16_t d[3], e[3], u[3], pad;
