@@ -269,6 +269,135 @@ bool arm_records(Tables *t) {
   return ok;
 }
 
+// LDS slots of the edges (X_OFF), chosen for the LDS banks.  The kernel reads and writes the edges
+// through its records, 16 lanes of an utterance per instruction: the row phase the edges of the
+// sections of one slot, the arm solver those of one position of every lane's segment.  Two
+// utterances share a 32-lane bank group (their blocks X_STRIDE = 16 mod 32 doubles apart), so the
+// lanes of one instruction are conflict-free when their edges' slots differ modulo 16 doubles
+// (MI355X_MICROARCH.md §LDS).  Numbered in graph order, lanes k and k + 5 of an arm position met
+// on one bank (tools/lds_banks.cpp); here every edge gets a residue modulo 16 that minimises the
+// clashes within the access groups (greedy, then single moves and swaps until none helps), and
+// the residue classes are laid out over the slots.  The edges' values are the same; only where
+// they sit changes.
+void bank_edge_slots(Consts &c) {
+  using namespace tree;
+  constexpr int R = 16;
+  auto id_of = [](uint16_t v) -> int {  // the zero and sink edges keep their slots TREE_NE, TREE_NE + 1
+    const int slot = (int)(v / 8) - X_OFF;
+    return (slot >= 0 && slot < TREE_NE + 2) ? slot : -1;
+  };
+  std::vector<std::vector<int>> groups;
+  auto add = [&](const std::vector<int> &g) {
+    std::vector<int> u;
+    for (int e : g)
+      if (e >= 0 && std::find(u.begin(), u.end(), e) == u.end()) u.push_back(e);
+    if (u.size() > 1) groups.push_back(u);
+  };
+  constexpr int W = 16;
+  for (int j = 0; j < Shape<W>::NSL; ++j) {
+    std::vector<int> g0, g1, g2;
+    for (int gl = 0; gl < W; ++gl) {
+      const int s0 = slot_section<W>(j, gl);
+      const SecRec &q = c.sec[s0 < 0 ? NS : s0];
+      g0.push_back(id_of(q.x_e0));
+      g1.push_back(id_of(q.x_e1));
+      g2.push_back(id_of(q.x_e2));
+    }
+    add(g0), add(g1), add(g2);
+  }
+  for (int p = 0; p + 1 < ARM_P; ++p) {
+    std::vector<int> g;
+    for (int k = 0; k < TREE_CHAINS; ++k) g.push_back(id_of(c.arm[k].e[p]));
+    add(g);
+  }
+  {
+    std::vector<int> ga, gj, gx;
+    for (int k = 0; k < TREE_CHAINS; ++k) {
+      ga.push_back(id_of(c.arm[k].ea));
+      gj.push_back(id_of(c.arm[k].ej));
+      gx.push_back(id_of(c.arm[k].fx0));
+      gx.push_back(id_of(c.arm[k].fx1));
+    }
+    add(ga), add(gj), add(gx);
+  }
+  for (int f = 0; f < ARM_FOLDS; ++f) {
+    std::vector<int> g0, g1;
+    for (int k = 0; k < TREE_CHAINS; ++k) {
+      g0.push_back(id_of(c.arm[k].le0[f]));
+      g1.push_back(id_of(c.arm[k].le1[f]));
+    }
+    add(g0), add(g1);
+  }
+  int cap[R] = {};
+  for (int sl = 0; sl < TREE_NE; ++sl) cap[(X_OFF + sl) % R]++;
+  std::vector<int> res(TREE_NE + 2, -1), used(R, 0);
+  res[TREE_NE] = (X_OFF + TREE_NE) % R;  // (fixed)
+  res[TREE_NE + 1] = (X_OFF + TREE_NE + 1) % R;
+  std::vector<std::vector<int>> of(TREE_NE + 2);  // groups of an edge
+  for (int gi = 0; gi < (int)groups.size(); ++gi)
+    for (int e : groups[gi]) of[e].push_back(gi);
+  auto clash = [&](int e, int r) {  // edges of e's groups on residue r
+    int n = 0;
+    for (int gi : of[e])
+      for (int f : groups[gi]) n += f != e && res[f] == r;
+    return n;
+  };
+  // greedy, the edges in most groups first
+  std::vector<int> order(TREE_NE);
+  for (int e = 0; e < TREE_NE; ++e) order[e] = e;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return of[a].size() > of[b].size(); });
+  for (int e : order) {
+    int best = -1, bc = 1 << 30;
+    for (int r = 0; r < R; ++r)
+      if (used[r] < cap[r]) {
+        const int cc = clash(e, r);
+        if (cc < bc) bc = cc, best = r;
+      }
+    res[e] = best;
+    used[best]++;
+  }
+  for (bool better = true; better;) {
+    better = false;
+    for (int e = 0; e < TREE_NE; ++e) {
+      const int r0 = res[e], c0 = clash(e, r0);
+      if (c0 == 0) continue;
+      for (int r = 0; r < R && !better; ++r) {
+        if (r == r0) continue;
+        if (used[r] < cap[r]) {  // move
+          if (clash(e, r) < c0) {
+            res[e] = r, used[r]++, used[r0]--, better = true;
+          }
+          continue;
+        }
+        for (int f = 0; f < TREE_NE && !better; ++f) {  // swap with an edge on r
+          if (res[f] != r) continue;
+          const int before = c0 + clash(f, r);
+          res[e] = r, res[f] = r0;
+          if (clash(e, r) + clash(f, r0) < before) better = true;
+          else res[e] = r0, res[f] = r;
+        }
+      }
+    }
+  }
+  // residue classes over the slots, in edge order within a class
+  std::vector<int> slot(TREE_NE, -1), next(R, 0);
+  std::vector<std::vector<int>> slots_of(R);
+  for (int sl = 0; sl < TREE_NE; ++sl) slots_of[(X_OFF + sl) % R].push_back(sl);
+  for (int e = 0; e < TREE_NE; ++e) slot[e] = slots_of[res[e]][next[res[e]]++];
+  auto remap = [&](uint16_t &v) {
+    const int e = id_of(v);
+    if (e >= 0 && e < TREE_NE) v = (uint16_t)((X_OFF + slot[e]) * 8);
+  };
+  for (int s = 0; s <= NS; ++s) remap(c.sec[s].x_e0), remap(c.sec[s].x_e1), remap(c.sec[s].x_e2);
+  for (int k = 0; k < TREE_CHAINS; ++k) {
+    ArmRec &r = c.arm[k];
+    for (int p = 0; p + 1 < ARM_P; ++p) remap(r.e[p]);
+    remap(r.ea), remap(r.ej), remap(r.fx0), remap(r.fx1);
+    for (int f = 0; f < ARM_FOLDS; ++f) remap(r.le0[f]), remap(r.le1[f]);
+  }
+  for (int q = 0; q < 3; ++q) remap(c.armj.e[q]);
+}
+
 }  // namespace
 
 // IirFilter::createChebyshev, IirFilter.cpp:286-432 (0.5 % ripple).
@@ -490,6 +619,7 @@ void build_tables(Tables *t, double fs_hz, const afs_options &opt) {
       *f = (uint16_t)(*f * 8);
     for (int k = 0; k < 6; ++k) q.x_rad[k] = (uint16_t)(q.x_rad[k] * 8);
   }
+  bank_edge_slots(c);
   for (int k = 0; k < NSTATIC; ++k) {
     int s = k < 23 ? k : k + 46;
     c.stat[k][ST_E] = t->E[s];
