@@ -48,6 +48,14 @@ using std::fma;
 #define AFS_LDS_DRAIN() ((void)0)
 #endif
 
+// AFS_RNG_AHEAD = 2: rng_ahead keeps at least two blocks (60 values) of the rand() stream
+// pending, in a 128-entry prefix-sum ring, so that a sample with up to five active dipoles (the
+// usual four: the glottis source and a tongue constriction, two each) draws without generating
+// on the noise phase's chain; 1: one block ahead in a 64-entry ring (rounds 2-5).
+#ifndef AFS_RNG_AHEAD
+#define AFS_RNG_AHEAD 2
+#endif
+
 namespace afs {
 namespace tree {
 
@@ -90,8 +98,8 @@ enum : int {
   X_PREVFLOW = X_OUTF + 16,
   X_NONFIN = X_PREVFLOW + 1,
   X_NDRAW = X_NONFIN + 1,      // rand() calls so far (u64; diagnostics: afs_rng_draws)
-  X_RNG = X_NDRAW + 1,         // rand(): value ring, prefix-sum ring (64 u32 each), head, pending (65 doubles)
-  X_GP = X_RNG + 65,           // interpolated glottis controls (6), 2 spare
+  X_RNG = X_NDRAW + 1,         // rand(): value ring (64 u32), prefix-sum ring (128 / 64 u32)
+  X_GP = X_RNG + (AFS_RNG_AHEAD >= 2 ? 96 : 64),  // interpolated glottis controls (6), 2 spare
   X_RNG_SINK = X_GP + 6,       //   (spare: the sink of rng_ahead's idle stores, outside the solver arrays)
   X_TGLOT = X_GP + 8,          // transglottal-pressure filter x1..x4, y1..y4 (variable entrance loss)
   X_TVEL = X_TGLOT + 8,        // transvelar coupling filters H1, H2: x1..x4, y1..y4 each
@@ -298,7 +306,8 @@ struct Lane {
   double sample;                                                     // lane 0
   uint64_t planw;                                                    // word gl of this sample's plan (tree_plan.h)
   uint32_t racc[S::NDP];                                             // rand() sums of owned dipoles
-  uint32_t rtmp[3];                                                  // rand() block scratch
+  uint32_t rtmp[8];                                                  // rand() block scratch
+  int32_t rhead, rpend;                                              // rand() ring head, values pending (rng_ring_seed)
   ArmCarry ac;                                                       // arm solver, during the solve
   // per-sample values of the geometry/network block (not state: cleared before a save)
   double acur[S::ND], lcur[S::ND];                                   // area, length of the slots
@@ -518,11 +527,16 @@ AFS_HD inline void rng_seed(int32_t *r, uint32_t seed) {
 
 // The rand() stream as a sequence r_i = r_{i-3} + r_{i-31} (mod 2^32), output r_i >> 1 --
 // glibc's TYPE_3 generator read in generation order.  The LDS block holds the last 64
-// values (RNG_R, index = sequence number mod 64), the inclusive prefix sums of the outputs
-// S_i = sum_{i' <= i} (r_i' >> 1) (RNG_S, same indexing; sums of draws are differences of
-// two of them), RNG_HEAD = ring index of the next value to generate and RNG_PEND = how many
-// generated values have not been drawn yet (< two blocks: rng_ahead).
-constexpr int RNG_RING = 64, RNG_R = 0, RNG_S = 64, RNG_HEAD = 128, RNG_PEND = 129;
+// values (RNG_R, index = sequence number mod 64: the generator's 31-value history and a
+// block), the inclusive prefix sums of the outputs S_i = sum_{i' <= i} (r_i' >> 1) (RNG_S,
+// index = sequence number mod RNG_SRING; sums of draws are differences of two of them),
+// and in the lane registers (Lane::rhead, Lane::rpend, the same on every lane of the utterance:
+// no LDS round trip before the noise phase's addresses) the sequence number mod RNG_SRING of the
+// next value to generate and how many generated values have not been drawn yet (rng_ahead).
+// (AFS_RNG_AHEAD: see the top of this file)
+constexpr int RNG_RING = 64, RNG_SRING = AFS_RNG_AHEAD >= 2 ? 128 : 64;
+constexpr int RNG_R = 0, RNG_S = RNG_RING;
+static_assert((RNG_S + RNG_SRING) / 2 == X_GP - X_RNG, "the rand() region of the LDS block");
 // values per generation block: 3 residue chains x min(W, 10) lanes (<= 30 keeps every
 // term of the block in the 31-value history)
 template <int W> constexpr int rng_lanes() { return W < 10 ? W : 10; }
@@ -532,10 +546,9 @@ AFS_HD inline void rng_ring_seed(uint32_t *g, uint32_t seed) {
   int32_t st[32];
   rng_seed(st, seed);
   const int f = st[31];  // glibc's fptr: the oldest value of the window
-  for (int j = 0; j < RNG_S + RNG_RING; ++j) g[j] = 0;
+  for (int j = 0; j < RNG_S + RNG_SRING; ++j) g[j] = 0;
   for (int j = 0; j < 31; ++j) g[RNG_R + j] = (uint32_t)st[(f + j) % 31];
-  ((int32_t *)g)[RNG_HEAD] = 31;  // S[30] = 0 is the base of the prefix sums
-  ((int32_t *)g)[RNG_PEND] = 0;
+  // (the head, 31 -- S[30] = 0 is the base of the prefix sums -- and the pending count 0: reset_lane)
 }
 
 // ---------------------------------------------------------------------------
@@ -561,6 +574,8 @@ AFS_HD inline void reset_lane(int gl, Lane<W> &R) {
   R.sample = 0.0;
 #pragma unroll
   for (int k = 0; k < S::NDP; ++k) R.racc[k] = 0u;
+  R.rhead = 31;
+  R.rpend = 0;
 }
 
 AFS_HD inline void reset_lds(double *X, uint32_t seed) {
@@ -1136,7 +1151,7 @@ template <int W, class Xc>
 AFS_HD inline void rng_block(Xc &x, uint32_t *g, uint32_t *sink, int head, bool gen) {
   constexpr int RJ = rng_lanes<W>();
   const uint32_t b0 = g[RNG_R + ((head - 3) & (RNG_RING - 1))], b1 = g[RNG_R + ((head - 2) & (RNG_RING - 1))],
-                 b2 = g[RNG_R + ((head - 1) & (RNG_RING - 1))], sb = g[RNG_S + ((head - 1) & (RNG_RING - 1))];
+                 b2 = g[RNG_R + ((head - 1) & (RNG_RING - 1))], sb = g[RNG_S + ((head - 1) & (RNG_SRING - 1))];
   x.template scan_add<3>(
       [&](int gl, Lane<W> &R) {
         (void)R;
@@ -1163,9 +1178,9 @@ AFS_HD inline void rng_block(Xc &x, uint32_t *g, uint32_t *sink, int head, bool 
       [&](int gl, Lane<W> &R, const U4 &p) {
         const bool on = gen && gl < RJ;
         const uint32_t s2 = sb + p.v[0], s1 = s2 - R.rtmp[2], s0 = s1 - R.rtmp[1];
-        *(on ? &g[RNG_S + ((head + 3 * gl) & (RNG_RING - 1))] : sink) = s0;
-        *(on ? &g[RNG_S + ((head + 3 * gl + 1) & (RNG_RING - 1))] : sink) = s1;
-        *(on ? &g[RNG_S + ((head + 3 * gl + 2) & (RNG_RING - 1))] : sink) = s2;
+        *(on ? &g[RNG_S + ((head + 3 * gl) & (RNG_SRING - 1))] : sink) = s0;
+        *(on ? &g[RNG_S + ((head + 3 * gl + 1) & (RNG_SRING - 1))] : sink) = s1;
+        *(on ? &g[RNG_S + ((head + 3 * gl + 2) & (RNG_SRING - 1))] : sink) = s2;
       });
 }
 
@@ -1194,7 +1209,7 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
     return;
   }
   uint32_t *g = (uint32_t *)(X + X_RNG);
-  const int head0 = ((const int32_t *)g)[RNG_HEAD], pend = ((const int32_t *)g)[RNG_PEND];
+  const int head0 = x.first().rhead, pend = x.first().rpend;
   const int base = head0 - pend;  // ring index of this sample's first draw
   const int need = 12 * __builtin_popcountll(act);
   // draws [lo, hi) of this sample are generated: add their share to the owners' sums
@@ -1207,8 +1222,8 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
         const bool on = d < NDIP && ((act >> d) & 1);
         const int q0 = 12 * __builtin_popcountll(act & ((1ull << d) - 1));
         const int a = q0 > lo ? q0 : lo, b = q0 + 12 < hi ? q0 + 12 : hi;
-        const uint32_t sb = g[RNG_S + ((base + b - 1) & (RNG_RING - 1))];
-        const uint32_t sa = g[RNG_S + ((base + a - 1) & (RNG_RING - 1))];
+        const uint32_t sb = g[RNG_S + ((base + b - 1) & (RNG_SRING - 1))];
+        const uint32_t sa = g[RNG_S + ((base + a - 1) & (RNG_SRING - 1))];
         R.racc[k] += (on && a < b) ? sb - sa : 0u;
       }
     });
@@ -1222,7 +1237,7 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
     x.sync();
     consume(avail, avail + RNG_BLOCK);
     avail += RNG_BLOCK;
-    head = (head + RNG_BLOCK) & (RNG_RING - 1);
+    head = (head + RNG_BLOCK) & (RNG_SRING - 1);
   }
   x.sync();
   x.mark(PH_N_RNG);
@@ -1231,9 +1246,8 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
   const uint64_t ndraw = *(const uint64_t *)(X + X_NDRAW) + (uint64_t)need;
   x.par([&](int gl, Lane<W> &R) {
     (void)gl; (void)R;
-    int32_t *c = (int32_t *)g;
-    c[RNG_HEAD] = head;
-    c[RNG_PEND] = avail - need;
+    R.rhead = head;
+    R.rpend = avail - need;
     *(uint64_t *)(X + X_NDRAW) = ndraw;  // (every lane stores the same count)
   });
   x.par([&](int gl, Lane<W> &R) {
@@ -1256,26 +1270,109 @@ AFS_HD inline void phase_noise(Xc &x, double *X, const Uni &U, const Consts &C) 
   });
 }
 
-// The rand() stream generated ahead of its use: one block whenever fewer than RNG_BLOCK values
-// are pending, so that the noise phase of the next sample (one or two active sources: 12 or
-// 24 draws) finds its draws generated.  It depends on the ring alone, not on the acoustic
-// state, so it runs in the update block after the solver, beside the update's own chains
-// instead of on the noise phase's.  The block overwrites ring entries head - 64 .. head - 35: with fewer than 30
-// values pending, none of them (nor the prefix sum before the oldest) is still needed.  Draws
-// are counted when consumed (phase_noise), so the rand() call count is the reference's.
+// Two blocks of the stream (2 RNG_BLOCK values at head) in one pass (gen == false: evaluated,
+// stored into the sink).  The second block's history terms r_{i-31} are the first block's values,
+// taken from the lanes' registers instead of a store, a wave fence and a load: its chains c = 1,
+// 2 sum lane j's values c = 0, 1 of the first block, its chain c = 0 lane j-1's value 2 (lane 0:
+// r_{head-1}), and its bases r_{i-3} are the first block's last lane (RJ - 1).  Every history
+// load precedes the stores, which overwrite values head - 64 .. head - 5 (the second block's
+// history, head - 1 .. head + 28, is in registers) and prefix sums head - RNG_SRING ..
+// head - RNG_SRING + 2 RNG_BLOCK - 1.
+template <int W, class Xc>
+AFS_HD inline void rng_block2(Xc &x, uint32_t *g, uint32_t *sink, int head, bool gen) {
+  constexpr int RJ = rng_lanes<W>(), RB = 3 * RJ;
+  static_assert(RJ == 10, "ten lanes per block (the 31-value lag)");
+  const uint32_t b0 = g[RNG_R + ((head - 3) & (RNG_RING - 1))], b1 = g[RNG_R + ((head - 2) & (RNG_RING - 1))],
+                 b2 = g[RNG_R + ((head - 1) & (RNG_RING - 1))], sb = g[RNG_S + ((head - 1) & (RNG_SRING - 1))];
+  // block 1: r_{head+3j+c} = r_{head+c-3} + sum_{t<=j} r_{head+3t+c-31}
+  x.template scan_add<3>(
+      [&](int gl, Lane<W> &R) {
+        (void)R;
+        U4 v{{0u, 0u, 0u, 0u}};
+        for (int c = 0; c < 3; ++c) v.v[c] = g[RNG_R + ((head + 3 * gl + c - 31) & (RNG_RING - 1))];
+        return v;
+      },
+      [&](int, Lane<W> &R, const U4 &p) {
+        R.rtmp[0] = b0 + p.v[0];
+        R.rtmp[1] = b1 + p.v[1];
+        R.rtmp[2] = b2 + p.v[2];
+      });
+  // block 2: r_{head+RB+3j+c} = r_{head+RB+c-3} + sum_{t<=j} r_{head+3t+c-1}
+  x.template pull_u<-1, 1>([&](int, Lane<W> &R) { return U4{{R.rtmp[2], 0u, 0u, 0u}}; },
+                           [&](int gl, Lane<W> &R, const U4 &v) { R.rtmp[3] = gl == 0 ? b2 : v.v[0]; });
+  x.template scan_add<3>([&](int, Lane<W> &R) { return U4{{R.rtmp[3], R.rtmp[0], R.rtmp[1], 0u}}; },
+                         [&](int, Lane<W> &R, const U4 &p) {
+                           R.rtmp[3] = p.v[0];
+                           R.rtmp[4] = p.v[1];
+                           R.rtmp[5] = p.v[2];
+                         });
+  x.template bcast_u<RJ - 1, 3>([&](int, Lane<W> &R) { return U4{{R.rtmp[0], R.rtmp[1], R.rtmp[2], 0u}}; },
+                                [&](int, Lane<W> &R, const U4 &v) {
+                                  R.rtmp[3] += v.v[0];
+                                  R.rtmp[4] += v.v[1];
+                                  R.rtmp[5] += v.v[2];
+                                });
+  // prefix sums of the outputs r >> 1 in sequence order: both blocks' lane sums scanned together,
+  // the second block based on the first's last sum (lane RJ - 1)
+  x.template scan_add<2>(
+      [&](int, Lane<W> &R) {
+        return U4{{(R.rtmp[0] >> 1) + (R.rtmp[1] >> 1) + (R.rtmp[2] >> 1),
+                   (R.rtmp[3] >> 1) + (R.rtmp[4] >> 1) + (R.rtmp[5] >> 1), 0u, 0u}};
+      },
+      [&](int, Lane<W> &R, const U4 &p) {
+        R.rtmp[6] = p.v[0];
+        R.rtmp[7] = p.v[1];
+      });
+  x.template bcast_u<RJ - 1, 1>(
+      [&](int, Lane<W> &R) { return U4{{R.rtmp[6], 0u, 0u, 0u}}; },
+      [&](int gl, Lane<W> &R, const U4 &v) {
+        const bool on = gen && gl < RJ;  // the others store into the sink
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int h = head + q * RB + 3 * gl;
+          const uint32_t n0 = R.rtmp[3 * q], n1 = R.rtmp[3 * q + 1], n2 = R.rtmp[3 * q + 2];
+          const uint32_t s2 = sb + (q ? v.v[0] + R.rtmp[7] : R.rtmp[6]), s1 = s2 - (n2 >> 1), s0 = s1 - (n1 >> 1);
+          *(on ? &g[RNG_R + (h & (RNG_RING - 1))] : sink) = n0;
+          *(on ? &g[RNG_R + ((h + 1) & (RNG_RING - 1))] : sink) = n1;
+          *(on ? &g[RNG_R + ((h + 2) & (RNG_RING - 1))] : sink) = n2;
+          *(on ? &g[RNG_S + (h & (RNG_SRING - 1))] : sink) = s0;
+          *(on ? &g[RNG_S + ((h + 1) & (RNG_SRING - 1))] : sink) = s1;
+          *(on ? &g[RNG_S + ((h + 2) & (RNG_SRING - 1))] : sink) = s2;
+        }
+      });
+}
+
+// The rand() stream generated ahead of its use, so that the noise phase of the next sample
+// finds its draws generated: AFS_RNG_AHEAD = 2: two blocks (rng_block2) whenever fewer than two
+// blocks are pending (up to five active sources, 60 draws; the usual four -- the glottis source
+// and a tongue constriction, two dipoles each -- draw 48); 1: one block whenever fewer than one
+// is pending (one or two active sources).  A sample that needs more generates further blocks in
+// the noise phase.  It depends on the ring alone, not on the acoustic state, so it runs in the
+// update block after the solver, beside the update's own chains instead of on the noise
+// phase's.  With fewer than AFS_RNG_AHEAD blocks pending, the values and prefix sums a
+// generation overwrites (rng_block, rng_block2) are no longer needed: neither the pending ones,
+// the prefix sum before the oldest of them, nor the generator's 31-value history.  Draws are
+// counted when consumed (phase_noise), so the rand() call count is the reference's.
+#ifndef AFS_RNG_SKIP
+#define AFS_RNG_SKIP 0  // 1: a wave none of whose utterances needs the blocks skips them (a uniform branch: slower)
+#endif
 template <int W, class Xc>
 AFS_HD inline void rng_ahead(Xc &x, double *X) {
   constexpr int RNG_BLOCK = 3 * rng_lanes<W>();
-  static_assert(2 * RNG_BLOCK <= RNG_RING, "pending values (< RNG_BLOCK), the prefix sum before them and a block fit");
+  constexpr int GEN = AFS_RNG_AHEAD >= 2 ? 2 * RNG_BLOCK : RNG_BLOCK;  // values per generation
+  static_assert(GEN <= RNG_SRING - GEN, "pending values (< GEN), the prefix sum before them and a generation fit the ring");
+  static_assert(GEN <= RNG_RING, "a generation fits the value ring");
   uint32_t *g = (uint32_t *)(X + X_RNG);
-  int32_t *c = (int32_t *)g;
-  const int head = c[RNG_HEAD], pend = c[RNG_PEND];
-  const bool gen = pend < RNG_BLOCK;
-  rng_block<W>(x, g, (uint32_t *)(X + X_RNG_SINK), head, gen);
+  const int head = x.first().rhead, pend = x.first().rpend;
+  const bool gen = pend < GEN;
+  if (!AFS_RNG_SKIP || x.wave_any(gen)) {
+    if constexpr (AFS_RNG_AHEAD >= 2) rng_block2<W>(x, g, (uint32_t *)(X + X_RNG_SINK), head, gen);
+    else rng_block<W>(x, g, (uint32_t *)(X + X_RNG_SINK), head, gen);
+  }
   x.par([&](int gl, Lane<W> &R) {
-    (void)gl; (void)R;
-    c[RNG_HEAD] = gen ? ((head + RNG_BLOCK) & (RNG_RING - 1)) : head;
-    c[RNG_PEND] = gen ? pend + RNG_BLOCK : pend;
+    (void)gl;
+    R.rhead = gen ? ((head + GEN) & (RNG_SRING - 1)) : head;
+    R.rpend = gen ? pend + GEN : pend;
   });
 }
 

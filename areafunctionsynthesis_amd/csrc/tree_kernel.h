@@ -52,6 +52,8 @@ struct GpuExec {
   uint64_t last = 0;
   uint64_t acc[PROF ? PH_COUNT : 1] = {};
   template <class F> __device__ __forceinline__ void par(F f) { f(gl, *R); }
+  // the lane's registers, for values that are the same on every lane of the utterance
+  __device__ __forceinline__ const Lane<W> &first() const { return *R; }
   template <class F> __device__ __forceinline__ void one(F f) { if (gl == 0) f(*R); }
   // Per-lane work and lane-uniform work in one block: every lane also evaluates the uniform
   // part (same inputs, same values, same stores), so the two interleave without a branch.
@@ -146,6 +148,25 @@ struct GpuExec {
     for (int i = 0; i < N; ++i) o.v[i] = shift<K>(v.v[i]);
     g(gl, *R, o);
   }
+  // 32-bit forms of pull (lane gl+K's value inside the 16-lane row, zero fill) and of a broadcast
+  // of lane K of the row (row_newbcast K), for the rand() stream's double block (rng_block2)
+  template <int K, int N, class F, class G> __device__ __forceinline__ void pull_u(F f, G g) {
+    static_assert(K != 0 && K > -16 && K < 16, "row shift");
+    constexpr int CTRL = K > 0 ? 0x100 + K : 0x110 - K;
+    U4 v = f(gl, *R);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v.v[i] = (uint32_t)AFS_DPP((int)v.v[i], CTRL, 0xF, 0xF, true);
+    g(gl, *R, v);
+  }
+  template <int K, int N, class F, class G> __device__ __forceinline__ void bcast_u(F f, G g) {
+    static_assert(K >= 0 && K < 16, "lane of the row");
+    U4 v = f(gl, *R);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v.v[i] = (uint32_t)AFS_DPP((int)v.v[i], 0x150 + K, 0xF, 0xF, false);
+    g(gl, *R, v);
+  }
+  // whether p holds on any lane of the wave (every utterance of it)
+  __device__ __forceinline__ static bool wave_any(bool p) { return __ballot(p) != 0; }
   // The lane half (0: lanes 0-7, 1: lanes 8-15 of the utterance) and lane gl ^ 8's value
   // (row_ror 8 inside the 16-lane row), for glottis_eval_split.
   __device__ __forceinline__ int half8() const { return (gl >> 3) & 1; }

@@ -22,6 +22,7 @@ struct CpuExec {
   Lane<W> *R;
   template <class F> void par(F f) { for (int gl = 0; gl < W; ++gl) f(gl, R[gl]); }
   template <class F> void one(F f) { f(R[0]); }
+  const Lane<W> &first() const { return R[0]; }
   template <class F, class G> void par_uniform(F f, G g) { par(f); g(R[0]); }
   template <class F> void lanes(int n, F f) { for (int k = 0; k < n; ++k) f(k, R[k]); }
   void dyn_neighbors() {
@@ -68,6 +69,27 @@ struct CpuExec {
       g(gl, R[gl], o);
     }
   }
+  template <int K, int N, class F, class G> void pull_u(F f, G g) {
+    std::vector<U4> v(W);
+    for (int gl = 0; gl < W; ++gl) v[gl] = f(gl, R[gl]);
+    for (int gl = 0; gl < W; ++gl) {
+      const int src = gl + K;
+      U4 o{{0u, 0u, 0u, 0u}};
+      if (src >= 0 && src < W && src / 16 == gl / 16)
+        for (int i = 0; i < N; ++i) o.v[i] = v[src].v[i];
+      g(gl, R[gl], o);
+    }
+  }
+  template <int K, int N, class F, class G> void bcast_u(F f, G g) {
+    std::vector<U4> v(W);
+    for (int gl = 0; gl < W; ++gl) v[gl] = f(gl, R[gl]);
+    for (int gl = 0; gl < W; ++gl) {
+      U4 o{{0u, 0u, 0u, 0u}};
+      for (int i = 0; i < N; ++i) o.v[i] = v[gl / 16 * 16 + K].v[i];
+      g(gl, R[gl], o);
+    }
+  }
+  static bool wave_any(bool p) { return p; }  // (one utterance: its lanes agree)
   template <class F> double max_value(F f) {
     double b = f(0, R[0]);
     for (int gl = 1; gl < W; ++gl) b = max_combine(b, f(gl, R[gl]));
