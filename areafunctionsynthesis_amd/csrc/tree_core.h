@@ -23,6 +23,7 @@
 #pragma once
 
 #include <cstdint>
+#include <type_traits>
 
 #if !defined(__HIPCC__)
 #include <cmath>
@@ -54,6 +55,11 @@ using std::fma;
 // on the noise phase's chain; 1: one block ahead in a 64-entry ring (rounds 2-5).
 #ifndef AFS_RNG_AHEAD
 #define AFS_RNG_AHEAD 2
+#endif
+// AFS_ARM_SCAN = 1: the arm solver's lane-to-lane reduction and back substitution as prefix
+// scans (solve_arms); 0: one DPP step per lane of the longest arm (rounds 2-5)
+#ifndef AFS_ARM_SCAN
+#define AFS_ARM_SCAN 1
 #endif
 
 namespace afs {
@@ -150,6 +156,7 @@ struct ArmCarry {
   double e28, e29;    // fossa lane: edges 84-28, 84-29
   double xJ;          // last lanes: the solution of their junction node (then the anchor's)
   double jd[3], jy[3], je[3], xj[3];  // junction lane: triangle pivots, rhs, edges, solutions
+  double sm[4];       // AFS_ARM_SCAN: the lane's segment of the pivot recurrence (2x2), then of the rhs / solution
   int sf, sb, end;    // the arm steps this lane reduces in (forward) / solves in (back), -1: none
   bool neg;           // a pivot this lane met was negative (the system is not positive definite)
 };
@@ -1675,6 +1682,68 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
       },
       [&](int, Lane<W> &R, const D4 &v) { R.ac.Db -= v.v[0]; R.ac.Yb -= v.v[1]; R.ac.F -= v.v[2]; });
   x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.neg = R.ac.neg | (R.ac.Db < 0.0); });
+#if AFS_ARM_SCAN
+  // Arm reduction toward the junction as prefix scans over the lanes (three DPP steps each
+  // instead of ARM_MAXLEN - 1 dependent ones).  The boundary pivots follow d_k = D_k - F_k^2 /
+  // d_{k-1} (F_k: the lane's edge to the previous lane's boundary, 0 at an arm's first lane),
+  // i.e. (n_k, m_k) = M_k (n_{k-1}, m_{k-1}), M_k = [[D_k, -F_k^2], [1, 0]], d_k = n_k / m_k: the
+  // lanes scan the products of their M (an arm's first lane makes the ratio independent of the
+  // lanes before it); then the rhs y'_k = Yb_k - F_k y'_{k-1} / d_{k-1}, an affine recurrence.
+  static_assert(ARM_MAXLEN <= 8, "three doubling steps cover an arm");
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
+    const double Fe = R.ac.sf >= 1 ? R.ac.F : 0.0;
+    R.ac.sm[0] = R.ac.Db;
+    R.ac.sm[1] = -(Fe * Fe);
+    R.ac.sm[2] = 1.0;
+    R.ac.sm[3] = 0.0;
+  });
+  // S_k <- S_k S_{k-s} (lanes before the row: the identity)
+  auto mob = [&](auto sh, bool full) {
+    constexpr int S_ = decltype(sh)::value;
+    x.template pull<-S_, 4>([&](int, Lane<W> &R) { return D4{{R.ac.sm[0], R.ac.sm[1], R.ac.sm[2], R.ac.sm[3]}}; },
+                            [&](int k, Lane<W> &R, const D4 &t) {
+                              const bool in = (k & 15) >= S_;
+                              const double t00 = in ? t.v[0] : 1.0, t01 = t.v[1], t10 = t.v[2], t11 = in ? t.v[3] : 1.0;
+                              const double *m = R.ac.sm;
+                              const double n00 = fma(m[0], t00, m[1] * t10), n10 = fma(m[2], t00, m[3] * t10);
+                              if (full) {
+                                const double n01 = fma(m[0], t01, m[1] * t11), n11 = fma(m[2], t01, m[3] * t11);
+                                R.ac.sm[1] = n01;
+                                R.ac.sm[3] = n11;
+                              }
+                              R.ac.sm[0] = n00;
+                              R.ac.sm[2] = n10;
+                            });
+  };
+  mob(std::integral_constant<int, 1>{}, true);
+  mob(std::integral_constant<int, 2>{}, true);
+  mob(std::integral_constant<int, 4>{}, false);
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
+    R.ac.inv = R.ac.sm[2] * pivot_recip(R.ac.sm[0]);  // 1 / d_k = m_k / n_k
+    R.ac.neg = R.ac.neg | (R.ac.inv < 0.0);
+  });
+  x.template pull<-1, 1>([&](int, Lane<W> &R) { return D4{{R.ac.inv, 0.0, 0.0, 0.0}}; },
+                         [&](int, Lane<W> &R, const D4 &v) {
+                           R.ac.sm[0] = (R.ac.sf >= 1 ? -R.ac.F : 0.0) * v.v[0];
+                           R.ac.sm[1] = R.ac.Yb;
+                         });
+  // (A, B)_k <- (A_k A_{k-s}, A_k B_{k-s} + B_k): lanes before the row read zeros, which start a chain
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    auto aff = [&](auto sh) {
+      constexpr int S_ = decltype(sh)::value;
+      x.template pull<-S_, 2>([&](int, Lane<W> &R) { return D4{{R.ac.sm[0], R.ac.sm[1], 0.0, 0.0}}; },
+                              [&](int, Lane<W> &R, const D4 &t) {
+                                R.ac.sm[1] = fma(R.ac.sm[0], t.v[1], R.ac.sm[1]);
+                                R.ac.sm[0] = R.ac.sm[0] * t.v[0];
+                              });
+    };
+    if (q == 0) aff(std::integral_constant<int, 1>{});
+    if (q == 1) aff(std::integral_constant<int, 2>{});
+    if (q == 2) aff(std::integral_constant<int, 4>{});
+  }
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.Yb = R.ac.sm[1]; });
+#else
   // arm reduction toward the junction: in step s the lanes at position s of their arm
   // eliminate the previous boundary (lane k-1) from their own
   // (a lane off its step updates with a zero edge: no change, the same reciprocal again)
@@ -1691,6 +1760,7 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
                            });
   }
   x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.neg = R.ac.neg | (R.ac.Db < 0.0); });
+#endif
   // the junction lane takes the three arms' last boundaries (pivot inverse, rhs, edge) and
   // solves the triangle: eliminate 65, then 41; solve 40 (uniform code on every lane)
   auto give = [&](int, Lane<W> &R) { return D4{{R.ac.inv, R.ac.Yb, R.ac.ej, 0.0}}; };
@@ -1737,6 +1807,31 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
   // back along the arms
   x.template pull<1, 1>([&](int, Lane<W> &R) { return D4{{R.ac.F, 0.0, 0.0, 0.0}}; },
                         [&](int, Lane<W> &R, const D4 &v) { R.ac.Fn = v.v[0]; });
+#if AFS_ARM_SCAN
+  // x_k = (Yb_k - Fn_k x_{k+1}) / d_k along an arm, x = (Yb - ej xJ) / d at its last lane: an
+  // affine recurrence toward the arms' far ends, scanned (lanes past the row read zeros: the arms'
+  // last lanes, the fossa and the junction lane have no successor term)
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
+    const bool mid = R.ac.sb >= 0;
+    R.ac.sm[0] = mid ? -R.ac.Fn * R.ac.inv : 0.0;
+    R.ac.sm[1] = mid ? R.ac.Yb * R.ac.inv : (R.ac.end ? fma(-R.ac.ej, R.ac.xJ, R.ac.Yb) * R.ac.inv : 0.0);
+  });
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    auto aff = [&](auto sh) {
+      constexpr int S_ = decltype(sh)::value;
+      x.template pull<S_, 2>([&](int, Lane<W> &R) { return D4{{R.ac.sm[0], R.ac.sm[1], 0.0, 0.0}}; },
+                             [&](int, Lane<W> &R, const D4 &t) {
+                               R.ac.sm[1] = fma(R.ac.sm[0], t.v[1], R.ac.sm[1]);
+                               R.ac.sm[0] = R.ac.sm[0] * t.v[0];
+                             });
+    };
+    if (q == 0) aff(std::integral_constant<int, 1>{});
+    if (q == 1) aff(std::integral_constant<int, 2>{});
+    if (q == 2) aff(std::integral_constant<int, 4>{});
+  }
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.x = R.ac.sm[1]; });
+#else
   x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
     R.ac.x = R.ac.end ? fma(-R.ac.ej, R.ac.xJ, R.ac.Yb) * R.ac.inv : 0.0;
   });
@@ -1748,6 +1843,7 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
                             R.ac.x = on ? fma(-R.ac.Fn, v.v[0], R.ac.Yb) * R.ac.inv : R.ac.x;
                           });
   }
+#endif
   // the fossa lane: 84 from 28 and 29
   x.template pull<ARM_L28 - ARM_FOSSA, 1>([&](int, Lane<W> &R) { return D4{{R.ac.x, 0.0, 0.0, 0.0}}; },
                                           [&](int, Lane<W> &R, const D4 &v) { R.ac.Fn = v.v[0]; });
