@@ -61,6 +61,14 @@ using std::fma;
 #ifndef AFS_ARM_SCAN
 #define AFS_ARM_SCAN 1
 #endif
+// AFS_JUNCTION_ADJ = 1: the junction triangle solved by its adjugate (solve_arms)
+#ifndef AFS_JUNCTION_ADJ
+#define AFS_JUNCTION_ADJ 1
+#endif
+// AFS_BACK_SCALED = 1: a lane's back substitution with its x-independent terms scaled ahead (arm_back)
+#ifndef AFS_BACK_SCALED
+#define AFS_BACK_SCALED 1
+#endif
 
 namespace afs {
 namespace tree {
@@ -1630,10 +1638,23 @@ AFS_HD inline void arm_back(const ArmRec &rr, const ArmJunction &J, bool junctio
   }
   double xs[ARM_P];
   xs[ARM_P - 1] = a.x;
+#if AFS_BACK_SCALED
+  // x_p = (y_p - F_p xA - E_p x_{p+1}) / d_p with the terms that do not depend on x_{p+1} scaled
+  // ahead: one fma per position on the chain instead of three dependent operations
+  double c[ARM_P - 1], e[ARM_P - 1];
+#pragma unroll
+  for (int p = 0; p < ARM_P - 1; ++p) {
+    c[p] = fma(-Fp[p], xA, y[p]) * inv[p];
+    e[p] = -Ep[p] * inv[p];
+  }
+#pragma unroll
+  for (int p = ARM_P - 2; p >= 0; --p) xs[p] = fma(e[p], xs[p + 1], c[p]);
+#else
 #pragma unroll
   for (int p = ARM_P - 2; p >= 0; --p) {
     xs[p] = fma(-Fp[p], xA, fma(-Ep[p], xs[p + 1], y[p])) * inv[p];
   }
+#endif
 #pragma unroll
   for (int p = 0; p < ARM_P; ++p) xat(X, r.u[p]) = xs[p];
 #pragma unroll
@@ -1662,13 +1683,15 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
     }
     R.ac.xJ = 0.0;
   });
+  // (the fossa lane's pivot reciprocal for its fold below: its boundary takes no anchor update --
+  // the junction lane sends zeros -- so it is taken before the anchors' updates, off their chain)
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.inv = pivot_recip(R.ac.Db); });
   // the anchors' updates: lane k's anchor is lane k-1's boundary (a first lane of an arm, the
   // fossa and the junction lane send zeros)
   x.template pull<1, 2>([&](int, Lane<W> &R) { return D4{{R.ac.dA, R.ac.yA, 0.0, 0.0}}; },
                         [&](int, Lane<W> &R, const D4 &v) { R.ac.Db += v.v[0]; R.ac.Yb += v.v[1]; });
   // the fossa lane folds 84 into 28 (lane ARM_L28) and 29 (lane ARM_L28 + 1); every other
   // lane's fossa edges are zero, so it sends zeros
-  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) { R.ac.inv = pivot_recip(R.ac.Db); });
   x.template pull<ARM_FOSSA - ARM_L28, 2>(
       [&](int, Lane<W> &R) {
         const double c0 = R.ac.e28 * R.ac.inv;
@@ -1774,6 +1797,25 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
   x.template pull<ARM_END_A - ARM_JUNCTION, 3>(give, take(0));
   x.template pull<ARM_END_B - ARM_JUNCTION, 3>(give, take(1));
   x.template pull<ARM_END_C - ARM_JUNCTION, 3>(give, take(2));
+#if AFS_JUNCTION_ADJ
+  // the triangle's 3 x 3 SPD system by its adjugate: cofactors, determinant and the three
+  // numerators side by side, one reciprocal (9 dependent operations instead of ~16 of the
+  // elimination); not positive definite (the elimination's negative pivot) <=> d2, its 2 x 2
+  // minor or the determinant negative
+  x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
+    const double *d = R.ac.jd, *y = R.ac.jy;
+    const double e01 = R.ac.je[0], e02 = R.ac.je[1], e12 = R.ac.je[2];
+    const double c00 = fma(d[1], d[2], -(e12 * e12)), c01 = fma(e02, e12, -(e01 * d[2]));
+    const double c02 = fma(e01, e12, -(e02 * d[1])), c11 = fma(d[0], d[2], -(e02 * e02));
+    const double c12 = fma(e01, e02, -(d[0] * e12)), c22 = fma(d[0], d[1], -(e01 * e01));
+    const double det = fma(d[0], c00, fma(e01, c01, e02 * c02));
+    const bool dneg = (d[2] < 0.0) | (c00 < 0.0) | (det < 0.0);
+    const double r = dneg ? NAN : pivot_recip(det);
+    R.ac.xj[0] = fma(c00, y[0], fma(c01, y[1], c02 * y[2])) * r;
+    R.ac.xj[1] = fma(c01, y[0], fma(c11, y[1], c12 * y[2])) * r;
+    R.ac.xj[2] = fma(c02, y[0], fma(c12, y[1], c22 * y[2])) * r;
+  });
+#else
   x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
     double *d = R.ac.jd, *y = R.ac.jy;
     double e01 = R.ac.je[0];
@@ -1796,6 +1838,7 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
     R.ac.xj[1] = x1;
     R.ac.xj[2] = fma(-e12, x1, fma(-e02, x0, y[2])) * i2;
   });
+#endif
   x.template pull<ARM_JUNCTION - ARM_END_A, 1>([&](int, Lane<W> &R) { return D4{{R.ac.xj[0], 0.0, 0.0, 0.0}}; },
                                                [&](int k, Lane<W> &R, const D4 &v) { if (k == ARM_END_A) R.ac.xJ = v.v[0]; });
   x.template pull<ARM_JUNCTION - ARM_END_B, 1>([&](int, Lane<W> &R) { return D4{{R.ac.xj[1], 0.0, 0.0, 0.0}}; },
