@@ -61,6 +61,11 @@ using std::fma;
 #ifndef AFS_ARM_SCAN
 #define AFS_ARM_SCAN 1
 #endif
+// AFS_WALK_PRESCALED = 1: the arm walk stores Y / d, F / d, E / d for the back substitution
+// (arm_back, which needs AFS_BACK_SCALED) instead of 1 / d, Y, F, E
+#ifndef AFS_WALK_PRESCALED
+#define AFS_WALK_PRESCALED 0
+#endif
 // AFS_JUNCTION_ADJ = 1: the junction triangle solved by its adjugate (solve_arms)
 #ifndef AFS_JUNCTION_ADJ
 #define AFS_JUNCTION_ADJ 1
@@ -1598,10 +1603,18 @@ AFS_HD inline void arm_walk(const ArmRec &rr, double *X, ArmCarry &a) {
     yA = fma(-g, Y[p], yA);
     D[p + 1] = fma(-e2, inv, D[p + 1]);
     Y[p + 1] = fma(-h, Y[p], Y[p + 1]);
+#if AFS_WALK_PRESCALED
+    // the back substitution's factors, scaled by the pivot's reciprocal here (g and h are needed
+    // anyway): x_p = Y_p / d_p - (F_p / d_p) xA - (E_p / d_p) x_{p+1} (arm_back)
+    xat(X, r.d[p] + RHS_DELTA) = Y[p] * inv;
+    xat(X, r.u[p]) = g;
+    xat(X, r.e[p]) = h;
+#else
     xat(X, r.d[p]) = inv;                // factors for the back substitution
     xat(X, r.d[p] + RHS_DELTA) = Y[p];
     xat(X, r.u[p]) = F;
     xat(X, r.e[p]) = E[p];
+#endif
     F = -(g * E[p]);                     // fill edge anchor - p+1
   }
 #pragma unroll
@@ -1624,7 +1637,7 @@ AFS_HD inline void arm_back(const ArmRec &rr, const ArmJunction &J, bool junctio
   double il[ARM_FOLDS], yl[ARM_FOLDS], l0[ARM_FOLDS], l1[ARM_FOLDS];
 #pragma unroll
   for (int p = 0; p < ARM_P - 1; ++p) {
-    inv[p] = xat(X, r.d[p]);
+    inv[p] = AFS_WALK_PRESCALED ? 1.0 : xat(X, r.d[p]);  // (prescaled: Y / d, F / d, E / d)
     y[p] = xat(X, r.d[p] + RHS_DELTA);
     Fp[p] = xat(X, r.u[p]);
     Ep[p] = xat(X, r.e[p]);
@@ -1644,8 +1657,13 @@ AFS_HD inline void arm_back(const ArmRec &rr, const ArmJunction &J, bool junctio
   double c[ARM_P - 1], e[ARM_P - 1];
 #pragma unroll
   for (int p = 0; p < ARM_P - 1; ++p) {
-    c[p] = fma(-Fp[p], xA, y[p]) * inv[p];
-    e[p] = -Ep[p] * inv[p];
+    if constexpr (AFS_WALK_PRESCALED) {
+      c[p] = fma(-Fp[p], xA, y[p]);
+      e[p] = -Ep[p];
+    } else {
+      c[p] = fma(-Fp[p], xA, y[p]) * inv[p];
+      e[p] = -Ep[p] * inv[p];
+    }
   }
 #pragma unroll
   for (int p = ARM_P - 2; p >= 0; --p) xs[p] = fma(e[p], xs[p + 1], c[p]);
