@@ -64,7 +64,7 @@ using std::fma;
 // AFS_WALK_PRESCALED = 1: the arm walk stores Y / d, F / d, E / d for the back substitution
 // (arm_back, which needs AFS_BACK_SCALED) instead of 1 / d, Y, F, E
 #ifndef AFS_WALK_PRESCALED
-#define AFS_WALK_PRESCALED 0
+#define AFS_WALK_PRESCALED 1
 #endif
 // AFS_JUNCTION_ADJ = 1: the junction triangle solved by its adjugate (solve_arms)
 #ifndef AFS_JUNCTION_ADJ
