@@ -160,6 +160,8 @@ def config1_frames(fs: float):
 WORKLOAD_TEXT = {
     "static": "BASELINE config 4: {G} static-vowel utterances x {sec:g} s @ {fs:g} Hz over {N} GPU(s), {B} per GPU, "
               "frames resident in HBM",
+    "config2": "BASELINE config 2: {B} static-vowel utterances x {sec:g} s @ {fs:g} Hz on one GPU (one utterance per "
+               "SIMD: the voice kernel's per-sample latency), frames resident in HBM",
     "fricatives": "BASELINE config 5: {B} fricative utterances (s f z S Z x C R v) + velum 1.0 cm^2 per GPU x "
                   "{sec:g} s @ {fs:g} Hz, frames resident in HBM",
     "vcv": "BASELINE config 3 (fp64 state): {B} VCV utterances/GPU through playTargetSequence ({T} samples @ "
@@ -370,7 +372,7 @@ def describe(args, m: Measured, world: int, digest: str) -> dict:
     if tr and tr.get("plan_kernel_traffic_bytes_per_launch") is not None:
         roof["plan_kernel_traffic_bytes_per_launch"] = tr["plan_kernel_traffic_bytes_per_launch"]
     return {"value": value, "ms_per_step": m.elapsed / m.steps * 1e3, "roofline": roof, "fp64": fp64,
-            "step_device_ms": float(np.mean(m.synth_ms))}
+            "step_device_ms": float(np.mean(m.synth_ms)), "sq": sq}
 
 
 def cpu_leg(args, m: Measured, n: int):
@@ -415,6 +417,8 @@ def main() -> None:
                     help="tree solver: force 16 (throughput kernel) or 64 (voice kernel) lanes per utterance; "
                          "default: the library's choice for the batch")
     ap.add_argument("--sub-steps", type=int, default=2)
+    ap.add_argument("--config2-batch", type=int, default=1024,
+                    help="one GPU: utterances of the config-2 sub-object (BASELINE config 2: 1024 static vowels)")
     ap.add_argument("--gather-transport", choices=("rccl", "gloo"), default="rccl",
                     help="N > 1: rccl (the library's afs_gather_pcm; default) or gloo through the host (test only)")
     ap.add_argument("--one-device", action="store_true",
@@ -496,6 +500,9 @@ def main() -> None:
     # one GPU: config 5 and config 3 are timed too (sub-objects, a few steps each)
     subs = []
     if world == 1 and args.workload == "static" and not args.no_sub_configs:
+        # config 2 (1024 static vowels: one utterance per SIMD, the voice kernel's per-sample latency)
+        subs.append(("config2", measure(args, ctx, dev, stream, "static", args.config2_batch, 0, world, rank, None,
+                                        args.sub_steps, 1)))
         for wl, label in (("fricatives", "config5"), ("vcv", "config3")):
             subs.append((label, measure(args, ctx, dev, stream, wl, args.sub_batch, 0, world, rank, None,
                                         args.sub_steps, 1)))
@@ -560,14 +567,23 @@ def main() -> None:
             result["configs"] = {}
             for label, ms in subs:
                 ds = describe(args, ms, world, digest)
+                text = WORKLOAD_TEXT["config2" if label == "config2" else ms.workload]
                 o = {
-                    "workload": WORKLOAD_TEXT[ms.workload].format(B=ms.B, G=ms.B, N=1, sec=args.seconds, fs=args.fs,
-                                                                  T=ms.T),
+                    "workload": text.format(B=ms.B, G=ms.B, N=1, sec=args.seconds, fs=args.fs, T=ms.T),
                     "batch": ms.B,
                     "value": ds["value"], "unit": "samples/s", "steps": ms.steps, "warmup": ms.warmup,
                     "ms_per_step": ds["ms_per_step"], "samples_per_utterance": ms.T, "hop": ms.hop,
+                    "lanes_per_utterance": ctx.lanes_per_utterance(ms.B),
                     "avg_launch_ms": ds["roofline"]["avg_launch_ms"], "roofline": ds["roofline"], "fp64": ds["fp64"],
                 }
+                if ds.get("sq"):
+                    o["cycles_per_wave_sample"] = ds["sq"]["wave_cycles_per_wave_sample"]
+                    o["utterances_per_wave"] = ds["sq"].get("utterances_per_wave", 4)
+                    o["cycles_source"] = ds["fp64"]["executed_source"] if ds["fp64"] else None
+                if label == "config2":
+                    # the voice kernel's per-sample latency: one utterance per wave, one wave per SIMD
+                    o["us_per_sample_per_utterance"] = ds["roofline"]["avg_launch_ms"] * 1e3 / (
+                        ms.T / max(1.0, ds["roofline"]["launches_per_step"]))
                 if not args.no_cpu_baseline:
                     cb, max_abs, max_rms = cpu_leg(args, ms, min(args.sub_cpu_utterances, ms.B))
                     o["cpu_reference_per_core_samples_per_s"] = cb["per_core_samples_per_s"]

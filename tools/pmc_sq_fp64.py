@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--samples", type=int, default=44100)
     ap.add_argument("--hop", type=int, default=441)
+    ap.add_argument("--upw", type=int, default=4, help="utterances per wave (4: the 16-lane kernel, 1: the voice kernel)")
     a = ap.parse_args()
     d = a.dir or os.path.join(ROOT, "gpurun_out", a.tag)
     tot = {}
@@ -53,17 +54,18 @@ def main():
             tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     utt_samples = float(a.batch) * a.samples  # one step: every launch of the step summed
     waves = tot["SQ_WAVES"]
-    wave_samples = utt_samples / 4.0          # 4 utterances per wave
+    wave_samples = utt_samples / a.upw        # a.upw utterances per wave
     entry = {
         "tag": a.tag,
-        "lane_flops_per_sample": tot["SQ_INSTS_VALU_FLOPS_FP64"] / wave_samples * 64.0 / 4.0,
+        "lane_flops_per_sample": tot["SQ_INSTS_VALU_FLOPS_FP64"] / wave_samples * 64.0 / a.upw,
+        "utterances_per_wave": a.upw,
         "waves_per_launch_sum": waves,
         "valu_insts_per_wave_sample": tot["SQ_INSTS_VALU"] / wave_samples,
         "wave_cycles_per_wave_sample": 4.0 * tot["SQ_WAVE_CYCLES"] / wave_samples,
         "wait_any_cycles_per_wave_sample": 4.0 * tot["SQ_WAIT_ANY"] / wave_samples,
         "active_valu_cycles_per_wave_sample": 4.0 * tot["SQ_ACTIVE_INST_VALU"] / wave_samples,
         "note": "SQ_WAVE_CYCLES / SQ_WAIT_ANY / SQ_ACTIVE_INST_VALU count quad-cycles (x 4); per wave-sample = "
-                "per wave and audio sample (a wave holds 4 utterances)",
+                "per wave and audio sample (a wave holds utterances_per_wave utterances)",
     }
     import sys
     sys.path.insert(0, ROOT)
