@@ -7,6 +7,7 @@
 #include <cfloat>
 
 #include <hip/hip_runtime.h>
+#include <hipcub/device/device_radix_sort.hpp>
 
 #include "afs_af.h"
 #include "afs_model.h"
@@ -181,7 +182,45 @@ __global__ void utterance_key_kernel(const afs_frame *frames, int64_t fstride, i
                 : (cls << 48) | ((uint64_t)bucket << 40) | ((uint64_t)imin << 32) | (uint64_t)__float_as_uint(af);
 }
 
+// The slot order's rule on the device (afs_capi.cpp shape_order, one block): whether the call runs
+// the noise-phase variants -- mode 2 always, 0 never, 1 when at least half the utterances have a light
+// noise class (the class field at bit `shift` non-zero) or every SIMD runs many waves -- into
+// *variants; without them the class field is masked out of the keys (it then plays no part in the
+// order); idx[u] = u; the padding slots order[B .. slots) = B.
+__global__ void __launch_bounds__(1024) order_rule_kernel(uint64_t *keys, int B, int shift, int mode, int many_waves,
+                                                          int32_t *variants, int32_t *idx, int32_t *order, int slots) {
+  __shared__ int light;
+  if (threadIdx.x == 0) light = 0;
+  __syncthreads();
+  if (mode == 1 && shift >= 0) {
+    int n = 0;
+    for (int u = threadIdx.x; u < B; u += blockDim.x) n += ((keys[u] >> shift) & 3) != 0;
+    atomicAdd(&light, n);
+  }
+  __syncthreads();
+  const bool on = mode == 2 || (mode == 1 && (2 * (int64_t)light >= (int64_t)B || many_waves != 0));
+  if (threadIdx.x == 0) *variants = on ? 1 : 0;
+  const uint64_t mask = (shift >= 0 && !on) ? ~(3ull << shift) : ~0ull;
+  for (int u = threadIdx.x; u < B; u += blockDim.x) {
+    keys[u] &= mask;
+    idx[u] = u;
+  }
+  for (int q = B + (int)threadIdx.x; q < slots; q += blockDim.x) order[q] = B;
+}
+
 }  // namespace
+
+hipError_t launch_slot_order(uint64_t *keys, uint64_t *keys_sorted, int32_t *idx, int B, int shift, int mode,
+                             bool many_waves, int32_t *variants, int32_t *order, int slots, void *temp,
+                             size_t *temp_bytes, hipStream_t st) {
+  if (!temp) return hipcub::DeviceRadixSort::SortPairs(nullptr, *temp_bytes, keys, keys_sorted, idx, order, B, 0, 64, st);
+  hipLaunchKernelGGL(order_rule_kernel, dim3(1), dim3(1024), 0, st, keys, B, shift, mode, many_waves ? 1 : 0,
+                     variants, idx, order, slots);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // stable (LSD radix): ties keep the utterance order, as the host's stable sort did
+  return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, keys, keys_sorted, idx, order, B, 0, 64, st);
+}
 
 hipError_t launch_utterance_keys(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, int noise_class,
                                  hipStream_t st) {

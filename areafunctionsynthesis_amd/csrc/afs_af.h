@@ -36,4 +36,12 @@ hipError_t launch_target_frames(const double *seq, int Q, const TargetPlan &plan
 hipError_t launch_utterance_keys(const afs_frame *frames, int64_t fstride, int B, uint64_t *keys, int noise_class,
                                  hipStream_t st);
 
+// The slot order on the device from keys[B] (launch_utterance_keys; overwritten): the variant rule
+// (mode 0 never, 1 the rule, 2 always; the class field at bit `shift`, -1: none) into *variants, the
+// utterances sorted stably by their (masked) keys into order[0 .. B), order[B .. slots) = B.
+// keys_sorted[B], idx[B]: scratch.  temp == nullptr: only *temp_bytes is set (the sort's scratch).
+hipError_t launch_slot_order(uint64_t *keys, uint64_t *keys_sorted, int32_t *idx, int B, int shift, int mode,
+                             bool many_waves, int32_t *variants, int32_t *order, int slots, void *temp,
+                             size_t *temp_bytes, hipStream_t st);
+
 }  // namespace afs

@@ -150,9 +150,24 @@ std::vector<int32_t> xcd_order(const std::vector<int32_t> &row, int B, int upb, 
   return order;
 }
 
+// A call's slot order for K1 (shape_order): the order (null: the identity), the launch's blocks, and
+// whether K1 may run the noise-phase variants (variants_dev: decided on the device, else `variants`).
+struct SlotOrder {
+  const int32_t *order = nullptr;
+  int grid = 0;
+  bool variants = true;
+  const int32_t *variants_dev = nullptr;
+};
+// the slot order of a call without one (the voice kernel, sessions, target sequences, small batches)
+SlotOrder plain_order(const afs_ctx *c) {
+  SlotOrder so;
+  so.variants = c->noise_variants != 0;
+  return so;
+}
+
 afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int rows, int ntrans, int hop,
                       double *out, int64_t ostride, void *ws, int32_t *rng, void *lanes, int64_t bp, int B,
-                      int width, const int32_t *frame_row = nullptr, const int32_t *order = nullptr, int grid = 0) {
+                      int width, const int32_t *frame_row, const SlotOrder &so) {
   if (tree(c)) {
     const int64_t S = (int64_t)ntrans * hop;
     const int two = c->cfg.options.glottis_model == AFS_GLOTTIS_TWO_MASS ? 1 : 0;
@@ -163,7 +178,7 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
     // (stride and base congruent to the output's modulo 16 doubles): K1 stores both through one
     // line-aligned window (tree_kernel.h).
     auto p25_for = [&](int64_t per, int64_t *stride) -> afs_status {
-      if (!AFS_TONE_K6) return AFS_OK;  // (the tone filter in K1: no pressures stored)
+      if (AFS_TONE_K6 != 1) return AFS_OK;  // (the tone filter in K1: no pressures stored)
       *stride = per + ((ostride - per) % 16 + 16) % 16;
       return ensure(c, &c->p25, &c->p25_bytes, ((size_t)B * (size_t)*stride + 32) * sizeof(double));
     };
@@ -173,19 +188,22 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       return (double *)c->p25 + ((want - have) % 16 + 16) % 16;
     };
     // K1 over samples [s0, s1), then K6 over them (both timed)
+    // (skip: the launches of the hop-mode fast path when its compact slots may overflow: they do
+    // nothing when K5 claimed more than skip_cap slots)
     auto synth = [&](int64_t s0, int64_t s1, const uint64_t *plan, int64_t plan_stride, const afs::tree::PlanHop *hops,
-                     int64_t hop_stride, int64_t p25_stride) -> afs_status {
+                     int64_t hop_stride, int64_t p25_stride, const uint32_t *skip = nullptr,
+                     int64_t skip_cap = 0) -> afs_status {
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride, plan, plan_stride, lanes,
-                      (double *)ws, B, c->host_tab.uni, hops, hop_stride, p25_row0(s0), p25_stride, order,
-                      c->call_variants ? 1 : 0, grid};
+                      (double *)ws, B, c->host_tab.uni, hops, hop_stride, p25_row0(s0), p25_stride, so.order,
+                      so.variants ? 1 : 0, so.grid, so.variants_dev, skip, skip_cap};
       hipEvent_t e1 = prof_event(c);
       HIP_TRY(c, afs::launch_tree_synth(a, width, c->stream));
       hipEvent_t e2 = prof_event(c);
       prof_pair(c, e1, e2, 0);
       // K6: the glottal-tone filter and the output stage of the launch's samples
       HIP_TRY(c, afs::launch_tree_output(c->dev_tab, (double *)ws, out + s0, ostride, s1 - s0, B,
-                                         AFS_TONE_K6 ? p25_row0(s0) : nullptr, p25_stride,
-                                         c->cfg.options.radiation_from_skin, c->stream));
+                                         AFS_TONE_K6 == 1 ? p25_row0(s0) : nullptr, p25_stride,
+                                         c->cfg.options.radiation_from_skin, c->stream, skip, skip_cap));
       prof_pair(c, e2, prof_event(c), 2);
       return AFS_OK;
     };
@@ -211,45 +229,41 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       afs::PlanArgs pa{c->dev_tab, frames, fstride, rows, hop, 0, S, nullptr, 0, two, uo, hbuf, hstride, work, true};
       hipEvent_t e0 = prof_event(c);
       HIP_TRY(c, afs::launch_plan_hops_iv(pa, c->stream));
-      // Slots for the mixed hops.  When every hop of the call fits them (small calls: real-time
-      // sessions, short batches) they are sized for that worst case and the call runs without a
-      // host wait.  Otherwise the host reads the list's length back (waiting for the work queued so
-      // far on the stream, the previous call's kernels included) and offers min(listed, budget)
-      // slots; only when the list is longer than the budget's slots does it read back how many the
-      // mixed hops claimed (most listed hops are not mixed: near-ties decided alike by every sample).
+      // Slots for the mixed hops: one for every hop of the call when they fit the budget (small calls:
+      // real-time sessions, short batches), else the budget's worth.  No host read-back before K1: the
+      // launches are queued at once, guarded by the count of slots K5's second stage claimed (they do
+      // nothing if it exceeds the slots); the host then waits for K5 alone -- the launches are already
+      // queued behind it, so the device never idles for the host -- and, in the rare call whose mixed
+      // hops overflowed the slots, queues the chunked path below (most listed hops are not mixed:
+      // near-ties decided alike by every sample; static vowels have none).
       const int64_t slot_bytes = (int64_t)hop * afs::PLAN_RECORD_BYTES;
-      int64_t cap = (int64_t)rows * call_hops;
-      bool check = false;
-      if (cap * slot_bytes > std::min<int64_t>(c->plan_budget, SMALL_CALL_DENSE_BYTES)) {
-        HIP_TRY(c, hipMemcpyAsync(c->hcount, work, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        const int64_t listed = (int64_t)(uint32_t)*c->hcount;
-        cap = std::min<int64_t>(listed, c->plan_budget / slot_bytes);
-        check = cap < listed;
-      }
-      if (cap > 0 && (st = ensure(c, &c->plan, &c->plan_bytes, (size_t)(cap * slot_bytes))) != AFS_OK) return st;
+      const int64_t every = (int64_t)rows * call_hops;
+      const bool small = every * slot_bytes <= std::min<int64_t>(c->plan_budget, SMALL_CALL_DENSE_BYTES);
+      const int64_t cap = small ? every : std::min<int64_t>(every, std::max<int64_t>(1, c->plan_budget / slot_bytes));
+      if ((st = ensure(c, &c->plan, &c->plan_bytes, (size_t)(cap * slot_bytes))) != AFS_OK) return st;
       pa.plan = (uint64_t *)c->plan;
       pa.dense_cap = cap;
       HIP_TRY(c, afs::launch_plan_hops_wave(pa, c->stream));
-      bool fits = true;
-      if (check) {
+      const bool guard = cap < every;
+      if (guard) {
         HIP_TRY(c, hipMemcpyAsync(c->hcount, work + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        fits = (int64_t)(uint32_t)*c->hcount <= cap;
+        HIP_TRY(c, hipEventRecord(c->ev_k5, c->stream));
       }
       prof_pair(c, e0, prof_event(c), 1);
-      if (fits) {
-        const int64_t per = std::min<int64_t>(S, c->launch_cap);
-        int64_t p25_stride = 0;
-        if ((st = p25_for(per, &p25_stride)) != AFS_OK) return st;
-        for (int64_t s0 = 0; s0 < S; s0 += per) {
-          const int64_t s1 = std::min(S, s0 + per);
-          // (K1 indexes the records from the launch's first hop)
-          if ((st = synth(s0, s1, (const uint64_t *)c->plan, 0, hbuf + s0 / hop, hstride, p25_stride)) != AFS_OK)
-            return st;
-        }
-        return AFS_OK;
+      const int64_t per = std::min<int64_t>(S, c->launch_cap);
+      int64_t p25_stride = 0;
+      if ((st = p25_for(per, &p25_stride)) != AFS_OK) return st;
+      for (int64_t s0 = 0; s0 < S; s0 += per) {
+        const int64_t s1 = std::min(S, s0 + per);
+        // (K1 indexes the records from the launch's first hop)
+        if ((st = synth(s0, s1, (const uint64_t *)c->plan, 0, hbuf + s0 / hop, hstride, p25_stride,
+                        guard ? work + 1 : nullptr, cap)) != AFS_OK)
+          return st;
       }
+      if (!guard) return AFS_OK;
+      HIP_TRY(c, hipEventSynchronize(c->ev_k5));
+      if ((int64_t)(uint32_t)*c->hcount <= cap) return AFS_OK;
+      // (overflow: the guarded launches did nothing, the state is still the call's initial state)
     }
     // Chunked path: launches of `per` samples, each K5 (the chunk's plans: dense records, or in
     // hop mode the chunk's hop records with sample-indexed dense records) and then K1.  With
@@ -474,7 +488,7 @@ afs_status afs_create(afs_ctx **out, const afs_config *cfg) {
     if (v > 0) ctx->launch_cap = std::min<int64_t>(v, 65536);
   }
   if (hipStreamCreateWithFlags(&ctx->plan_stream, hipStreamNonBlocking) != hipSuccess) return bail(AFS_ERR_HIP);
-  for (hipEvent_t *e : {&ctx->ev_go, &ctx->ev_plan[0], &ctx->ev_plan[1], &ctx->ev_free[0], &ctx->ev_free[1]})
+  for (hipEvent_t *e : {&ctx->ev_go, &ctx->ev_plan[0], &ctx->ev_plan[1], &ctx->ev_free[0], &ctx->ev_free[1], &ctx->ev_k5})
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return bail(AFS_ERR_HIP);
   {
     ctx->plan_budget = PLAN_BUDGET_DEFAULT;
@@ -501,6 +515,7 @@ void afs_destroy(afs_ctx *c) {
   if (c->tgt) (void)hipFree(c->tgt);
   if (c->keys) (void)hipFree(c->keys);
   if (c->order_buf) (void)hipFree(c->order_buf);
+  if (c->sort_tmp) (void)hipFree(c->sort_tmp);
   if (c->plan_stream) (void)hipStreamSynchronize(c->plan_stream);
   if (c->plan) (void)hipFree(c->plan);
   if (c->plan2) (void)hipFree(c->plan2);
@@ -510,7 +525,7 @@ void afs_destroy(afs_ctx *c) {
     if (w) (void)hipFree(w);
   if (c->p25) (void)hipFree(c->p25);
   if (c->plan_stream) (void)hipStreamDestroy(c->plan_stream);
-  for (hipEvent_t e : {c->ev_go, c->ev_plan[0], c->ev_plan[1], c->ev_free[0], c->ev_free[1]})
+  for (hipEvent_t e : {c->ev_go, c->ev_plan[0], c->ev_plan[1], c->ev_free[0], c->ev_free[1], c->ev_k5})
     if (e) (void)hipEventDestroy(e);
   if (c->stage_nf) (void)hipFree(c->stage_nf);
   if (c->dcount) (void)hipFree(c->dcount);
@@ -545,54 +560,62 @@ afs_status afs_synchronize(afs_ctx *c) {
 // (noise sources, the cutoff filter's exponential, mixed hops) -- and the blocks of a compute unit
 // play alike shapes, the heaviest (narrowest constrictions) first.  Each utterance's audio is the
 // same in any slot.  Config-4 shard: +2.7 % static vowels, +1.4 % fricatives against the call order
-// (profiles/r04s_shape_order_ab.txt, r04v_shape_key_ab.txt).  One key kernel, a 64-KB read-back and
-// a host sort per call; off for the voice kernel (one utterance per wave), batches of one block and
-// AFS_SHAPE_ORDER=0.
-static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstride, int B, int width,
-                              const int32_t **dord, int *grid) {
-  *dord = nullptr;
-  *grid = 0;
-  c->call_variants = c->noise_variants != 0;  // (calls without a slot order: the voice kernel, small batches)
+// (profiles/r04s_shape_order_ab.txt, r04v_shape_key_ab.txt).  Off for the voice kernel (one
+// utterance per wave), batches of one block and AFS_SHAPE_ORDER=0.
+//
+// All on the device, with no host wait (the call's K1 is queued behind it while the previous call's
+// K1 still runs): the key kernel, the variant rule and a stable radix sort of (key, utterance)
+// (af_kernels.hip launch_slot_order).  The rule: the noise-phase variants pay when most waves are
+// light, or when every SIMD runs many waves: at 8192 static vowels (61 % light, two waves per SIMD)
+// +2.3 %, at 8192 fricatives (28 % light) -3 % -- the full-phase waves lose more to the light ones'
+// copies of the kernel body in their CUs' instruction caches than the light ones gain -- but at 65536
+// fricatives (16 waves per SIMD, the classes in long runs of the slot order) +0.7 %, at 32768 (8 per
+// SIMD) +0.05 % (profiles/r05i_fricatives_variants_ab.txt, r05k_variant_rule_ab.txt,
+// r05r_variant_rule_ab.txt).  Without them the class is left out of the sort (the class key alone
+// measured -0.6 %, r05f_variant_order_ab.txt).  (AFS_CLASS_ORDER=3, an A/B study, deals the blocks to
+// the XCDs on the host.)
+static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstride, int B, int width, SlotOrder *so) {
+  *so = plain_order(c);
   const int upb = afs::TREE_UPB;
   if (!tree(c) || !c->shape_order || width == afs::TREE_VOICE_W || B <= upb) return AFS_OK;
   const int nb = (B + upb - 1) / upb;
   const bool by_xcd = c->class_order == 3 && c->noise_variants != 0;
   afs_status s;
-  if ((s = ensure(c, &c->keys, &c->keys_bytes, (size_t)B * sizeof(uint64_t))) != AFS_OK) return s;
+  // keys[B], sorted keys[B], indices[B], the variant flag
+  const size_t kb = (size_t)B * (2 * sizeof(uint64_t) + sizeof(int32_t)) + 16;
+  if ((s = ensure(c, &c->keys, &c->keys_bytes, kb)) != AFS_OK) return s;
   uint64_t *dkeys = (uint64_t *)c->keys;
   HIP_TRY(c, afs::launch_utterance_keys(dframes, fstride, B, dkeys, by_xcd ? 1 : (c->class_order == 3 ? 0 : c->class_order),
                                         c->stream));
+  if (!by_xcd) {
+    uint64_t *dsorted = dkeys + B;
+    int32_t *didx = (int32_t *)(dsorted + B);
+    int32_t *dvar = didx + B;
+    const int shift = c->class_order == 1 ? 48 : c->class_order == 2 ? 40 : -1;
+    const int64_t waves_per_simd = (int64_t)B / ((int64_t)(64 / afs::TREE_W) * std::max(1, c->simds));
+    const int mode = c->noise_variants == 0 ? 0 : c->noise_variants == 1 ? 1 : 2;
+    if ((s = ensure(c, &c->order_buf, &c->order_bytes, (size_t)nb * upb * sizeof(int32_t))) != AFS_OK) return s;
+    size_t tb = 0;
+    HIP_TRY(c, afs::launch_slot_order(dkeys, dsorted, didx, B, shift, mode, waves_per_simd >= 16, dvar,
+                                      (int32_t *)c->order_buf, nb * upb, nullptr, &tb, c->stream));
+    if ((s = ensure(c, &c->sort_tmp, &c->sort_tmp_bytes, tb + 256)) != AFS_OK) return s;
+    tb = c->sort_tmp_bytes;
+    HIP_TRY(c, afs::launch_slot_order(dkeys, dsorted, didx, B, shift, mode, waves_per_simd >= 16, dvar,
+                                      (int32_t *)c->order_buf, nb * upb, c->sort_tmp, &tb, c->stream));
+    so->order = (const int32_t *)c->order_buf;
+    so->grid = nb;
+    so->variants_dev = dvar;
+    return AFS_OK;
+  }
   c->hkeys.resize((size_t)B);
   HIP_TRY(c, hipMemcpyAsync(c->hkeys.data(), dkeys, (size_t)B * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  // The noise-phase variants pay when most waves are light, or when every SIMD runs many waves: at
-  // 8192 static vowels (61 % light, two waves per SIMD) +2.3 %, at 8192 fricatives (28 % light)
-  // -3 % -- the full-phase waves lose more to the light ones' copies of the kernel body in their
-  // CUs' instruction caches than the light ones gain -- but at 65536 fricatives (16 waves per SIMD,
-  // the classes in long runs of the slot order) +0.7 %, at 32768 (8 per SIMD) +0.05 %
-  // (profiles/r05i_fricatives_variants_ab.txt, r05k_variant_rule_ab.txt, r05r_variant_rule_ab.txt).  Without them the class is left out of the sort (the class key alone
-  // measured -0.6 %, r05f_variant_order_ab.txt).
-  uint64_t class_mask = 0;
-  if (c->class_order == 1 || c->class_order == 3) class_mask = 3ull << 48;
-  if (c->class_order == 2) class_mask = 3ull << 40;
-  if (class_mask && c->noise_variants == 1) {
-    const int shift = class_mask == (3ull << 48) ? 48 : 40;
-    int64_t light = 0;
-    for (int u = 0; u < B; ++u) light += ((c->hkeys[(size_t)u] >> shift) & 3) != 0;
-    const int64_t waves_per_simd = (int64_t)B / ((int64_t)(64 / afs::TREE_W) * std::max(1, c->simds));
-    c->call_variants = 2 * light >= (int64_t)B || waves_per_simd >= 16;
-  }
-  const uint64_t sort_mask = c->call_variants ? ~0ull : ~class_mask;
   std::vector<int32_t> idx((size_t)B);
   for (int u = 0; u < B; ++u) idx[(size_t)u] = u;
-  std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) {
-    return (c->hkeys[(size_t)a] & sort_mask) < (c->hkeys[(size_t)b] & sort_mask);
-  });
+  std::stable_sort(idx.begin(), idx.end(),
+                   [&](int32_t a, int32_t b) { return c->hkeys[(size_t)a] < c->hkeys[(size_t)b]; });
   int nblocks = nb;
-  if (!by_xcd) {
-    c->horder.assign((size_t)nb * upb, B);
-    for (int q = 0; q < B; ++q) c->horder[(size_t)q] = idx[(size_t)q];
-  } else {
+  {
     // The blocks of the class-major order (the full noise phases first) dealt to the 8 XCDs in
     // contiguous runs of equal expected cost, so that the blocks one XCD runs -- whose waves share
     // its CUs' instruction caches -- run one noise-phase variant (at most one change per XCD): a
@@ -635,8 +658,9 @@ static afs_status shape_order(afs_ctx *c, const afs_frame *dframes, int64_t fstr
   const size_t obytes = c->horder.size() * sizeof(int32_t);
   if ((s = ensure(c, &c->order_buf, &c->order_bytes, obytes)) != AFS_OK) return s;
   HIP_TRY(c, hipMemcpyAsync(c->order_buf, c->horder.data(), obytes, hipMemcpyHostToDevice, c->stream));
-  *dord = (const int32_t *)c->order_buf;
-  *grid = nblocks;
+  so->order = (const int32_t *)c->order_buf;
+  so->grid = nblocks;
+  so->variants = true;
   return AFS_OK;
 }
 
@@ -678,11 +702,10 @@ static afs_status synth_core(afs_ctx *c, const afs_frame *frames, const uint32_t
     return s;
   if ((s = reset_state(c, c->ws, c->rng, c->tree_lanes, bp, B, dseeds, width)) != AFS_OK) return s;
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-  const int32_t *dord = nullptr;
-  int grid = 0;
-  if ((s = shape_order(c, dframes, F, B, width, &dord, &grid)) != AFS_OK) return s;
+  SlotOrder so;
+  if ((s = shape_order(c, dframes, F, B, width, &so)) != AFS_OK) return s;
   if ((s = run_chunks(c, dframes, F, B, F - 1, hop, dout, T, c->ws, c->rng, c->tree_lanes, bp, B, width, nullptr,
-                      dord, grid)) != AFS_OK)
+                      so)) != AFS_OK)
     return s;
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   c->last_B = B;
@@ -959,18 +982,15 @@ afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32
   afs_ctx *c = s->ctx;
   HIP_TRY(c, hipSetDevice(c->cfg.device));
   const int B = s->B;
-  // (the kinds of the caller's pointers are probed once per new pointer: a real-time caller
-  // passes the same buffers every call)
-  if (frames != s->last_in) {
-    s->last_in = frames;
-    s->last_in_dev = is_device_ptr(frames);
-  }
+  // (the kinds of the caller's pointers are probed on every call: a freed buffer's address may come
+  // back as memory of the other kind; one pointer query is ~1 us beside a ~6 ms call)
+  const bool in_dev = is_device_ptr(frames);
   const afs_frame *src = frames;
-  if (!s->last_in_dev) {  // host frames: through the session's pinned buffer
+  if (!in_dev) {  // host frames: through the session's pinned buffer
     std::memcpy(s->hframes, frames, (size_t)B * sizeof(afs_frame));
     src = s->hframes;
   }
-  const hipMemcpyKind k = s->last_in_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  const hipMemcpyKind k = in_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   // frames[u] -> pair[u][slot]
   const int slot = s->latched ? 1 : 0;
   HIP_TRY(c, hipMemcpy2DAsync(s->pair + slot, 2 * sizeof(afs_frame), src, sizeof(afs_frame),
@@ -984,12 +1004,8 @@ afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32
   }
   if (!out) return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_session_synthesize: out is NULL");
   if (n < 1) n = 1;  // Synthesizer.cpp:543-546
-  if (out != s->last_out) {
-    s->last_out = out;
-    s->last_out_dev = is_device_ptr(out);
-  }
   double *dout = out;
-  const bool host_out = !s->last_out_dev;
+  const bool host_out = !is_device_ptr(out);
   const size_t nout = (size_t)B * (size_t)n;
   afs_status st;
   if (host_out) {
@@ -1004,7 +1020,8 @@ afs_status afs_session_synthesize(afs_session *s, const afs_frame *frames, int32
     }
   }
   HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
-  if ((st = run_chunks(c, s->pair, 2, B, 1, n, dout, n, s->ws, s->rng, s->tree_lanes, s->bp, B, s->lanes)) != AFS_OK)
+  if ((st = run_chunks(c, s->pair, 2, B, 1, n, dout, n, s->ws, s->rng, s->tree_lanes, s->bp, B, s->lanes, nullptr,
+                       plain_order(c))) != AFS_OK)
     return st;
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
   // prevTube = *newTube (Synthesizer.cpp:633-637)
@@ -1222,8 +1239,10 @@ afs_status afs_play_target_sequences(afs_ctx *c, const double *shapes, int32_t n
   for (int64_t k0 = 0; k0 < T; k0 += Tc) {
     const int nk = (int)std::min<int64_t>(Tc, T - k0);
     HIP_TRY(c, afs::launch_target_frames(dseq, Q, plan, k0, nk + 1, Tc + 1, dframes, c->stream));
+    SlotOrder so = plain_order(c);
+    so.order = dord;
     if ((s = run_chunks(c, dframes, Tc + 1, Q, nk, 1, dout + k0, T, c->ws, c->rng, c->tree_lanes, bp, B, width,
-                        drow, dord)) != AFS_OK)
+                        drow, so)) != AFS_OK)
       return s;
   }
   HIP_TRY(c, hipEventRecord(c->ev1, c->stream));

@@ -49,10 +49,11 @@ struct afs_ctx {
   // AFS_NOISE_VARIANTS: 1 (default) K1's noise-phase variants for the calls whose slot order finds
   // at least half of the utterances in a light class (shape_order), 2 for every call, 0 never
   int noise_variants = 1;
-  bool call_variants = true;           // this call's choice (shape_order; run_chunks passes it to K1)
   int class_order = 2;                 // AFS_CLASS_ORDER: the slot order's noise-class key (af_kernels.hip; A/B)
-  void *keys = nullptr;                // shape keys (device)
+  void *keys = nullptr;                // shape keys, sorted keys, utterance indices, the variant flag (device)
   size_t keys_bytes = 0;
+  void *sort_tmp = nullptr;            // the device radix sort's scratch
+  size_t sort_tmp_bytes = 0;
   void *order_buf = nullptr;           // the slot order built from them (device)
   size_t order_bytes = 0;
   std::vector<uint64_t> hkeys;
@@ -60,6 +61,7 @@ struct afs_ctx {
   hipStream_t plan_stream = nullptr;  // K5 of the next launch, beside K1 of this one (overlap)
   bool overlap = false;                // AFS_PLAN_OVERLAP=1 (afs_capi.cpp run_chunks)
   hipEvent_t ev_go = nullptr, ev_plan[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
+  hipEvent_t ev_k5 = nullptr;  // after K5 and the read-back of its claimed slots (run_chunks' guarded fast path)
   int64_t plan_budget = 0;  // bytes of plans one launch may use (afs_capi.cpp)
   void *stage_nf = nullptr;  // per-utterance non-finite flags staged for a host array
   size_t stage_nf_bytes = 0;
@@ -92,12 +94,10 @@ struct afs_session {
   uint32_t *seeds = nullptr;   // device copy
   bool latched = false;
   // pinned staging of host frames and host output (a real-time caller's per-call copies go
-  // through these instead of pageable memory) and the kinds of the caller's last pointers
+  // through these instead of pageable memory)
   afs_frame *hframes = nullptr;
   double *hout = nullptr;
   size_t hout_cap = 0;  // doubles
-  const void *last_in = nullptr, *last_out = nullptr;
-  bool last_in_dev = false, last_out_dev = false;
 };
 
 namespace afs {

@@ -44,6 +44,14 @@ struct TreeArgs {
   // blocks of the launch (0: enough for B utterances); with `order`, blocks whose slots are all
   // padding exit at once (the XCD-dealt slot order of afs_capi.cpp shape_order)
   int grid_blocks = 0;
+  // the variant rule decided on the device (afs_capi.cpp shape_order: the call's slot order sorted
+  // on the device): when set, *variants_dev replaces noise_variants
+  const int32_t *variants_dev = nullptr;
+  // hop mode with compact slots that may not hold every mixed hop (afs_capi.cpp run_chunks): the
+  // launch does nothing when K5 claimed more than skip_cap slots (*skip_claims > skip_cap); the host
+  // then runs the call through the chunked path instead
+  const uint32_t *skip_claims = nullptr;
+  int64_t skip_cap = 0;
 };
 // K5: the noise-source plans of samples [s_begin, s_end) of `rows` frame rows.
 struct PlanArgs {
@@ -63,7 +71,8 @@ struct PlanArgs {
                              // the compact slots claimed, then rows * hop slots list entries
   // hop mode: the dense records of a mixed hop go to the next free slot e of a compact array
   // (plan[(e * hop + i) * 16 + w] for the hop's sample i; PlanHop::dense = e; e < dense_cap, else
-  // nothing is written and the host, which reads work[1] back, falls back to shorter launches)
+  // nothing is written: the K1 / K6 launches guarded by work[1] do nothing and the host, which reads
+  // work[1] back, falls back to shorter launches)
   // instead of sample-indexed rows (the diagnostics' layout)
   bool compact = false;
   int64_t dense_cap = 0;
@@ -79,7 +88,9 @@ inline int64_t plan_work_bytes(int64_t rows, int64_t slots) { return (rows * slo
 #endif
 #ifndef AFS_TONE_K6
 // 1: K1 stores section 25's pressure per sample and K6 runs the glottal-tone filter over it
-// (+0.5 % end to end in round 3, profiles/r03ai_ab.txt); 0: K1 runs the filter itself (A/B builds)
+// (+0.5 % end to end in round 3, profiles/r03ai_ab.txt); 0: K1 runs the filter itself, per sample
+// (A/B builds); 2: K1 runs it over each 16-sample output window when the window is stored, the tone
+// added to the stored flows (tree_kernel.h tone_window; A/B builds)
 #define AFS_TONE_K6 1
 #endif
 #ifndef AFS_TREE_WPB
@@ -104,8 +115,10 @@ hipError_t launch_tree_synth(const TreeArgs &a, int lanes, hipStream_t st);
 // K6, after each tree_synth launch of samples [s_begin, s_end): the glottal-tone filter over the
 // section-25 pressures (p25, skin != 0) and the output stage over the flows the launch stored
 // (out[u * out_stride + s - s_begin], replaced by the audio).
+// (skip_claims: as TreeArgs::skip_claims -- the launch does nothing when *skip_claims > skip_cap)
 hipError_t launch_tree_output(const Tables *tab, double *lds_state, double *out, int64_t out_stride, int64_t n, int B,
-                              const double *p25, int64_t p25_stride, int skin, hipStream_t st);
+                              const double *p25, int64_t p25_stride, int skin, hipStream_t st,
+                              const uint32_t *skip_claims = nullptr, int64_t skip_cap = 0);
 // Load the tree kernels' and K5's code objects on the current device (afs_create: no code-object
 // load inside the first synthesis call).
 hipError_t preload_tree_kernels();

@@ -26,9 +26,11 @@ __global__ void __launch_bounds__(64 * Geom<W>::WPB, AFS_TREE_MIN_WAVES) tree_sy
 // stored pressures, added to the flows, in the output filter's loop (tone_output_run).
 __global__ void __launch_bounds__(64) tree_output_kernel(const Tables *tab, double *lds_state, double *out,
                                                          int64_t out_stride, int64_t n, int B, const double *p25,
-                                                         int64_t p25_stride, int skin) {
+                                                         int64_t p25_stride, int skin,
+                                                         const uint32_t *skip_claims, int64_t skip_cap) {
   const int u = blockIdx.x * 64 + threadIdx.x;
   if (u >= B) return;
+  if (skip_claims && (int64_t)*skip_claims > skip_cap) return;  // (as the guarded K1 launch: TreeArgs)
   double *X = lds_state + (int64_t)u * X_TOTAL;
   double *o = out + (int64_t)u * out_stride;
   if (p25 && skin) tone_output_run(X, tab->consts, p25 + (int64_t)u * p25_stride, o, (int)n);
@@ -114,10 +116,11 @@ hipError_t launch_tree_interp(const Tables *tab, const afs_frame *fl, const afs_
 }
 
 hipError_t launch_tree_output(const Tables *tab, double *lds_state, double *out, int64_t out_stride, int64_t n, int B,
-                              const double *p25, int64_t p25_stride, int skin, hipStream_t st) {
+                              const double *p25, int64_t p25_stride, int skin, hipStream_t st,
+                              const uint32_t *skip_claims, int64_t skip_cap) {
   if (B <= 0 || n <= 0) return hipSuccess;
   hipLaunchKernelGGL(tree_output_kernel, dim3((B + 63) / 64), dim3(64), 0, st, tab, lds_state, out, out_stride, n, B,
-                     p25, p25_stride, skin);
+                     p25, p25_stride, skin, skip_claims, skip_cap);
   return hipGetLastError();
 }
 

@@ -226,7 +226,50 @@ __device__ __forceinline__ int noise_variant(const TreeArgs &a) {
   if ((AFS_NZ_SET & 4) && (m & ~NoiseV<W, NZ_T1ALL>::SERVES) == 0) nz = NZ_T1ALL;
   if ((AFS_NZ_SET & 1) && (m & ~NoiseV<W, NZ_TONGUE1>::SERVES) == 0) nz = NZ_TONGUE1;
   if ((AFS_NZ_SET & 2) && (m & ~NoiseV<W, NZ_GLOTTIS>::SERVES) == 0) nz = NZ_GLOTTIS;
-  return __builtin_amdgcn_readfirstlane(a.noise_variants ? nz : (int)NZ_FULL);
+  const int on = a.variants_dev ? *a.variants_dev : a.noise_variants;
+  return __builtin_amdgcn_readfirstlane(on ? nz : (int)NZ_FULL);
+}
+
+// AFS_TONE_K6 == 2: the glottal-tone filter (TdsModel.cpp:494-510, 687-705) over positions j0 .. j1
+// of a 16-sample output window -- lane p of the utterance's row holds sample p's section-25 pressure
+// (wp) and radiated flow (wo) -- in sample order, with K6's operations in K6's order (uncontracted),
+// so the audio is the same bit for bit as with the filter in K6; the state (X_TONE) in LDS between
+// windows.  Every lane evaluates the recurrence (lane-uniform), lane p keeps its sample's sum.
+template <int P, class F> __device__ __forceinline__ void unroll16(F &f) {
+  f(std::integral_constant<int, P>{});
+  if constexpr (P + 1 < 16) unroll16<P + 1>(f);
+}
+template <class Ex>
+__device__ __forceinline__ void tone_window(int gl, double *X, const Consts &C, int j0, int j1, double &wo,
+                                            double wp) {
+#pragma clang fp contract(off)
+  double x1 = X[X_TONE + 0], x2 = X[X_TONE + 1], x3 = X[X_TONE + 2], x4 = X[X_TONE + 3];
+  double y1 = X[X_TONE + 4], y2 = X[X_TONE + 5], y3 = X[X_TONE + 6], y4 = X[X_TONE + 7];
+  const double *ta = C.h.tone_a, *tb = C.h.tone_b;
+  const double a0 = ta[0], a1 = ta[1], a2 = ta[2], a3 = ta[3], a4 = ta[4];
+  const double b1 = tb[1], b2 = tb[2], b3 = tb[3], b4 = tb[4];
+  auto step = [&](auto P) {
+    constexpr int p = decltype(P)::value;
+    if (p < j0 || p > j1) return;
+    const double xp = Ex::template dpp<0x150 + p>(wp);  // (row_newbcast p)
+    double tacc = a0 * xp;
+    tacc += a1 * x1;
+    tacc += b1 * y1;
+    tacc += a2 * x2;
+    tacc += b2 * y2;
+    tacc += a3 * x3;
+    tacc += b3 * y3;
+    tacc += a4 * x4;
+    tacc += b4 * y4;
+    x4 = x3; x3 = x2; x2 = x1; x1 = xp;
+    y4 = y3; y3 = y2; y2 = y1; y1 = tacc;
+    wo = gl == p ? wo + tacc : wo;
+  };
+  unroll16<0>(step);
+  if (gl == 0) {
+    X[X_TONE + 0] = x1; X[X_TONE + 1] = x2; X[X_TONE + 2] = x3; X[X_TONE + 3] = x4;
+    X[X_TONE + 4] = y1; X[X_TONE + 5] = y2; X[X_TONE + 6] = y3; X[X_TONE + 7] = y4;
+  }
 }
 
 // prof (PROF only): per wave, PH_COUNT cycle sums (s_memtime) over the launch.
@@ -329,10 +372,19 @@ __device__ __forceinline__ void tree_synth_run(const TreeArgs &a, WaveLdsT<W> &l
       const bool mine = gl == j;
       wo = mine ? R.sample : wo;
       wp = mine ? p25v : wp;
+      if constexpr (AFS_TONE_K6 == 2) {
+        // the glottal-tone filter over the window's samples once it is complete (positions j0 .. j),
+        // its outputs added to the window's flows before the store (wave-uniform when the utterances'
+        // rows are congruent modulo 16 doubles, else per utterance)
+        if (j == 15 || t + 1 == n) {
+          const int j0 = t >= j ? 0 : (int)(j - t);
+          if (a.uni.opt.radiation_from_skin) tone_window<GpuExec<PROF, W>>(gl, X, C, j0, j, wo, wp);
+        }
+      }
       // lane gl stores window entry gl, sample t - j + gl, if it belongs to this launch
       if (valid && (j == 15 || t + 1 == n) && gl <= j && t - j + gl >= 0) {
         o[t - j + gl] = wo;
-        if constexpr (AFS_TONE_K6 != 0) p25o[t - j + gl] = wp;
+        if constexpr (AFS_TONE_K6 == 1) p25o[t - j + gl] = wp;
       }
     }
     if (++i == hop) {
@@ -380,6 +432,9 @@ __device__ __forceinline__ void tree_synth_run(const TreeArgs &a, WaveLdsT<W> &l
 #endif
 template <bool PROF, int MODEL, bool HOPS = false, int W = TW>
 __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &lds, uint64_t *prof) {
+  // (a launch of the hop-mode fast path whose mixed hops overflowed K5's compact slots: the host runs
+  // the call through the chunked path instead, afs_capi.cpp run_chunks)
+  if (a.skip_claims && (int64_t)*a.skip_claims > a.skip_cap) return;
   if (a.order) {  // a block of padding slots only (the XCD-dealt slot order) has nothing to do
     bool any = false;
 #pragma unroll

@@ -132,9 +132,11 @@ class Context:
             nonfinite = np.zeros(B, dtype=np.uint8)
         if nonfinite is not None and _nbytes(nonfinite) != B:
             raise ValueError("nonfinite must hold B bytes")
+        # (a report makes the call wait for the device: only when asked, so that an AFS_ASYNC context's
+        # calls with device buffers return once queued)
         rep = _native.AfsReport()
         st = self._lib.afs_synthesize(self._h, _vp(_addr(frames)), _vp(_addr(seeds)), B, F, hop,
-                                      _vp(_addr(out)), _vp(_addr(nonfinite)), ctypes.byref(rep))
+                                      _vp(_addr(out)), _vp(_addr(nonfinite)), ctypes.byref(rep) if report else None)
         _native.check(st, self._h, "afs_synthesize")
         if report:
             return out, {"device_ms": rep.device_ms, "samples": rep.samples,

@@ -111,10 +111,12 @@ typedef struct afs_options {
   double flow_separation_area_ratio; /* 1.0 */
 } afs_options;
 
-/* Calls return once their work is queued on the context's stream, except where a call must read
- * something back to order or size its launches (large tree batches: the slot order's shape keys,
- * the length of K5's noise-plan work list); such a read-back waits for all work queued before it
- * on the stream, the previous call's synthesis included. */
+/* Calls return once their work is queued on the context's stream.  One exception: a large tree call
+ * (its mixed hops' noise plans may overflow the plan budget) reads back how many plan slots K5
+ * claimed, after its synthesis launches are queued (guarded on the device: they do nothing on an
+ * overflow, and the call then queues its chunked path).  That wait covers the work queued before K5,
+ * the previous call's synthesis included, but the device does not idle: this call's synthesis is
+ * queued behind K5.  The slot order is sorted on the device, with no read-back. */
 #define AFS_ASYNC 0x1u
 /* Record an event pair around every kernel launch of the synthesis calls; afs_kernel_times
  * returns their summed durations (measurement only: a few microseconds per launch). */
@@ -167,7 +169,9 @@ int32_t afs_abi_version(void);
 /* Environment read by afs_create (studies and A/B runs; the defaults are the measured best):
  *   AFS_PLAN_DENSE=1        every hop reads K5's dense per-sample records (bit-exact plan, below)
  *   AFS_PLAN_BUDGET_MB=N    noise-plan memory per call (default 4096); past it the call runs in
- *                           launches of at most N MB of plans
+ *                           launches of at most N MB of plans -- with one floor: a launch spans at
+ *                           least one hop, so a hop-mode launch holds at least two hops of dense
+ *                           records per row (2 x hop x 128 B x rows) even when that exceeds N MB
  *   AFS_LAUNCH_SAMPLES=N    samples per synthesis-kernel launch at most (default 65536; the state
  *                           crosses launches, the audio is the same bit for bit)
  *   AFS_XCD_ORDER=0         shared trajectories (target sequences) in utterance order instead of

@@ -284,3 +284,34 @@ def test_noise_variants_bitwise(emu, oracle, hop_mode, W):
     if W == 16:
         assert used[1] > 0 and used[2] > 0, used  # (and both tongue variants)
     hop_mode()
+
+
+@pytest.mark.parametrize("case", ["tiny_pharynx", "alternating", "wide_open"])
+def test_arm_scan_extreme_areas_vs_oracle(emu, oracle, case):
+    """The arm solver's lane scans (tree_core.h solve_arms, AFS_ARM_SCAN) on tracts far outside
+    speech: sections at the area clamp beside 60 cm^2 sections, a whole pharynx at the clamp, every
+    section wide open.  The pivot recurrence's 2 x 2 products span up to 8 lanes, an arm's first lane
+    included (its F = 0 makes the ratio, not the magnitude, independent of the lanes before it): the
+    products of up to 8 pivots must stay inside the fp64 range for any tract the model accepts (the
+    diagonal is bounded by the area clamp, ~1e7 at 44.1 kHz).  The emulator's audio stays finite and
+    equals the oracle's sequential Cholesky to the usual tolerance, relative to the signal."""
+    from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS
+    from areafunctionsynthesis_amd.params import default_shapes
+    f = oracle.af_to_frame(default_shapes()["a:"])
+    f["glottis"] = DEFAULT_GLOTTIS
+    f["velum_opening_cm2"] = 2.0
+    a = f["area_cm2"]
+    if case == "tiny_pharynx":
+        a[:20] = 0.0011
+    elif case == "alternating":
+        a[:] = np.where(np.arange(a.size) % 2 == 0, 0.0011, 60.0)
+    else:
+        a[:] = 60.0
+    f["area_cm2"] = a
+    frames = np.stack([f] * 6)
+    for fs, hop in ((22050.0, 256), (44100.0, 441)):
+        x = emu(frames, hop, 3, fs)
+        y = oracle.utterance(frames, hop, 3, fs)
+        assert np.all(np.isfinite(x)) and np.all(np.isfinite(y)), (case, fs)
+        scale = max(1.0, float(np.abs(y).max()))
+        assert np.abs(x[:2048] - y[:2048]).max() <= TOL * scale, (case, fs)
