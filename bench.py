@@ -405,7 +405,9 @@ def main() -> None:
     ap.add_argument("--seconds", type=float, default=1.0)
     ap.add_argument("--fs", type=float, default=44100.0)
     ap.add_argument("--solver", default=os.environ.get("AFS_SOLVER", "tree"))
-    ap.add_argument("--cpu-utterances", type=int, default=32)
+    ap.add_argument("--cpu-utterances", type=int, default=128,
+                    help="CPU baseline: utterances of the headline's bounded sample (128 x 1 s: ~38 core-seconds of "
+                         "the reference's work, ~2.5 s on the box's 16-CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=("static", "fricatives", "vcv"), default="static",
                     help="static: config-4 shard of static vowels (default); fricatives: config 5 "
@@ -423,7 +425,7 @@ def main() -> None:
                     help="N > 1: rccl (the library's afs_gather_pcm; default) or gloo through the host (test only)")
     ap.add_argument("--one-device", action="store_true",
                     help="N > 1: every rank on device 0 (test of the multi-process path on a one-GPU box)")
-    ap.add_argument("--sub-cpu-utterances", type=int, default=16)
+    ap.add_argument("--sub-cpu-utterances", type=int, default=48)
     ap.add_argument("--pg-timeout", type=float, default=300.0,
                     help="N > 1: seconds a rank waits in a control-plane collective before failing")
     ap.add_argument("--launch-check", action="store_true",
