@@ -20,7 +20,8 @@ from HIP events around every launch: afs_kernel_times), the fp64 object (the pat
 resource: algorithmic flops counted from the restatement, profiles/flops_per_sample.json) and
 the CPU baseline (the reference's own sources, oracle/_ref, timed on this host's cores over a
 bounded sample, plus the single-core config-1 figure).  On one GPU the line also carries
-"configs": config 5 (8192 fricatives, velum 1.0 cm^2) and config 3 (8192 VCV utterances through
+"configs": config 2 (1024 static vowels: one utterance per SIMD, the voice kernel's per-sample
+latency), config 5 (8192 fricatives, velum 1.0 cm^2) and config 3 (8192 VCV utterances through
 playTargetSequence), each timed over a few steps with its own launch times, roofline, fp64
 object, reference CPU rate and error against the reference build, and "config4_shard": config 4's
 per-GPU shard at 8 GPUs (8192 utterances; the headline of rounds 1-4), its rows checked bit for
