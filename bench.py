@@ -225,7 +225,8 @@ def measure(args, ctx, dev, stream, workload: str, B: int, first: int, world: in
     if comm is not None:
         comm.gather_times()  # (and the warm-up gathers)
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -235,12 +236,14 @@ def measure(args, ctx, dev, stream, workload: str, B: int, first: int, world: in
         synth()
         ev[k][1].record(stream)
         pcm.submit(out_dev)
+        ev[k][2].record(stream)
     pcm.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    m.synth_ms = [a.elapsed_time(b) for a, b in ev]
+    m.synth_ms = [a.elapsed_time(b) for a, b, _ in ev]
+    m.int16_ms = [b.elapsed_time(c) for _, b, c in ev]  # (the int16 conversion, and at N > 1 its gather's enqueue)
     m.kt = ctx.kernel_times()
     t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
@@ -372,8 +375,11 @@ def describe(args, m: Measured, world: int, digest: str) -> dict:
         roof["distinct_frame_bytes_per_launch"] = float(m.distinct) * samples_per_launch / B * 1072.0
     if tr and tr.get("plan_kernel_traffic_bytes_per_launch") is not None:
         roof["plan_kernel_traffic_bytes_per_launch"] = tr["plan_kernel_traffic_bytes_per_launch"]
-    return {"value": value, "ms_per_step": m.elapsed / m.steps * 1e3, "roofline": roof, "fp64": fp64,
-            "step_device_ms": float(np.mean(m.synth_ms)), "sq": sq}
+    ms_step = m.elapsed / m.steps * 1e3
+    dev_ms, i16_ms = float(np.mean(m.synth_ms)), float(np.mean(m.int16_ms))
+    return {"value": value, "ms_per_step": ms_step, "roofline": roof, "fp64": fp64,
+            "step_device_ms": dev_ms, "int16_ms_per_step": i16_ms, "idle_ms_per_step": ms_step - dev_ms - i16_ms,
+            "sq": sq}
 
 
 def cpu_leg(args, m: Measured, n: int):
@@ -549,6 +555,10 @@ def main() -> None:
             },
             "x_realtime": d["value"] / args.fs,
             "step_device_ms": d["step_device_ms"],
+            "int16_ms_per_step": d["int16_ms_per_step"],
+            # (the step's wall time not covered by its device work: host waits and launch gaps; HIP events on
+            # the library's stream around the synthesis call and the int16 conversion)
+            "idle_ms_per_step": d["idle_ms_per_step"],
             "roofline": d["roofline"],
             "fp64": d["fp64"],
         }
