@@ -86,6 +86,9 @@ inline int64_t plan_work_bytes(int64_t rows, int64_t slots) { return (rows * slo
 #ifndef AFS_TREE_W
 #define AFS_TREE_W 16
 #endif
+#ifndef AFS_PAIR
+#define AFS_PAIR 0  // 1: the throughput kernel as wave pairs (tree_kernel.h tree_pair_body; an A/B build)
+#endif
 #ifndef AFS_TONE_K6
 // 1: K1 stores section 25's pressure per sample and K6 runs the glottal-tone filter over it
 // (+0.5 % end to end in round 3, profiles/r03ai_ab.txt); 0: K1 runs the filter itself, per sample

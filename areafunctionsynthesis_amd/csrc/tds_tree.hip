@@ -18,6 +18,17 @@ __global__ void __launch_bounds__(64 * Geom<W>::WPB, AFS_TREE_MIN_WAVES) tree_sy
   tree_synth_body<false, MODEL, HOPS, W>(a, lds, nullptr);
 }
 
+#if AFS_PAIR
+// the wave-pair build of the throughput kernel (tree_kernel.h tree_pair_body): four waves per
+// workgroup, two per SIMD
+template <int MODEL, bool HOPS>
+__global__ void __launch_bounds__(256, 2) tree_pair_kernel(TreeArgs a) {
+  __shared__ WaveLdsT<TW> lds;
+  __shared__ int pattern[5];
+  tree_pair_body<MODEL, HOPS>(a, lds, pattern);
+}
+#endif
+
 // K6: the output stage of a launch's samples -- dU/dt, the 8-pole Chebyshev low-pass, x 0.004 /
 // 32767 (Synthesizer.cpp:614-627) -- over the radiated flows the synthesis kernel stored, in
 // place, one thread per utterance; the filter state (X_OUTF, X_PREVFLOW, X_NONFIN, X_TONE) lives in
@@ -144,6 +155,20 @@ static void launch_synth_w(const TreeArgs &a, hipStream_t st) {
   constexpr int UPB_ = Geom<W>::UPB;
   const dim3 grid(a.grid_blocks > 0 ? a.grid_blocks : (a.B + UPB_ - 1) / UPB_), block(64 * Geom<W>::WPB);
   const bool two = a.uni.opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
+#if AFS_PAIR
+  if constexpr (W == TW) {
+    static_assert(Geom<TW>::WPB == 2, "a wave pair per four utterances: 4 waves per 8-utterance block");
+    const dim3 pblock(256);
+    if (a.hops) {
+      if (two) hipLaunchKernelGGL((tree_pair_kernel<AFS_GLOTTIS_TWO_MASS, true>), grid, pblock, 0, st, a);
+      else hipLaunchKernelGGL((tree_pair_kernel<AFS_GLOTTIS_TRIANGULAR, true>), grid, pblock, 0, st, a);
+    } else {
+      if (two) hipLaunchKernelGGL((tree_pair_kernel<AFS_GLOTTIS_TWO_MASS, false>), grid, pblock, 0, st, a);
+      else hipLaunchKernelGGL((tree_pair_kernel<AFS_GLOTTIS_TRIANGULAR, false>), grid, pblock, 0, st, a);
+    }
+    return;
+  }
+#endif
   if (a.hops) {
     if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true, W>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, W>), grid, block, 0, st, a);

@@ -124,7 +124,13 @@ enum : int {
   X_TVEL = X_TGLOT + 8,        // transvelar coupling filters H1, H2: x1..x4, y1..y4 each
   X_TVP = X_TVEL + 16,         // p[43], p[67] after the last update (transvelar filter inputs)
   X_RRAD = X_TVP + 2,          // mouth radiation R and L (section 64), from the network phase
+#if AFS_PAIR
+  X_RELX2 = X_RRAD + 2,        // wave pairs: the glottis displacements' second buffer (sample_step_pair)
+  X_RNGHP = X_RELX2 + 4,       // wave pairs: the rand() ring head and pending count (two int32)
+  X_TOTAL = X_RNGHP + 1,
+#else
   X_TOTAL = X_RRAD + 2,
+#endif
   // LDS stride of the utterance blocks: 128 B modulo the 256-B bank row, so that the two
   // utterances of a 32-lane LDS lane group (ds_read_b64: lanes 0-31, 32-63) address the
   // same slot through disjoint banks
@@ -135,7 +141,10 @@ static_assert(X_STRIDE % 32 == 16, "utterance blocks offset by half a bank row")
 // Phase ids for Exec::mark (cycle accounting in tools/phase_prof; a no-op otherwise).
 enum : int {
   PH_GEOMETRY, PH_NETWORK, PH_NOISE, PH_N_AMP, PH_N_RNG,
-  PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_TARGETS, PH_COUNT
+  PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_TARGETS,
+  // wave pairs (sample_step_pair): the waits at the four barriers, the DYN wave's rand() blocks, the
+  // loop's tail (output window, frame transition and its barrier)
+  PH_P1WAIT, PH_P2WAIT, PH_P3WAIT, PH_P4WAIT, PH_RNGP, PH_TAIL, PH_COUNT
 };
 
 // Solver sink / zero slots (see ArmRec).
@@ -149,6 +158,15 @@ struct Shape {
   static constexpr int NSL = ND + NST;
   static constexpr int NDP = (NDIP + W - 1) / W;
 };
+
+// Wave pairs (tree_kernel.h, AFS_PAIR): two waves hold the same four utterances, each half of every
+// lane's slots -- ROLE_DYN the dynamic ones (and the radiated flow, the output window), ROLE_STAT the
+// static ones and the lane-uniform phases (glottis commit, targets, noise, solver, rand() blocks) --
+// so that two waves share each SIMD.  ROLE_ALL: one wave does everything (the default kernel).
+enum : int { ROLE_ALL = 0, ROLE_DYN = 1, ROLE_STAT = 2 };
+template <int ROLE> AFS_HD constexpr bool role_slot(int j, int nd) {
+  return ROLE == ROLE_ALL || ((ROLE == ROLE_DYN) == (j < nd));
+}
 
 AFS_HD inline int dyn_section(int W, int j, int gl) {
   int k = j * W + gl;
@@ -724,13 +742,13 @@ AFS_HD inline void phase_interpolate(int gl, Lane<W> &R, double *X, const Consts
 struct GlotIn { double fl[6], fr[6], rel[4]; };
 struct GlotRes { GlotOut go; double gp[6], rel[4]; };
 
-AFS_HD inline GlotIn glottis_inputs(const double *X) {
+AFS_HD inline GlotIn glottis_inputs(const double *X, int relx = X_RELX) {
   GlotIn in;
   for (int k = 0; k < 6; ++k) {
     in.fl[k] = X[X_FRAME + 4 + k];
     in.fr[k] = X[X_FRAME + 10 + k];
   }
-  for (int k = 0; k < 4; ++k) in.rel[k] = X[X_RELX + k];
+  for (int k = 0; k < 4; ++k) in.rel[k] = X[relx + k];
   return in;
 }
 
@@ -857,9 +875,9 @@ AFS_HD inline GlotRes glottis_eval_split(const GlotIn &in, const CT &C, double r
 
 // The glottis state of the sample: new displacements, interpolated controls (X_GP + 1, the lung
 // pressure, is the row phase's source term of section 0).
-AFS_HD inline void glottis_commit(double *X, const GlotRes &r) {
+AFS_HD inline void glottis_commit(double *X, const GlotRes &r, int relx = X_RELX) {
   for (int k = 0; k < 6; ++k) X[X_GP + k] = r.gp[k];
-  for (int k = 0; k < 4; ++k) X[X_RELX + k] = r.rel[k];
+  for (int k = 0; k < 4; ++k) X[relx + k] = r.rel[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -876,7 +894,7 @@ AFS_HD inline double static_beta(const Lane<W> &R, int j, const Uni &U, const Co
   return U.opt.soft_walls ? v : 0.0;
 }
 
-template <int W, bool VARLOSS>
+template <int W, bool VARLOSS, int ROLE = ROLE_ALL>
 AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, const Consts &C, const GlotOut &go) {
   // One branch-free block over the lane's slots (absent slots compute on a valid section and
   // store into the sinks), so that the scheduler interleaves the slots' reciprocal and square
@@ -887,6 +905,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
 #pragma unroll
   for (int j = 0; j < S::NST; ++j) {
     const int jj = S::ND + j;
+    if (!role_slot<ROLE>(jj, S::ND)) continue;
     const int s0 = static_section(W, j, gl);
     const int s = s0 < 0 ? 0 : s0;
     const double E = C.stat[static_index(s)][ST_E];
@@ -898,6 +917,7 @@ AFS_HD inline void phase_network(int gl, Lane<W> &R, double *X, const Uni &U, co
   // previous solution, the areas the glottis values), so every lane computes them inside the
   // block and slot 0 of lane 0 adds them; only lane 0 stores the separation state (the others
   // store into a sink).  The variable (Fulcher) loss keeps its lane-0 block after the loop.
+  if constexpr (ROLE == ROLE_STAT) return;  // (the rest: the dynamic slots)
   double dR0g = 0.0, dR1g = 0.0;
   bool on0 = false, on1 = false;
   if constexpr (!VARLOSS) {
@@ -1421,7 +1441,7 @@ AFS_HD inline void load_sec_recs(int gl, const Consts &C, SecRec *rec) {
   }
 }
 
-template <int W>
+template <int W, int ROLE = ROLE_ALL>
 AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, double *__restrict__ Xw,
                               const Uni &U, const Consts &C) {
   // X (reads) and Xw (writes) are the same utterance block; the phase writes only the
@@ -1441,6 +1461,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
   double xla[S::NSL], xra[S::NSL], xea[S::NSL], xda[S::NSL], xsx[S::NSL], xub[S::NSL], xurb[S::NSL], xrad[S::NSL];
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
+    if (!role_slot<ROLE>(j, S::ND)) continue;
     const SecRec &q = rec[j];
     // (the source's L, R1 and E sit at fixed distances in the dynamic arrays: one address)
     xla[j] = xat(X, q.x_la);
@@ -1454,6 +1475,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
   }
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
+    if (!role_slot<ROLE>(j, S::ND)) continue;
     const bool dyn = j < S::ND;
     const int s0 = slot_section<W>(j, gl);
     const int s = s0 < 0 ? (dyn ? DYN0 : 0) : s0;
@@ -1500,6 +1522,7 @@ AFS_HD inline void phase_rows(int gl, Lane<W> &R, const double *__restrict__ X, 
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
     if (j != J64 && j != J83) continue;  // (no other slot holds a radiation section)
+    if (!role_slot<ROLE>(j, S::ND)) continue;
     if (!(rec[j].flags & SR_RADIATION)) continue;
     // radiation rows of s = 64 / 83 (TdsModel.cpp:1841-1911)
     const bool dyn = j < S::ND;
@@ -1686,10 +1709,154 @@ AFS_HD inline void arm_back(const ArmRec &rr, const ArmJunction &J, bool junctio
   xat(X, junction ? J.u[2] : sink) = a.xj[2];
 }
 
-template <int W, class Xc>
+// The same walk and back substitution with the loads issued two positions ahead instead of all
+// ahead (wave pairs, sample_step_pair: the pair's kernel must fit 256 registers).  The record's
+// offsets come into registers first (no LDS round trip for an address on the chain), and every
+// value is computed by the same operations in the same order as arm_walk / arm_back: a fold's terms
+// on positions q, q + 1 (its part on q -- pivot, rhs and the edge q - q+1 -- before the walk's step
+// q - 1 updates position q, its part on q + 1 before step q), so the factors and solutions are
+// bitwise theirs.  (A value loaded ahead of an earlier position's store is one that store cannot
+// change: the stores go to the lane's own slots, or as constants into the shared dummy slots --
+// arm_walk loads everything before any store.)
+struct ArmRaw {  // position q's pivot, rhs, edge q - q+1; the fold at q's pivot, rhs, edges
+  double D, Y, E, dl, yl, l0, l1;
+};
+AFS_HD constexpr int arm_fold_at(int q) { return q == 2 ? 0 : q == 3 ? 1 : q == 5 ? 2 : q == 6 ? 3 : -1; }
+static_assert(ARM_FOLDS == 4, "fold positions 2, 3, 5, 6 (arm_fold_pos)");
+AFS_HD inline ArmRaw arm_raw(const ArmRec &r, const double *X, int q) {
+  ArmRaw v{0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  if (q >= ARM_P) return v;
+  v.D = xat(X, r.d[q]);
+  v.Y = xat(X, r.d[q] + RHS_DELTA);
+  v.E = q < ARM_P - 1 ? xat(X, r.e[q]) : 0.0;
+  const int f = arm_fold_at(q);
+  if (f >= 0) {
+    v.dl = xat(X, r.ld[f]);
+    v.yl = xat(X, r.ld[f] + RHS_DELTA);
+    v.l0 = xat(X, r.le0[f]);
+    v.l1 = xat(X, r.le1[f]);
+  }
+  return v;
+}
+#ifndef AFS_ARM_AHEAD
+#define AFS_ARM_AHEAD 2  // positions the lean walk / back substitution load ahead (1 or 2)
+#endif
+AFS_HD inline void arm_walk_lean(const ArmRec &rr, double *X, ArmCarry &a) {
+  const ArmRec r = rr;
+  bool neg = false;
+  double il[ARM_FOLDS], f1v[ARM_FOLDS], ylv[ARM_FOLDS], l1v[ARM_FOLDS];
+  const double ea = xat(X, r.ea);
+  a.e28 = xat(X, r.fx0);
+  a.e29 = xat(X, r.fx1);
+  a.ej = xat(X, r.ej);
+  ArmRaw c = arm_raw(r, X, 0), n1 = AFS_ARM_AHEAD >= 2 ? arm_raw(r, X, 1) : ArmRaw{};
+  double Dc = c.D, Yc = c.Y, Ec = c.E;
+  double F = 0.0, dA = 0.0, yA = 0.0;
+#pragma unroll
+  for (int p = 0; p < ARM_P - 1; ++p) {
+    if (AFS_ARM_AHEAD < 2) n1 = arm_raw(r, X, p + 1);
+    const ArmRaw n2 = AFS_ARM_AHEAD >= 2 ? arm_raw(r, X, p + 2) : ArmRaw{};
+    double Dn = n1.D, Yn = n1.Y, En = n1.E;
+    const int fp = arm_fold_at(p), fn = arm_fold_at(p + 1);
+    if (fp >= 0) {  // the fold at p: its part on p + 1
+      Dn = fma(-f1v[fp], l1v[fp], Dn);
+      Yn = fma(-f1v[fp], ylv[fp], Yn);
+    }
+    if (fn >= 0) {  // the fold at p + 1: its part on p + 1
+      il[fn] = pivot_recip(n1.dl);
+      neg = neg | (n1.dl < 0.0);
+      const double f0 = n1.l0 * il[fn];
+      f1v[fn] = n1.l1 * il[fn];
+      ylv[fn] = n1.yl;
+      l1v[fn] = n1.l1;
+      Dn = fma(-f0, n1.l0, Dn);
+      Yn = fma(-f0, n1.yl, Yn);
+      En = fma(-f0, n1.l1, En);
+    }
+    if (p <= ARM_START_MAX) F = (p == (int)r.start) ? ea : F;
+    const double e2 = Ec * Ec;
+    const double inv = pivot_recip(Dc);
+    neg = neg | (Dc < 0.0);
+    const double g = F * inv, h = Ec * inv;
+    dA = fma(-g, F, dA);
+    yA = fma(-g, Yc, yA);
+    Dn = fma(-e2, inv, Dn);
+    Yn = fma(-h, Yc, Yn);
+    xat(X, r.d[p] + RHS_DELTA) = Yc * inv;
+    xat(X, r.u[p]) = g;
+    xat(X, r.e[p]) = h;
+    F = -(g * Ec);
+    Dc = Dn;
+    Yc = Yn;
+    Ec = En;
+    n1 = n2;
+  }
+#pragma unroll
+  for (int f = 0; f < ARM_FOLDS; ++f) xat(X, r.ld[f]) = il[f];
+  const bool in = (r.flags & ARM_IN) != 0, end = (r.flags & ARM_END) != 0;
+  a.sf = in ? (int)r.idx : -1;
+  a.sb = (in && !end) ? (int)r.idx : -1;
+  a.end = end ? 1 : 0;
+  a.F = ((int)r.start == ARM_P - 1) ? ea : F;
+  a.Db = Dc;
+  a.Yb = Yc;
+  a.dA = dA;
+  a.yA = yA;
+  a.neg = neg;
+}
+
+struct ArmRawB {  // position p's rhs, fill edge, edge p - p+1; the fold at p's pivot reciprocal, rhs, edges
+  double y, Fp, Ep, il, yl, l0, l1;
+};
+AFS_HD inline ArmRawB arm_raw_back(const ArmRec &r, const double *X, int p) {
+  ArmRawB v{0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  if (p < 0) return v;
+  v.y = xat(X, r.d[p] + RHS_DELTA);
+  v.Fp = xat(X, r.u[p]);
+  v.Ep = xat(X, r.e[p]);
+  const int f = arm_fold_at(p);
+  if (f >= 0) {
+    v.il = xat(X, r.ld[f]);
+    v.yl = xat(X, r.ld[f] + RHS_DELTA);
+    v.l0 = xat(X, r.le0[f]);
+    v.l1 = xat(X, r.le1[f]);
+  }
+  return v;
+}
+AFS_HD inline void arm_back_lean(const ArmRec &rr, const ArmJunction &J, bool junction, double *X, const ArmCarry &a,
+                                 double xA) {
+  static_assert(AFS_WALK_PRESCALED && AFS_BACK_SCALED, "the lean back substitution is the prescaled, scaled form");
+  const ArmRec r = rr;
+  double xn = a.x;  // x_{p+1}
+  ArmRawB q1 = arm_raw_back(r, X, ARM_P - 2), q2 = AFS_ARM_AHEAD >= 2 ? arm_raw_back(r, X, ARM_P - 3) : ArmRawB{};
+  xat(X, r.u[ARM_P - 1]) = xn;
+#pragma unroll
+  for (int p = ARM_P - 2; p >= 0; --p) {
+    const ArmRawB q3 = AFS_ARM_AHEAD >= 2 ? arm_raw_back(r, X, p - 2) : arm_raw_back(r, X, p - 1);
+    const double c = fma(-q1.Fp, xA, q1.y), e = -q1.Ep;
+    const double xp = fma(e, xn, c);
+    xat(X, r.u[p]) = xp;
+    const int f = arm_fold_at(p);
+    if (f >= 0) xat(X, r.lu[f]) = fma(-q1.l1, xn, fma(-q1.l0, xp, q1.yl)) * q1.il;
+    xn = xp;
+    if (AFS_ARM_AHEAD >= 2) {
+      q1 = q2;
+      q2 = q3;
+    } else {
+      q1 = q3;
+    }
+  }
+  const uint32_t sink = (uint32_t)(X_U + U_SINK) * 8u;
+  xat(X, junction ? J.u[0] : sink) = a.xj[0];
+  xat(X, junction ? J.u[1] : sink) = a.xj[1];
+  xat(X, junction ? J.u[2] : sink) = a.xj[2];
+}
+
+template <int W, class Xc, bool LEAN = false>
 AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
   static_assert(TREE_CHAINS == 16, "the arm partition has 16 lanes (one DPP row)");
-  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_walk(C.arm[k], X, R.ac); });
+  if constexpr (LEAN) x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_walk_lean(C.arm[k], X, R.ac); });
+  else x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_walk(C.arm[k], X, R.ac); });
   // the junction triangle's values (every lane loads them; only the junction lane's matter)
   x.lanes(TREE_CHAINS, [&](int, Lane<W> &R) {
     const ArmJunction &J = C.armj;
@@ -1925,7 +2092,10 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
   // every lane's segment from its boundary and its anchor (lane k-1's boundary)
   x.template pull<-1, 1>([&](int, Lane<W> &R) { return D4{{R.ac.x, 0.0, 0.0, 0.0}}; },
                          [&](int, Lane<W> &R, const D4 &v) { R.ac.xJ = v.v[0]; });
-  x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_back(C.arm[k], C.armj, k == ARM_JUNCTION, X, R.ac, R.ac.xJ); });
+  if constexpr (LEAN)
+    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_back_lean(C.arm[k], C.armj, k == ARM_JUNCTION, X, R.ac, R.ac.xJ); });
+  else
+    x.lanes(TREE_CHAINS, [&](int k, Lane<W> &R) { arm_back(C.arm[k], C.armj, k == ARM_JUNCTION, X, R.ac, R.ac.xJ); });
   x.sync();
   x.mark(PH_BACKWARD);
 }
@@ -1933,7 +2103,7 @@ AFS_HD inline void solve_arms(Xc &x, double *X, const Consts &C) {
 // ---------------------------------------------------------------------------
 // Phase U: updateVariables (TdsModel.cpp:2046-2098).
 // ---------------------------------------------------------------------------
-template <int W>
+template <int W, int ROLE = ROLE_ALL>
 AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X, double *__restrict__ Xw,
                                 const Uni &U, const Consts &C) {
   // X (reads) and Xw (writes) are the same utterance block; the phase publishes into X_UR,
@@ -1948,6 +2118,7 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
   double unew[S::NSL], cout[S::NSL], Ds[S::NSL], Es[S::NSL];
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
+    if (!role_slot<ROLE>(j, S::ND)) continue;
     const int s0 = slot_section<W>(j, gl);
     const int s = s0 < 0 ? (j < S::ND ? DYN0 : 0) : s0;
     unew[j] = X[X_U + s];
@@ -1959,6 +2130,7 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
   }
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
+    if (!role_slot<ROLE>(j, S::ND)) continue;
     const int s0 = slot_section<W>(j, gl);
     const int s = s0 < 0 ? (j < S::ND ? DYN0 : 0) : s0;
     double alpha, beta;
@@ -1987,12 +2159,14 @@ AFS_HD inline void phase_update(int gl, Lane<W> &R, const double *__restrict__ X
   // publish (all stores after all loads: the scheduler may batch the loads of every slot)
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
+    if (!role_slot<ROLE>(j, S::ND)) continue;
     xat(Xw, rec[j].x_ur) = R.ur[j];  // for the bifurcation partner (or the sink)
     xat(Xw, rec[j].x_un) = R.un[j];  // for the noise sources (or the sink)
     xat(Xw, rec[j].x_p4) = R.p[j];   // p[22..25] for the glottis (or the sink)
   }
 #pragma unroll
   for (int j = 0; j < S::NSL; ++j) {
+    if (!role_slot<ROLE>(j, S::ND)) continue;
     const int s = slot_section<W>(j, gl);
     // transvelar filter inputs p[43], p[67]: only the slots that can hold sections 43 / 67
     // store, a lane without them into the sink (no branch)
@@ -2303,6 +2477,155 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
   x.mark(PH_OUTPUT);
 }
 
+
+// One sample on a wave pair (tree_kernel.h, AFS_PAIR): the wave of role ROLE runs its half of the
+// phases; the pair's waves meet at a workgroup barrier (x.bar()) between the four phase groups, so
+// LDS carries everything one wave writes and the other reads (the dynamic slots' L, R, E, D and the
+// static slots' D, the dipole samples, the rows, the solution, the published pressures and flows).
+//   P1  DYN: interpolation, the glottis (its areas for the network), the dynamic slots' network
+//       STAT: the glottis and its commit, the static slots' D, targets, noise
+//   P2  rows of each role's slots
+//   P3  STAT: the arm solver (lean form) and the rand() blocks ahead
+//   P4  the state update of each role's slots; DYN: the radiated flow (R.sample)
+// Both waves read the glottis displacements at the start of P1 and STAT commits the new ones in P1:
+// two buffers, sample parity par reads X_RELX (par 0) or X_RELX2 and writes the other.
+#if AFS_PAIR
+#ifndef AFS_PAIR_LEAN
+#define AFS_PAIR_LEAN 1  // the STAT wave's solver in the lean form (arm_walk_lean; 0: arm_walk, every load ahead)
+#endif
+#ifndef AFS_PAIR_RNG_DYN
+#define AFS_PAIR_RNG_DYN 1  // the rand() blocks ahead on the DYN wave during the solver (0: on the STAT wave after it)
+#endif
+template <int W, int MODEL, int NZ, int ROLE, bool VARLOSS, class Xc>
+AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Consts &C, double ratio, int par) {
+  static_assert(ROLE == ROLE_DYN || ROLE == ROLE_STAT, "a wave pair's roles");
+// (scheduling barriers between the phase groups: the scheduler otherwise mixes their code and keeps
+// values of both live at once -- the pair kernel must fit 256 registers; with AFS_PAIR_MARKS named
+// markers in the assembly instead, for spill accounting)
+#if defined(AFS_PAIR_MARKS) && defined(__HIP_DEVICE_COMPILE__)
+#define AFS_PM(t) __asm__ volatile(t)
+#else
+#define AFS_PM(t) AFS_SCHED_BARRIER()
+#endif
+  AFS_PM(";MARK P1 begin");
+  const int rcur = par ? X_RELX2 : X_RELX, rnext = par ? X_RELX : X_RELX2;
+  if constexpr (ROLE == ROLE_DYN) {
+    GlotRes g{};
+    x.par_uniform([&](int gl, Lane<W> &R) { phase_interpolate<W>(gl, R, X, C, ratio); },
+                  [&](Lane<W> &R) {
+                    (void)R;
+                    const double p4[4] = {X[X_P4 + 0], X[X_P4 + 1], X[X_P4 + 2], X[X_P4 + 3]};
+                    if constexpr (Xc::kGlottisSplit && MODEL == AFS_GLOTTIS_TRIANGULAR)
+                      g = glottis_eval_split(glottis_inputs(X, rcur), C, ratio, p4, x.half8(),
+                                             [&](double v) { return x.xch8(v); });
+                    else
+                      g = glottis_eval<MODEL>(glottis_inputs(X, rcur), C, ratio, p4);
+                  });
+    x.dyn_neighbors();
+    x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS, ROLE_DYN>(gl, R, X, U, C, g.go); });
+    x.mark(PH_NETWORK);
+  } else {
+    double a_glot_up = 0.0;
+    x.par_uniform([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS, ROLE_STAT>(gl, R, X, U, C, GlotOut{}); },
+                  [&](Lane<W> &R) {
+                    (void)R;
+                    const double p4[4] = {X[X_P4 + 0], X[X_P4 + 1], X[X_P4 + 2], X[X_P4 + 3]};
+                    GlotRes g;
+                    if constexpr (Xc::kGlottisSplit && MODEL == AFS_GLOTTIS_TRIANGULAR)
+                      g = glottis_eval_split(glottis_inputs(X, rcur), C, ratio, p4, x.half8(),
+                                             [&](double v) { return x.xch8(v); });
+                    else
+                      g = glottis_eval<MODEL>(glottis_inputs(X, rcur), C, ratio, p4);
+                    glottis_commit(X, g, rnext);
+                    a_glot_up = g.go.a1;
+                  });
+    AFS_PM(";MARK targets");
+#if !defined(AFS_PAIR_PROBE_NONOISE)
+#if AFS_PAIR_RNG_DYN
+    x.par([&](int gl, Lane<W> &R) {  // (the ring's head and pending count, which the DYN wave's rng_ahead moved)
+      (void)gl;
+      const int32_t *hp = (const int32_t *)(X + X_RNGHP);
+      R.rhead = hp[0];
+      R.rpend = hp[1];
+    });
+#endif
+    x.par([&](int gl, Lane<W> &R) { phase_targets<W, NZ>(x, gl, R, X, C, a_glot_up); });
+    x.sync();
+    AFS_PM(";MARK noise");
+    if (U.opt.generate_noise_sources) {
+      phase_noise<W, NZ>(x, X, U, C);
+    } else {
+      x.par([&](int gl, Lane<W> &R) {
+        (void)R;
+        for (int d = gl; d < NDIP; d += W) X[X_SMP + d] = 0.0;
+      });
+    }
+#if AFS_PAIR_RNG_DYN
+    x.par([&](int gl, Lane<W> &R) {
+      if (gl == 0) {
+        int32_t *hp = (int32_t *)(X + X_RNGHP);
+        hp[0] = R.rhead;
+        hp[1] = R.rpend;
+      }
+    });
+#endif
+#endif
+    x.mark(PH_NOISE);
+  }
+  x.bar();
+  x.mark(PH_P1WAIT);
+  AFS_PM(";MARK rows");
+  x.par([&](int gl, Lane<W> &R) { phase_rows<W, ROLE>(gl, R, X, X, U, C); });
+  x.mark(PH_ROWS);
+  x.bar();
+  x.mark(PH_P2WAIT);
+  AFS_PM(";MARK solver");
+  if constexpr (ROLE == ROLE_STAT) {
+#if !defined(AFS_PAIR_PROBE_NOSOLVE)
+    solve_arms<W, Xc, AFS_PAIR_LEAN != 0>(x, X, C);
+#endif
+    AFS_PM(";MARK rng");
+#if !defined(AFS_PAIR_PROBE_NORNG) && !AFS_PAIR_RNG_DYN
+    rng_ahead<W>(x, X);
+#endif
+  }
+#if AFS_PAIR_RNG_DYN
+  if constexpr (ROLE == ROLE_DYN) {  // the rand() blocks ahead on the DYN wave, beside the solver
+    x.par([&](int gl, Lane<W> &R) {
+      (void)gl;
+      const int32_t *hp = (const int32_t *)(X + X_RNGHP);
+      R.rhead = hp[0];
+      R.rpend = hp[1];
+    });
+    rng_ahead<W>(x, X);
+    x.par([&](int gl, Lane<W> &R) {
+      if (gl == 0) {
+        int32_t *hp = (int32_t *)(X + X_RNGHP);
+        hp[0] = R.rhead;
+        hp[1] = R.rpend;
+      }
+    });
+    x.mark(PH_RNGP);
+  }
+#endif
+  x.bar();
+  x.mark(PH_P3WAIT);
+  AFS_PM(";MARK update");
+  if constexpr (ROLE == ROLE_DYN)
+    x.par_uniform([&](int gl, Lane<W> &R) { phase_update<W, ROLE>(gl, R, X, X, U, C); },
+                  [&](Lane<W> &R) { R.sample = phase_output_flow(X); });
+  else
+    x.par([&](int gl, Lane<W> &R) { phase_update<W, ROLE>(gl, R, X, X, U, C); });
+  x.mark(PH_UPDATE);
+  x.bar();
+  x.mark(PH_P4WAIT);
+}
+template <int W, int MODEL, int NZ, int ROLE, class Xc>
+AFS_HD inline void sample_step_pair(Xc &x, double *X, const Uni &U, const Consts &C, double ratio, int par) {
+  if (U.opt.glottis_loss == AFS_ENTRANCE_LOSS_VARIABLE) sample_step_pair_v<W, MODEL, NZ, ROLE, true>(x, X, U, C, ratio, par);
+  else sample_step_pair_v<W, MODEL, NZ, ROLE, false>(x, X, U, C, ratio, par);
+}
+#endif
 
 }  // namespace tree
 }  // namespace afs

@@ -43,7 +43,10 @@ constexpr int WPB = Geom<TW>::WPB;
 constexpr int UPB = Geom<TW>::UPB;
 static_assert(UPB == TREE_UPB, "afs_tree.h TREE_UPB: the host's slot orders group utterances by block");
 
-template <bool PROF, int W = TW>
+#ifndef AFS_PAIR_MARK_SB
+#define AFS_PAIR_MARK_SB 1  // the pair kernel: a scheduling barrier at every phase mark (A/B)
+#endif
+template <bool PROF, int W = TW, bool MARK_SB = false>
 struct GpuExec {
   static constexpr bool kToneOut = AFS_TONE_K6 != 0;  // the tone filter in K6 from the stored p[25] (afs_tree.h)
   static constexpr bool kGlottisSplit = true;   // the glottis' masses on the two lane halves (+1.1 %, r03ag_ab.txt)
@@ -65,6 +68,14 @@ struct GpuExec {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // the wave pairs' barrier (AFS_PAIR): every wave of the workgroup, LDS visible across them
+  // (scheduling barriers around it: the scheduler does not mix the phases' code, which would keep
+  // both phases' values live at once -- the pair kernel must fit 256 registers)
+  __device__ __forceinline__ void bar() {
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
   }
   // Bit gl of the result: f(gl, R) of this utterance's lane gl.
   template <class F> __device__ __forceinline__ uint64_t ballot(F f) {
@@ -179,11 +190,16 @@ struct GpuExec {
     const int hi = AFS_DPP((int)(uint32_t)(v >> 32), 0x150 + K, 0xF, 0xF, false);
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
   }
+  // (MARK_SB, the wave pairs: a scheduling barrier at each phase mark -- the scheduler otherwise
+  // hoists a phase's loads into the one before and the pair kernel spills)
   __device__ __forceinline__ void mark(int ph) {
     if constexpr (PROF) {
       uint64_t t = __builtin_amdgcn_s_memtime();
       acc[ph] += t - last;
       last = t;
+    } else if constexpr (MARK_SB) {
+      (void)ph;
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 };
@@ -205,9 +221,12 @@ using WaveLds = WaveLdsT<TW>;
 // copy: tree_synth_body) has live ranges of its own: with the branch between time loops instead,
 // the register allocator spilled 160-250 VGPRs of the persistent state to scratch.
 template <int W>
-__device__ __forceinline__ int noise_variant(const TreeArgs &a) {
+__device__ __forceinline__ int noise_variant(const TreeArgs &a, int g = -1, int gl = -1) {
   constexpr int UPB_ = Geom<W>::UPB;
-  const int lane = threadIdx.x, g = lane / W, gl = lane % W;
+  if (g < 0) {
+    g = (int)threadIdx.x / W;
+    gl = (int)threadIdx.x % W;
+  }
   const int slot = blockIdx.x * UPB_ + g;
   const int u = a.order ? a.order[slot] : slot;
   const int ue = u < a.B ? u : 0;  // (a padding slot runs utterance 0's data and stores nothing)
@@ -465,6 +484,271 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
     tree_synth_run<PROF, MODEL, HOPS, W, NZ_FULL>(a, lds, prof);
   }
 }
+
+// ---------------------------------------------------------------------------
+// Wave pairs (AFS_PAIR = 1, an A/B build): a workgroup of four waves for the same eight utterances
+// -- waves 0 and 1 take the dynamic slots of utterances 0-3 / 4-7 (ROLE_DYN), waves 2 and 3 their
+// static slots and the lane-uniform phases (ROLE_STAT) -- and two workgroups per CU: two waves per
+// SIMD, whose instructions the SIMD interleaves (a wave alone issues one VALU instruction per 4
+// cycles; the SIMD executes one per 2, tree_core.h sample_step_pair).  Each wave holds half the
+// slots' state, so the pair's kernel must fit 256 registers per lane.
+// ---------------------------------------------------------------------------
+#if AFS_PAIR
+template <int MODEL, bool HOPS, int NZ, int ROLE, bool PROF = false>
+__device__ __forceinline__ void tree_pair_run(const TreeArgs &a, WaveLdsT<TW> &lds, int grp, uint64_t *prof = nullptr) {
+  constexpr int W = TW, UPB_ = Geom<W>::UPB;
+  using S = Shape<W>;
+  const int lane = threadIdx.x;  // 0 .. 255
+  const int g = grp * Geom<W>::UPW + (lane % 64) / W, gl = lane % W;
+  const int slot = blockIdx.x * UPB_ + g;
+  const int u = a.order ? a.order[slot] : slot;
+  const bool valid = u < a.B;
+  const int ue = valid ? u : 0;
+  double *X = lds.X[g];
+  const Tables &T = *a.tab;
+  {
+    const uint64_t *src = (const uint64_t *)&T.consts;
+    uint64_t *dst = (uint64_t *)&lds.C;
+    for (int k = lane; k < (int)(sizeof(Consts) / 8); k += 256) dst[k] = src[k];
+  }
+  Lane<W> R = ((const Lane<W> *)a.lane_state)[(int64_t)ue * W + gl];
+  const double *ls = a.lds_state + (int64_t)ue * X_TOTAL;
+  if constexpr (ROLE == ROLE_DYN)
+    for (int k = gl; k < X_TOTAL; k += W) X[k] = ls[k];
+  __syncthreads();
+  const Consts &C = lds.C;
+  GpuExec<PROF, W, AFS_PAIR_MARK_SB != 0> ex{gl, &R};
+  const int64_t row = a.frame_row ? a.frame_row[ue] : ue;
+  const afs_frame *fu = a.frames + row * a.frame_stride;
+  double *o = a.out + (int64_t)ue * a.out_stride;
+  double *p25o = a.p25 + (int64_t)ue * a.p25_stride;
+  const uint64_t *pl = a.plan + row * a.plan_stride * PLAN_WORDS + (gl & (PLAN_WORDS - 1));
+  const int hop = a.hop;
+  const int64_t n = a.s_end - a.s_begin;
+  int k = (int)(a.s_begin / hop) + 1, i = (int)(a.s_begin % hop);
+  if constexpr (ROLE == ROLE_DYN) frame_load<W>(gl, R, X, fu + (k - 1), fu + k);
+  const PlanHop *hr = HOPS ? a.hops + row * a.hop_stride : nullptr;
+  double hp[4] = {0.0, 0.0, 0.0, 0.0};
+  uint32_t hkind = PK_CONST;
+  bool hmixed = !HOPS;
+  const uint64_t *pd = nullptr;
+  auto hop_load = [&](const PlanHop *h) {
+    const double2 *q = reinterpret_cast<const double2 *>(h->p[gl & (PLAN_WORDS - 1)]);
+    const double2 v0 = q[0], v1 = q[1];
+    hp[0] = v0.x; hp[1] = v0.y; hp[2] = v1.x; hp[3] = v1.y;
+    hkind = h->kind[gl & (PLAN_WORDS - 1)];
+    hmixed = h->mixed != 0;
+    pd = a.plan + (int64_t)h->dense * hop * PLAN_WORDS + (gl & (PLAN_WORDS - 1));
+  };
+  if constexpr (HOPS && ROLE == ROLE_STAT) hop_load(hr);
+  NextFrame<W> nf{};
+  const int o_line = (int)((reinterpret_cast<uintptr_t>(o) >> 3) & 15);
+  double wo = 0.0, wp = 0.0;
+  const double dhop = (double)hop, inv_hop = 1.0 / dhop;
+#if AFS_PAIR_RNG_DYN
+  if constexpr (ROLE == ROLE_STAT) {  // (the ring's head and pending count from the saved lane state)
+    if (gl == 0) {
+      int32_t *hp = (int32_t *)(X + X_RNGHP);
+      hp[0] = R.rhead;
+      hp[1] = R.rpend;
+    }
+  }
+#endif
+  __syncthreads();  // (the LDS image and X_FRAME in place for both roles)
+  uint64_t next = 0;
+  if constexpr (ROLE == ROLE_STAT) next = hmixed ? (HOPS ? pd[i * PLAN_WORDS] : pl[0]) : 0;
+  uint64_t t_begin = 0;
+  if constexpr (PROF) t_begin = ex.last = __builtin_amdgcn_s_memtime();
+  for (int64_t t = 0; t < n; ++t) {
+    const double ratio = hop_ratio(i, dhop, inv_hop);
+    const int64_t tn = t + 1 < n ? t + 1 : t;
+    if constexpr (ROLE == ROLE_STAT) {
+      if constexpr (HOPS) {
+        const uint64_t ev = plan_word_fast(hkind, hp, ratio);
+        R.planw = hmixed ? next : ev;
+        next = *(hmixed ? pd + (i + 1 < hop ? i + 1 : i) * PLAN_WORDS : reinterpret_cast<const uint64_t *>(hr));
+      } else {
+        R.planw = next;
+        next = pl[tn * PLAN_WORDS];
+      }
+    } else if constexpr (!HOPS) {
+      if (i + 1 == hop && t + 1 < n) nf.load(gl, fu + k + 1);
+    }
+    sample_step_pair<W, MODEL, NZ, ROLE>(ex, X, a.uni, C, ratio, (int)(t & 1));
+    if constexpr (ROLE == ROLE_DYN) {
+      const int j = (o_line + (int)t) & 15;
+      const double p25v = GpuExec<false, W>::template dpp<0x152>(R.p[0]);
+      const bool mine = gl == j;
+      wo = mine ? R.sample : wo;
+      wp = mine ? p25v : wp;
+      if (valid && (j == 15 || t + 1 == n) && gl <= j && t - j + gl >= 0) {
+        o[t - j + gl] = wo;
+        if constexpr (AFS_TONE_K6 == 1) p25o[t - j + gl] = wp;
+      }
+    }
+    if (++i == hop) {
+      i = 0;
+      ++k;
+      if (t + 1 < n) {
+        if constexpr (ROLE == ROLE_DYN) {
+          if constexpr (HOPS) {
+            NextFrame<W> f{};
+            f.load(gl, fu + k);
+            frame_shift<W>(gl, R, X, f);
+          } else {
+            frame_shift<W>(gl, R, X, nf);
+          }
+        } else if constexpr (HOPS) {
+          hop_load(++hr);
+          if (hmixed) next = pd[0];
+        }
+      }
+      ex.bar();
+    }
+    ex.mark(PH_TAIL);
+  }
+  if constexpr (PROF) {
+    // (the slots no pair phase uses: the wave's placement -- HW_ID, XCC_ID -- and its loop's span)
+    ex.acc[PH_GEOMETRY] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                          ((uint64_t)(__builtin_amdgcn_s_getreg((15 << 11) | 20) & 15) << 32);
+    ex.acc[PH_OUTPUT] = t_begin;
+    ex.acc[PH_TARGETS] = __builtin_amdgcn_s_memtime();
+    if (lane % 64 == 0)
+      for (int q = 0; q < PH_COUNT; ++q) prof[((int64_t)blockIdx.x * 4 + lane / 64) * PH_COUNT + q] = ex.acc[q];
+  }
+  if constexpr (ROLE == ROLE_DYN) {  // (the displacements of the last sample into X_RELX, the image's slot)
+    if (n & 1) {
+      if (gl < 4) X[X_RELX + gl] = X[X_RELX2 + gl];
+    }
+  }
+  __syncthreads();
+  if (valid) {
+    Lane<W> *dst = (Lane<W> *)a.lane_state + (int64_t)u * W + gl;
+#pragma unroll
+    for (int j = 0; j < S::NSL; ++j) {
+      if (!role_slot<ROLE>(j, S::ND)) continue;
+      dst->p[j] = R.p[j]; dst->pr[j] = R.pr[j]; dst->w[j] = R.w[j]; dst->wr[j] = R.wr[j];
+      dst->wr2[j] = R.wr2[j]; dst->u[j] = R.u[j]; dst->ur[j] = R.ur[j]; dst->un[j] = R.un[j];
+    }
+    if constexpr (ROLE == ROLE_DYN) {
+#pragma unroll
+      for (int j = 0; j < S::ND; ++j) {
+        dst->aL[j] = R.aL[j]; dst->aR[j] = R.aR[j]; dst->lL[j] = R.lL[j]; dst->lR[j] = R.lR[j];
+        dst->al[j] = R.al[j]; dst->be[j] = R.be[j];
+      }
+      double *ws = a.lds_state + (int64_t)u * X_TOTAL;
+      for (int q = gl; q < X_TOTAL; q += W) ws[q] = X[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < S::NDP; ++q) {
+        dst->damp[q] = R.damp[q]; dst->dout[q] = R.dout[q]; dst->dcut[q] = R.dcut[q]; dst->racc[q] = R.racc[q];
+      }
+#if AFS_PAIR_RNG_DYN
+      const int32_t *hp = (const int32_t *)(X + X_RNGHP);
+      dst->rhead = hp[0];
+      dst->rpend = hp[1];
+#else
+      dst->rhead = R.rhead;
+      dst->rpend = R.rpend;
+#endif
+    }
+  }
+}
+
+// The two workgroups a compute unit holds at a time (AFS_PAIR_MAP 3): each claims one of two slots
+// in its CU's word (global atomics; released when the workgroup ends).
+__device__ unsigned int pair_cu_slots[2048];
+
+// Roles: two groups of four utterances; in each group one wave is DYN and one STAT.  The SIMD a wave
+// runs on decides (AFS_PAIR_MAP 3), so that each SIMD runs one DYN and one STAT wave of its CU's two
+// workgroups -- STAT carries the targets, noise and solver, the longer half: two STAT waves on one
+// SIMD would share its issue slots.  When a workgroup's four waves do not sit on four SIMDs, or
+// under the other maps, by the wave index (0: waves 0, 1 DYN; 1: a slot parity read from
+// HW_ID.WAVE_ID; 2: the block's parity).  Any placement gives a valid pairing; this only balances
+// the SIMDs.
+template <int MODEL, bool HOPS, bool PROF = false>
+__device__ __forceinline__ void tree_pair_body(const TreeArgs &a, WaveLdsT<TW> &lds, int *pattern,
+                                               uint64_t *prof = nullptr) {
+  if (a.skip_claims && (int64_t)*a.skip_claims > a.skip_cap) return;
+  if (a.order) {
+    bool any = false;
+#pragma unroll
+    for (int g = 0; g < Geom<TW>::UPB; ++g) any |= a.order[blockIdx.x * Geom<TW>::UPB + g] < a.B;
+    if (!any) return;
+  }
+  const int wave = (int)threadIdx.x / 64;
+#ifndef AFS_PAIR_MAP
+#define AFS_PAIR_MAP 1  // 0: waves 0, 1 DYN (groups 0, 1), 2, 3 STAT; 1: by the wave slot's parity; 2: by the block's parity
+#endif
+  int grp, st;
+  unsigned int *cu_word = nullptr;
+  unsigned int cu_bit = 0;
+  if constexpr (AFS_PAIR_MAP == 0) {
+    grp = wave & 1;
+    st = wave >> 1;
+  } else if constexpr (AFS_PAIR_MAP == 3) {
+    const unsigned int hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+    const int simd = (int)((hw >> 4) & 3);
+    if (threadIdx.x % 64 == 0) pattern[1 + wave] = simd;
+    if (threadIdx.x == 0) {
+      const unsigned int xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20) & 7;  // XCC_ID
+      cu_word = pair_cu_slots + ((xcc << 8) | ((hw >> 8) & 255));              // SE, SH, CU
+      const unsigned int old = atomicOr(cu_word, 1u);
+      cu_bit = 1u;
+      if (old & 1u) {
+        const unsigned int o2 = atomicOr(cu_word, 2u);
+        cu_bit = (o2 & 2u) ? 0u : 2u;
+      }
+      pattern[0] = cu_bit == 2u;
+    }
+    __syncthreads();
+    const int m = (1 << pattern[1]) | (1 << pattern[2]) | (1 << pattern[3]) | (1 << pattern[4]);
+    if (m == 15) {
+      grp = simd & 1;
+      st = (simd >> 1) ^ pattern[0];
+    } else {
+      grp = wave & 1;
+      st = (wave >> 1) ^ pattern[0];
+    }
+  } else {
+    if (threadIdx.x == 0)
+      *pattern = AFS_PAIR_MAP == 1 ? (int)(__builtin_amdgcn_s_getreg((3 << 11) | 4) & 1)  // HW_ID.WAVE_ID bit 0
+                                   : (int)(blockIdx.x & 1);
+    __syncthreads();
+    grp = wave >> 1;
+    st = (wave & 1) ^ *pattern;
+  }
+  const bool stat = st != 0;
+#ifdef AFS_PAIR_PROBE  // (register probes: 1 compiles the DYN role alone, 2 the STAT role's NZ_FULL copy alone)
+  if constexpr (AFS_PAIR_PROBE == 1) { tree_pair_run<MODEL, HOPS, NZ_FULL, ROLE_DYN, PROF>(a, lds, grp, prof); return; }
+  if constexpr (AFS_PAIR_PROBE == 2) { tree_pair_run<MODEL, HOPS, NZ_FULL, ROLE_STAT, PROF>(a, lds, grp, prof); return; }
+#endif
+  if (!stat) {
+    tree_pair_run<MODEL, HOPS, NZ_FULL, ROLE_DYN, PROF>(a, lds, grp, prof);
+  } else if constexpr (HOPS) {
+    const int g = grp * Geom<TW>::UPW + ((int)threadIdx.x % 64) / TW, gl = (int)threadIdx.x % TW;
+    const int nz = noise_variant<TW>(a, g, gl);
+    if (false) {
+#if AFS_NZ_SET & 2
+    } else if (nz == NZ_GLOTTIS) {
+      tree_pair_run<MODEL, HOPS, NZ_GLOTTIS, ROLE_STAT, PROF>(a, lds, grp, prof);
+#endif
+#if AFS_NZ_SET & 1
+    } else if (nz == NZ_TONGUE1) {
+      tree_pair_run<MODEL, HOPS, NZ_TONGUE1, ROLE_STAT, PROF>(a, lds, grp, prof);
+#endif
+    } else {
+      tree_pair_run<MODEL, HOPS, NZ_FULL, ROLE_STAT, PROF>(a, lds, grp, prof);
+    }
+  } else {
+    tree_pair_run<MODEL, HOPS, NZ_FULL, ROLE_STAT, PROF>(a, lds, grp, prof);
+  }
+  if constexpr (AFS_PAIR_MAP == 3) {
+    if (threadIdx.x == 0 && cu_bit) atomicAnd(cu_word, ~cu_bit);  // (after the run's last workgroup barrier)
+  }
+}
+
+#endif  // AFS_PAIR
 
 }  // namespace tree
 }  // namespace afs

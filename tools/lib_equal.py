@@ -17,7 +17,8 @@ def write(path):
     from areafunctionsynthesis_amd.synthesizer import Context, Synthesizer as Session
     out = {}
     for fs in (44100.0, 22050.0):
-        ctx = Context(fs, solver="tree")
+        lanes = int(os.environ.get("AFS_EQ_LANES", "0")) or None  # (16: the throughput kernel at this small batch)
+        ctx = Context(fs, solver="tree", lanes=lanes)
         for name, gen in (("static", workloads.static_vowels), ("fricatives", workloads.fricatives)):
             w = gen(96, seconds=0.3, fs=fs)
             frames = workloads.build_frames(w, ctx.af_to_frames)
