@@ -31,7 +31,7 @@ AFS_COMM_ID_BYTES = 128
 # Every symbol include/afs.h declares.
 EXPORTED = (
     "afs_abi_version", "afs_config_default", "afs_status_string", "afs_create", "afs_destroy",
-    "afs_last_error", "afs_set_stream", "afs_lanes_per_utterance", "afs_synchronize", "afs_synthesize",
+    "afs_last_error", "afs_set_stream", "afs_lanes_per_utterance", "afs_synthesis_kernel", "afs_synchronize", "afs_synthesize",
     "afs_session_create", "afs_session_synthesize", "afs_session_reset", "afs_session_destroy",
     "afs_af_to_frames", "afs_to_int16", "afs_target_sequence_default", "afs_target_sequence_samples",
     "afs_play_target_sequences", "afs_rng_draws", "afs_noise_plans", "afs_noise_plan_hops", "afs_plan_hop_words", "afs_tube_interpolate", "afs_session_rng_draws", "afs_kernel_times",
@@ -102,6 +102,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.afs_set_stream.argtypes = [vp, vp]
     lib.afs_lanes_per_utterance.argtypes = [vp, ctypes.c_int32]
     lib.afs_lanes_per_utterance.restype = ctypes.c_int32
+    lib.afs_synthesis_kernel.argtypes = [vp, ctypes.c_int32]
+    lib.afs_synthesis_kernel.restype = ctypes.c_char_p
     lib.afs_synchronize.argtypes = [vp]
     lib.afs_synthesize.argtypes = [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp,
                                    ctypes.POINTER(AfsReport)]

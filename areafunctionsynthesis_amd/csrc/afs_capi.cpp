@@ -747,6 +747,11 @@ int32_t afs_lanes_per_utterance(const afs_ctx *c, int32_t batch) {
   return lanes_for(c, batch);
 }
 
+const char *afs_synthesis_kernel(const afs_ctx *c, int32_t batch) {
+  if (!c || c->cfg.solver != AFS_SOLVER_TREE) return "lane_synth_kernel";
+  return (AFS_PAIR && afs_lanes_per_utterance(c, batch) == afs::TREE_W) ? "tree_pair_kernel" : "tree_synth_kernel";
+}
+
 afs_status afs_kernel_times_ex(afs_ctx *c, afs_kernel_timing *t) {
   if (!c || !t) return AFS_ERR_INVALID_ARGUMENT;
   if (!(c->cfg.flags & AFS_PROFILE)) return fail(c, AFS_ERR_INVALID_ARGUMENT, "afs_kernel_times: AFS_PROFILE is off");

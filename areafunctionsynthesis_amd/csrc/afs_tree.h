@@ -87,7 +87,11 @@ inline int64_t plan_work_bytes(int64_t rows, int64_t slots) { return (rows * slo
 #define AFS_TREE_W 16
 #endif
 #ifndef AFS_PAIR
-#define AFS_PAIR 0  // 1: the throughput kernel as wave pairs (tree_kernel.h tree_pair_body; an A/B build)
+// 1: the throughput kernel as wave pairs (tree_kernel.h tree_pair_body): two waves per SIMD, the
+// phases of each four utterances split between a DYN and a STAT wave -- +8.7 % at 8192 static
+// vowels, the audio bitwise the same (profiles/r06_pair_ab.txt); 0: one wave per SIMD running every
+// phase (tree_synth_body; A/B builds)
+#define AFS_PAIR 1
 #endif
 #ifndef AFS_TONE_K6
 // 1: K1 stores section 25's pressure per sample and K6 runs the glottal-tone filter over it

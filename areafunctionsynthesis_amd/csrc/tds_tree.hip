@@ -156,7 +156,7 @@ static void launch_synth_w(const TreeArgs &a, hipStream_t st) {
   const dim3 grid(a.grid_blocks > 0 ? a.grid_blocks : (a.B + UPB_ - 1) / UPB_), block(64 * Geom<W>::WPB);
   const bool two = a.uni.opt.glottis_model == AFS_GLOTTIS_TWO_MASS;
 #if AFS_PAIR
-  if constexpr (W == TW) {
+  if constexpr (W == TW) {  // (the one-wave kernel at 16 lanes is not instantiated in this build)
     static_assert(Geom<TW>::WPB == 2, "a wave pair per four utterances: 4 waves per 8-utterance block");
     const dim3 pblock(256);
     if (a.hops) {
@@ -166,8 +166,7 @@ static void launch_synth_w(const TreeArgs &a, hipStream_t st) {
       if (two) hipLaunchKernelGGL((tree_pair_kernel<AFS_GLOTTIS_TWO_MASS, false>), grid, pblock, 0, st, a);
       else hipLaunchKernelGGL((tree_pair_kernel<AFS_GLOTTIS_TRIANGULAR, false>), grid, pblock, 0, st, a);
     }
-    return;
-  }
+  } else
 #endif
   if (a.hops) {
     if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true, W>), grid, block, 0, st, a);
@@ -206,12 +205,20 @@ template <class K> static hipError_t preload_one(K k) {
 }
 hipError_t preload_tree_kernels() {
   hipError_t e = hipSuccess;
-  for (hipError_t x : {preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, TW>),
+  for (hipError_t x : {
+#if AFS_PAIR
+                       preload_one(tree_pair_kernel<AFS_GLOTTIS_TRIANGULAR, true>),
+                       preload_one(tree_pair_kernel<AFS_GLOTTIS_TRIANGULAR, false>),
+                       preload_one(tree_pair_kernel<AFS_GLOTTIS_TWO_MASS, true>),
+                       preload_one(tree_pair_kernel<AFS_GLOTTIS_TWO_MASS, false>),
+#else
+                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, TW>),
                        preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false, TW>),
-                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, 64>),
-                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false, 64>),
                        preload_one(tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true, TW>),
                        preload_one(tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, false, TW>),
+#endif
+                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, 64>),
+                       preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false, 64>),
                        preload_one(tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true, 64>),
                        preload_one(tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, false, 64>),
                        preload_one(tree_output_kernel), preload_one(tree_reset_kernel<TW>),

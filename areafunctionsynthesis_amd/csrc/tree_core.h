@@ -127,7 +127,8 @@ enum : int {
 #if AFS_PAIR
   X_RELX2 = X_RRAD + 2,        // wave pairs: the glottis displacements' second buffer (sample_step_pair)
   X_RNGHP = X_RELX2 + 4,       // wave pairs: the rand() ring head and pending count (two int32)
-  X_TOTAL = X_RNGHP + 1,
+  X_AGLOT = X_RNGHP + 1,       // wave pairs: the upper glottis section's area of this sample (DYN -> STAT)
+  X_TOTAL = X_AGLOT + 1,
 #else
   X_TOTAL = X_RRAD + 2,
 #endif
@@ -144,7 +145,12 @@ enum : int {
   PH_ROWS, PH_FORWARD, PH_BACKWARD, PH_UPDATE, PH_OUTPUT, PH_TARGETS,
   // wave pairs (sample_step_pair): the waits at the four barriers, the DYN wave's rand() blocks, the
   // loop's tail (output window, frame transition and its barrier)
-  PH_P1WAIT, PH_P2WAIT, PH_P3WAIT, PH_P4WAIT, PH_RNGP, PH_TAIL, PH_COUNT
+  PH_P1WAIT, PH_P2WAIT, PH_P3WAIT, PH_P4WAIT, PH_RNGP, PH_TAIL,
+  PH_S_GLOT, PH_S_TGT,  // (the STAT wave's first phase group: the glottis and static network; the targets)
+  PH_D_GEO,             // (the DYN wave's interpolation and glottis)
+  PH_P0WAIT,            // (the wait at the barrier inside the first phase group, AFS_PAIR_SPLIT1)
+  PH_PLACE_HW, PH_PLACE_T0, PH_PLACE_T1,  // (not timed: the pair kernel's wave placement and loop span)
+  PH_COUNT
 };
 
 // Solver sink / zero slots (see ArmRec).
@@ -1739,7 +1745,7 @@ AFS_HD inline ArmRaw arm_raw(const ArmRec &r, const double *X, int q) {
   return v;
 }
 #ifndef AFS_ARM_AHEAD
-#define AFS_ARM_AHEAD 2  // positions the lean walk / back substitution load ahead (1 or 2)
+#define AFS_ARM_AHEAD 1  // positions the lean walk / back substitution load ahead (1 or 2: -2 %, r06_pair_ab.txt)
 #endif
 AFS_HD inline void arm_walk_lean(const ArmRec &rr, double *X, ArmCarry &a) {
   const ArmRec r = rr;
@@ -2482,8 +2488,9 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
 // phases; the pair's waves meet at a workgroup barrier (x.bar()) between the four phase groups, so
 // LDS carries everything one wave writes and the other reads (the dynamic slots' L, R, E, D and the
 // static slots' D, the dipole samples, the rows, the solution, the published pressures and flows).
-//   P1  DYN: interpolation, the glottis (its areas for the network), the dynamic slots' network
-//       STAT: the glottis and its commit, the static slots' D, targets, noise
+//   P1  DYN: interpolation, the glottis and its commit, [barrier], the dynamic slots' network
+//       STAT: the static slots' D, [barrier], targets, noise
+//       (AFS_PAIR_SPLIT1=0: no barrier inside P1, both waves evaluate the glottis, STAT commits it)
 //   P2  rows of each role's slots
 //   P3  STAT: the arm solver (lean form) and the rand() blocks ahead
 //   P4  the state update of each role's slots; DYN: the radiated flow (R.sample)
@@ -2492,6 +2499,12 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
 #if AFS_PAIR
 #ifndef AFS_PAIR_LEAN
 #define AFS_PAIR_LEAN 1  // the STAT wave's solver in the lean form (arm_walk_lean; 0: arm_walk, every load ahead)
+#endif
+#ifndef AFS_PAIR_SPLIT1
+// the first phase group in two: the DYN wave evaluates and commits the glottis alone (the STAT wave
+// its static network meanwhile), a barrier, then DYN's network beside STAT's targets and noise (0:
+// both waves evaluate the glottis, no barrier inside the group; 1 measured -2.7 %, r06_pair_ab.txt)
+#define AFS_PAIR_SPLIT1 0
 #endif
 #ifndef AFS_PAIR_RNG_DYN
 #define AFS_PAIR_RNG_DYN 1  // the rand() blocks ahead on the DYN wave during the solver (0: on the STAT wave after it)
@@ -2520,12 +2533,28 @@ AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Cons
                                              [&](double v) { return x.xch8(v); });
                     else
                       g = glottis_eval<MODEL>(glottis_inputs(X, rcur), C, ratio, p4);
+                    if constexpr (AFS_PAIR_SPLIT1) {
+                      glottis_commit(X, g, rnext);
+                      X[X_AGLOT] = g.go.a1;
+                    }
                   });
+    x.mark(PH_D_GEO);
+    if constexpr (AFS_PAIR_SPLIT1) {
+      x.bar();
+      x.mark(PH_P0WAIT);
+    }
     x.dyn_neighbors();
     x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS, ROLE_DYN>(gl, R, X, U, C, g.go); });
     x.mark(PH_NETWORK);
   } else {
     double a_glot_up = 0.0;
+    if constexpr (AFS_PAIR_SPLIT1) {
+      x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS, ROLE_STAT>(gl, R, X, U, C, GlotOut{}); });
+      x.mark(PH_S_GLOT);
+      x.bar();
+      x.mark(PH_P0WAIT);
+      a_glot_up = X[X_AGLOT];
+    } else {
     x.par_uniform([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS, ROLE_STAT>(gl, R, X, U, C, GlotOut{}); },
                   [&](Lane<W> &R) {
                     (void)R;
@@ -2539,6 +2568,8 @@ AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Cons
                     glottis_commit(X, g, rnext);
                     a_glot_up = g.go.a1;
                   });
+    x.mark(PH_S_GLOT);
+    }
     AFS_PM(";MARK targets");
 #if !defined(AFS_PAIR_PROBE_NONOISE)
 #if AFS_PAIR_RNG_DYN
@@ -2551,6 +2582,7 @@ AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Cons
 #endif
     x.par([&](int gl, Lane<W> &R) { phase_targets<W, NZ>(x, gl, R, X, C, a_glot_up); });
     x.sync();
+    x.mark(PH_S_TGT);
     AFS_PM(";MARK noise");
     if (U.opt.generate_noise_sources) {
       phase_noise<W, NZ>(x, X, U, C);

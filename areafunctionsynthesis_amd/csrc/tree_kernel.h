@@ -608,11 +608,11 @@ __device__ __forceinline__ void tree_pair_run(const TreeArgs &a, WaveLdsT<TW> &l
     ex.mark(PH_TAIL);
   }
   if constexpr (PROF) {
-    // (the slots no pair phase uses: the wave's placement -- HW_ID, XCC_ID -- and its loop's span)
-    ex.acc[PH_GEOMETRY] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+    // (the wave's placement -- HW_ID, XCC_ID -- and its loop's span, for tools/phase_prof)
+    ex.acc[PH_PLACE_HW] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
                           ((uint64_t)(__builtin_amdgcn_s_getreg((15 << 11) | 20) & 15) << 32);
-    ex.acc[PH_OUTPUT] = t_begin;
-    ex.acc[PH_TARGETS] = __builtin_amdgcn_s_memtime();
+    ex.acc[PH_PLACE_T0] = t_begin;
+    ex.acc[PH_PLACE_T1] = __builtin_amdgcn_s_memtime();
     if (lane % 64 == 0)
       for (int q = 0; q < PH_COUNT; ++q) prof[((int64_t)blockIdx.x * 4 + lane / 64) * PH_COUNT + q] = ex.acc[q];
   }
@@ -678,7 +678,9 @@ __device__ __forceinline__ void tree_pair_body(const TreeArgs &a, WaveLdsT<TW> &
   }
   const int wave = (int)threadIdx.x / 64;
 #ifndef AFS_PAIR_MAP
-#define AFS_PAIR_MAP 1  // 0: waves 0, 1 DYN (groups 0, 1), 2, 3 STAT; 1: by the wave slot's parity; 2: by the block's parity
+// 3: by SIMD and the CU's workgroup slot; 0: waves 0, 1 DYN (groups 0, 1), 2, 3 STAT; 1: by the wave
+// slot's parity; 2: by the block's parity (profiles/r06_pair_ab.txt)
+#define AFS_PAIR_MAP 3
 #endif
   int grp, st;
   unsigned int *cu_word = nullptr;

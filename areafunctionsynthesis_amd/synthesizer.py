@@ -98,6 +98,10 @@ class Context:
         """Lanes per utterance the tree solver uses for a batch of this size."""
         return int(self._lib.afs_lanes_per_utterance(self._h, int(batch)))
 
+    def synthesis_kernel(self, batch: int) -> str:
+        """Name of the synthesis kernel a batch of this size runs (for matching profiler output)."""
+        return self._lib.afs_synthesis_kernel(self._h, int(batch)).decode()
+
     def set_stream(self, stream_handle: int) -> None:
         """Issue all work on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""
         _native.check(self._lib.afs_set_stream(self._h, _vp(stream_handle)), self._h, "afs_set_stream")

@@ -185,6 +185,7 @@ def measure(args, ctx, dev, stream, workload: str, B: int, first: int, world: in
 
     m = Measured()
     m.workload, m.B, m.steps, m.warmup = workload, B, steps, warmup
+    m.kernel = ctx.synthesis_kernel(B)  # (the profiler's name of the synthesis kernel this batch runs)
     if workload in ("static", "fricatives"):
         gen = static_vowels if workload == "static" else fricatives
         w = gen(B, seconds=args.seconds, fs=args.fs, first_utterance=first)
@@ -303,7 +304,7 @@ def describe(args, m: Measured, world: int, digest: str) -> dict:
     B, T, hop = m.B, m.T, m.hop
     total_samples = float(world) * B * T * m.steps
     value = total_samples / m.elapsed
-    kname = {"cholesky": "lane_synth_kernel", "sor": "lane_synth_kernel"}.get(args.solver, "tree_synth_kernel")
+    kname = m.kernel
     launches = max(1, m.kt["synth_launches"])
     avg_launch_s = m.kt["synth_ms"] / launches / 1e3
     samples_per_launch = B * T * m.steps / launches

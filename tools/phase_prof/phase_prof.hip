@@ -138,11 +138,9 @@ extern "C" int pp_run(const afs_frame *frames, const uint32_t *seeds, int B, int
   for (int p = 0; p < PH_COUNT; ++p) cycles[p] = 0;
   g_wave.assign(waves, 0);
   g_wave_ph = h;  // (before the pair kernel's placement slots are cleared)
-#if AFS_PAIR
   // (the pair kernel keeps each wave's placement and span in three slots it does not time)
   for (int w = 0; w < waves; ++w)
-    for (int p : {(int)PH_GEOMETRY, (int)PH_OUTPUT, (int)PH_TARGETS}) h[(size_t)w * PH_COUNT + p] = 0;
-#endif
+    for (int p : {(int)PH_PLACE_HW, (int)PH_PLACE_T0, (int)PH_PLACE_T1}) h[(size_t)w * PH_COUNT + p] = 0;
   for (int w = 0; w < waves; ++w)
     for (int p = 0; p < PH_COUNT; ++p) {
       cycles[p] += h[(size_t)w * PH_COUNT + p];

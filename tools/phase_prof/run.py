@@ -16,7 +16,9 @@ sys.path.insert(0, os.path.join(HERE, "..", ".."))
 
 PHASES = ["geometry", "network", "n:filter", "n:act", "n:rng", "rows", "forward", "backward", "update",
           "output", "targets", "pair:P1 wait", "pair:P2 wait", "pair:P3 wait", "pair:P4 wait", "pair:rng (DYN)",
-          "pair:tail"]
+          "pair:tail", "pair:glottis+static net (STAT)", "pair:targets (STAT)", "pair:interp+glottis (DYN)",
+          "pair:P0 wait", "(placement)", "(t0)", "(t1)"]
+PLACE = 21  # tree_core.h PH_PLACE_HW, then the loop's first and last memtime
 
 
 def main():
@@ -46,7 +48,8 @@ def main():
     print(f"[{os.environ.get('PP_LIB', 'libphase_prof.so')}] {args.workload} B={w.batch} T={T} waves={waves} kernel {ms.value:.2f} ms "
           f"({w.batch * T / ms.value * 1e3 / 1e6:.2f} M samples/s)")
     for p in range(n):
-        print(f"  {PHASES[p]:14s} {cyc[p] / waves / T:10.1f} clk/sample  {100 * cyc[p] / tot:5.1f} %")
+        if cyc[p]:
+            print(f"  {PHASES[p]:14s} {cyc[p] / waves / T:10.1f} clk/sample  {100 * cyc[p] / tot:5.1f} %")
     print(f"  {'total':14s} {tot / waves / T:10.1f} clk/sample")
     if not hasattr(lib, "pp_wave_totals"):
         return
@@ -54,9 +57,9 @@ def main():
         per = (ctypes.c_uint64 * (waves * n))()
         lib.pp_wave_phases(per)
         raw = np.array(per, dtype=np.uint64).reshape(waves, n)
-        hw, t0, t1 = raw[:, 0].copy(), raw[:, 9].astype(np.int64), raw[:, 10].astype(np.int64)
+        hw, t0, t1 = raw[:, PLACE].copy(), raw[:, PLACE + 1].astype(np.int64), raw[:, PLACE + 2].astype(np.int64)
         a = raw.astype(np.float64)
-        a[:, [0, 9, 10]] = 0
+        a[:, PLACE:PLACE + 3] = 0
         dyn = a[:, 1] > 0
         for role, m in (("DYN", dyn), ("STAT", ~dyn)):
             r = a[m].sum(axis=0) / max(1, m.sum()) / T
