@@ -879,6 +879,27 @@ AFS_HD inline GlotRes glottis_eval_split(const GlotIn &in, const CT &C, double r
   return res;
 }
 
+// The upper mass's area of the triangular glottis this sample (go.a1 of glottis_eval_split: the
+// same operations on its inputs), for the wave pairs' STAT wave, which needs no more of the glottis
+// (AFS_PAIR_SPLIT1=2).
+AFS_HD inline double glottis_upper_area(const GlotIn &in, double ratio) {
+  const double r1 = 1.0 - ratio;
+  double g0, g3, g4;
+  {
+#pragma clang fp contract(off)
+    g0 = r1 * in.fl[0] + ratio * in.fr[0];
+    g3 = r1 * in.fl[3] + ratio * in.fr[3];
+    g4 = r1 * in.fl[4] + ratio * in.fr[4];
+  }
+  const double chink = nonneg(g4);
+  const double q = glottis_q(g0);
+  const double f = fast_sqrt(q);
+  const double cord = G_REST_LEN * f;
+  double olen, clen, ow, cz;
+  glottis_open_close_one(g3, cord, in.rel[1], olen, clen, ow, cz);
+  return clampA_num(olen * ow + chink);
+}
+
 // The glottis state of the sample: new displacements, interpolated controls (X_GP + 1, the lung
 // pressure, is the row phase's source term of section 0).
 AFS_HD inline void glottis_commit(double *X, const GlotRes &r, int relx = X_RELX) {
@@ -2504,7 +2525,7 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
 // the first phase group in two: the DYN wave evaluates and commits the glottis alone (the STAT wave
 // its static network meanwhile), a barrier, then DYN's network beside STAT's targets and noise (0:
 // both waves evaluate the glottis, no barrier inside the group; 1 measured -2.7 %, r06_pair_ab.txt)
-#define AFS_PAIR_SPLIT1 0
+#define AFS_PAIR_SPLIT1 0  // (2: DYN commits the glottis, STAT evaluates its upper area alone, no barrier)
 #endif
 #ifndef AFS_PAIR_RNG_DYN
 #define AFS_PAIR_RNG_DYN 1  // the rand() blocks ahead on the DYN wave during the solver (0: on the STAT wave after it)
@@ -2522,6 +2543,10 @@ AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Cons
 #endif
   AFS_PM(";MARK P1 begin");
   const int rcur = par ? X_RELX2 : X_RELX, rnext = par ? X_RELX : X_RELX2;
+  // (SPLIT1 2: DYN commits the glottis, STAT evaluates only the upper area it needs -- the
+  // triangular model's split form; the two-mass model keeps both evaluations)
+  constexpr bool kSplitA = AFS_PAIR_SPLIT1 == 2 && MODEL == AFS_GLOTTIS_TRIANGULAR && Xc::kGlottisSplit;
+  constexpr bool kDynCommit = AFS_PAIR_SPLIT1 == 1 || kSplitA;
   if constexpr (ROLE == ROLE_DYN) {
     GlotRes g{};
     x.par_uniform([&](int gl, Lane<W> &R) { phase_interpolate<W>(gl, R, X, C, ratio); },
@@ -2533,13 +2558,11 @@ AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Cons
                                              [&](double v) { return x.xch8(v); });
                     else
                       g = glottis_eval<MODEL>(glottis_inputs(X, rcur), C, ratio, p4);
-                    if constexpr (AFS_PAIR_SPLIT1) {
-                      glottis_commit(X, g, rnext);
-                      X[X_AGLOT] = g.go.a1;
-                    }
+                    if constexpr (kDynCommit) glottis_commit(X, g, rnext);
+                    if constexpr (AFS_PAIR_SPLIT1 == 1) X[X_AGLOT] = g.go.a1;
                   });
     x.mark(PH_D_GEO);
-    if constexpr (AFS_PAIR_SPLIT1) {
+    if constexpr (AFS_PAIR_SPLIT1 == 1) {
       x.bar();
       x.mark(PH_P0WAIT);
     }
@@ -2548,12 +2571,19 @@ AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Cons
     x.mark(PH_NETWORK);
   } else {
     double a_glot_up = 0.0;
-    if constexpr (AFS_PAIR_SPLIT1) {
+    if constexpr (AFS_PAIR_SPLIT1 == 1) {
       x.par([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS, ROLE_STAT>(gl, R, X, U, C, GlotOut{}); });
       x.mark(PH_S_GLOT);
       x.bar();
       x.mark(PH_P0WAIT);
       a_glot_up = X[X_AGLOT];
+    } else if constexpr (kSplitA) {
+      x.par_uniform([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS, ROLE_STAT>(gl, R, X, U, C, GlotOut{}); },
+                    [&](Lane<W> &R) {
+                      (void)R;
+                      a_glot_up = glottis_upper_area(glottis_inputs(X, rcur), ratio);
+                    });
+      x.mark(PH_S_GLOT);
     } else {
     x.par_uniform([&](int gl, Lane<W> &R) { phase_network<W, VARLOSS, ROLE_STAT>(gl, R, X, U, C, GlotOut{}); },
                   [&](Lane<W> &R) {

@@ -1,6 +1,6 @@
 """Dynamic instruction mix and cycle split of the synthesis kernel from the three SQ passes of
 tools/session.sh (step `mix`, one bench step each): instructions and cycles per
-wave-sample (a wave holds 4 utterances; one audio sample of all four).  Writes
+wave-sample (--upw utterances per wave: 4 for the one-wave kernel, 2 for the wave pairs).  Writes
 profiles/pmc_mix.json under bench.py's key and the kernel sources' digest, and prints a table.
 
 usage: python tools/pmc_mix.py --tag r03h [--dir gpurun_out/r03h] [--batch 8192 --samples 44100 --hop 441]
@@ -39,12 +39,15 @@ def main():
     ap.add_argument("--samples", type=int, default=44100)
     ap.add_argument("--hop", type=int, default=441)
     ap.add_argument("--digest", default=None)
+    ap.add_argument("--upw", type=int, default=4,
+                    help="utterances per wave (4: the one-wave 16-lane kernel; 2: the wave pairs, two waves per "
+                         "four utterances; 1: the voice kernel)")
     a = ap.parse_args()
     d = a.dir or os.path.join(ROOT, "gpurun_out", a.tag)
     t = {}
     for p in ("pmc_mix1", "pmc_mix2", "pmc_mix3"):
         t.update(totals(os.path.join(d, p, "run_counter_collection.csv"), a.kernel))
-    ws = float(a.batch) * a.samples / 4.0  # wave-samples of one step
+    ws = float(a.batch) * a.samples / a.upw  # wave-samples of one step
     per = {k: (4.0 if k in QUAD else 1.0) * v / ws for k, v in t.items() if k != "SQ_WAVES"}
     f64 = sum(per.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("ADD", "MUL", "FMA", "TRANS"))
     valu = per["SQ_INSTS_VALU"]
@@ -74,8 +77,8 @@ def main():
         "wait_inst_any_cycles": per.get("SQ_WAIT_INST_ANY"),
         "wait_any_cycles": per.get("SQ_WAIT_ANY"),
     }
-    entry = {"tag": a.tag, "per_wave_sample": mix,
-             "note": "per wave and audio sample (4 utterances); VALU other = moves, selects, AGPR copies, DPP "
+    entry = {"tag": a.tag, "per_wave_sample": mix, "utterances_per_wave": a.upw,
+             "note": f"per wave and audio sample ({a.upw} utterances per wave); VALU other = moves, selects, AGPR copies, DPP "
                      "moves, lane reads/writes, compares (everything that is not fp64 arithmetic, int or cvt); "
                      "cycle counters x 4 (quad-cycles)"}
     from areafunctionsynthesis_amd.build import kernel_digest
