@@ -44,7 +44,8 @@ constexpr int UPB = Geom<TW>::UPB;
 static_assert(UPB == TREE_UPB, "afs_tree.h TREE_UPB: the host's slot orders group utterances by block");
 
 #ifndef AFS_PAIR_MARK_SB
-#define AFS_PAIR_MARK_SB 1  // the pair kernel: a scheduling barrier at every phase mark (A/B)
+// the pair kernel: a scheduling barrier at the phase marks whose bit (tree_core.h PH_*) is set (A/B)
+#define AFS_PAIR_MARK_SB 0xFFFFFFFFu
 #endif
 template <bool PROF, int W = TW, bool MARK_SB = false>
 struct GpuExec {
@@ -198,8 +199,7 @@ struct GpuExec {
       acc[ph] += t - last;
       last = t;
     } else if constexpr (MARK_SB) {
-      (void)ph;
-      __builtin_amdgcn_sched_barrier(0);
+      if ((((uint32_t)AFS_PAIR_MARK_SB) >> ph) & 1u) __builtin_amdgcn_sched_barrier(0);
     }
   }
 };
