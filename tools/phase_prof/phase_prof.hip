@@ -13,12 +13,12 @@ using namespace afs::tree;
 
 // lanes per utterance of the profiled kernel (-DPP_W=64: the voice kernel)
 #ifndef PP_W
-#define PP_W TREE_W
+#define PP_W AFS_TREE_W
 #endif
 constexpr int PW = PP_W;
 // (HOPS: K5's hop records and the noise-phase variants, as the library's large calls run)
-#if AFS_PAIR
-// the wave-pair kernel (AFS_PAIR=1 builds): four waves per block
+#if AFS_PAIR && PP_W == AFS_TREE_W
+// the wave-pair kernel (AFS_PAIR=1 builds, 16 lanes per utterance): four waves per block
 constexpr int PWPB = 4, PUPB = Geom<PW>::UPB;
 template <bool HOPS>
 __global__ void __launch_bounds__(256, 2) tree_prof_kernel(TreeArgs a, uint64_t *prof) {
