@@ -749,7 +749,10 @@ int32_t afs_lanes_per_utterance(const afs_ctx *c, int32_t batch) {
 
 const char *afs_synthesis_kernel(const afs_ctx *c, int32_t batch) {
   if (!c || c->cfg.solver != AFS_SOLVER_TREE) return "lane_synth_kernel";
-  return (AFS_PAIR && afs_lanes_per_utterance(c, batch) == afs::TREE_W) ? "tree_pair_kernel" : "tree_synth_kernel";
+  const int lanes = afs_lanes_per_utterance(c, batch);
+  if (AFS_PAIR && lanes == afs::TREE_W) return "tree_pair_kernel";
+  if (AFS_PAIR && lanes == afs::TREE_VOICE_W && batch <= afs::TREE_PAIR64_MAX) return "tree_pair64_kernel";
+  return "tree_synth_kernel";
 }
 
 afs_status afs_kernel_times_ex(afs_ctx *c, afs_kernel_timing *t) {

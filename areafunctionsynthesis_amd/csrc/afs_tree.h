@@ -112,6 +112,18 @@ inline int64_t plan_work_bytes(int64_t rows, int64_t slots) { return (rows * slo
 constexpr int TREE_W = AFS_TREE_W;      // lanes per utterance of the throughput kernel (16)
 constexpr int TREE_WPB = AFS_TREE_WPB;  // its waves per block
 constexpr int TREE_VOICE_W = 64;        // lanes per utterance of the voice kernel (one utterance per wave)
+// Batches up to this many utterances run the voice kernel as wave pairs (AFS_PAIR builds: two waves
+// per utterance on two SIMDs, 256 VGPRs each with the lean solver, so that a SIMD can hold two):
+// one voice's 1102-sample call 5.0 instead of 6.4 ms, config 2 (1024 utterances) +4.4 %, the audio
+// bitwise the one-wave kernel's (profiles/r06_pair_ab.txt r06z / r06za).  Larger batches that still
+// take 64 lanes (AFS_LANES_64) run one wave per utterance.
+#ifndef AFS_PAIR64_MAX
+#define AFS_PAIR64_MAX 1024
+#endif
+#ifndef AFS_PAIR64_WAVES
+#define AFS_PAIR64_WAVES 2  // waves per SIMD the voice pairs' registers must allow (1: the full solver, 282 VGPRs)
+#endif
+constexpr int TREE_PAIR64_MAX = AFS_PAIR64_MAX;
 constexpr int TREE_UPB = (64 / TREE_W) * TREE_WPB;  // utterances per block of the throughput kernel
 // Lanes per utterance: TREE_W or TREE_VOICE_W (the per-lane state layout, Lane<lanes>, differs).
 int64_t tree_lane_bytes(int lanes);

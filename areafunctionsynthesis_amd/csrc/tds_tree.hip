@@ -27,6 +27,12 @@ __global__ void __launch_bounds__(256, 2) tree_pair_kernel(TreeArgs a) {
   __shared__ int pattern[5];
   tree_pair_body<MODEL, HOPS>(a, lds, pattern);
 }
+// the voice kernel's pairs: two waves per utterance, each may take a whole SIMD's registers
+template <int MODEL, bool HOPS>
+__global__ void __launch_bounds__(128, AFS_PAIR64_WAVES) tree_pair64_kernel(TreeArgs a) {
+  __shared__ WaveLdsT<64> lds;
+  tree_pair64_body<MODEL, HOPS>(a, lds);
+}
 #endif
 
 // K6: the output stage of a launch's samples -- dU/dt, the 8-pole Chebyshev low-pass, x 0.004 /
@@ -150,6 +156,18 @@ hipError_t launch_tree_reset(void *lane_state, double *lds_state, int B, const u
   return hipGetLastError();
 }
 
+// the one-wave kernel (every phase on one wave)
+template <int W>
+static void launch_one_wave(const TreeArgs &a, dim3 grid, dim3 block, bool two, hipStream_t st) {
+  if (a.hops) {
+    if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true, W>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, W>), grid, block, 0, st, a);
+  } else {
+    if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, false, W>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false, W>), grid, block, 0, st, a);
+  }
+}
+
 template <int W>
 static void launch_synth_w(const TreeArgs &a, hipStream_t st) {
   constexpr int UPB_ = Geom<W>::UPB;
@@ -166,15 +184,23 @@ static void launch_synth_w(const TreeArgs &a, hipStream_t st) {
       if (two) hipLaunchKernelGGL((tree_pair_kernel<AFS_GLOTTIS_TWO_MASS, false>), grid, pblock, 0, st, a);
       else hipLaunchKernelGGL((tree_pair_kernel<AFS_GLOTTIS_TRIANGULAR, false>), grid, pblock, 0, st, a);
     }
-  } else
-#endif
-  if (a.hops) {
-    if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, true, W>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, W>), grid, block, 0, st, a);
-  } else {
-    if (two) hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TWO_MASS, false, W>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false, W>), grid, block, 0, st, a);
+  } else if constexpr (W == 64) {
+    if (a.B <= TREE_PAIR64_MAX) {
+      const dim3 pblock(128);
+      if (a.hops) {
+        if (two) hipLaunchKernelGGL((tree_pair64_kernel<AFS_GLOTTIS_TWO_MASS, true>), grid, pblock, 0, st, a);
+        else hipLaunchKernelGGL((tree_pair64_kernel<AFS_GLOTTIS_TRIANGULAR, true>), grid, pblock, 0, st, a);
+      } else {
+        if (two) hipLaunchKernelGGL((tree_pair64_kernel<AFS_GLOTTIS_TWO_MASS, false>), grid, pblock, 0, st, a);
+        else hipLaunchKernelGGL((tree_pair64_kernel<AFS_GLOTTIS_TRIANGULAR, false>), grid, pblock, 0, st, a);
+      }
+      return;
+    }
   }
+  if constexpr (W != TW) launch_one_wave<W>(a, grid, block, two, st);
+#else
+  launch_one_wave<W>(a, grid, block, two, st);
+#endif
 }
 
 hipError_t launch_tree_synth(const TreeArgs &a, int lanes, hipStream_t st) {
@@ -211,6 +237,10 @@ hipError_t preload_tree_kernels() {
                        preload_one(tree_pair_kernel<AFS_GLOTTIS_TRIANGULAR, false>),
                        preload_one(tree_pair_kernel<AFS_GLOTTIS_TWO_MASS, true>),
                        preload_one(tree_pair_kernel<AFS_GLOTTIS_TWO_MASS, false>),
+                       preload_one(tree_pair64_kernel<AFS_GLOTTIS_TRIANGULAR, true>),
+                       preload_one(tree_pair64_kernel<AFS_GLOTTIS_TRIANGULAR, false>),
+                       preload_one(tree_pair64_kernel<AFS_GLOTTIS_TWO_MASS, true>),
+                       preload_one(tree_pair64_kernel<AFS_GLOTTIS_TWO_MASS, false>),
 #else
                        preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, true, TW>),
                        preload_one(tree_synth_kernel<AFS_GLOTTIS_TRIANGULAR, false, TW>),

@@ -2644,7 +2644,8 @@ AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Cons
   AFS_PM(";MARK solver");
   if constexpr (ROLE == ROLE_STAT) {
 #if !defined(AFS_PAIR_PROBE_NOSOLVE)
-    solve_arms<W, Xc, AFS_PAIR_LEAN != 0>(x, X, C);
+    // (64 lanes at one wave per SIMD: registers to spare for the full form)
+    solve_arms<W, Xc, AFS_PAIR_LEAN != 0 && (W != 64 || AFS_PAIR64_WAVES >= 2)>(x, X, C);
 #endif
     AFS_PM(";MARK rng");
 #if !defined(AFS_PAIR_PROBE_NORNG) && !AFS_PAIR_RNG_DYN

@@ -494,9 +494,11 @@ __device__ __forceinline__ void tree_synth_body(const TreeArgs &a, WaveLdsT<W> &
 // slots' state, so the pair's kernel must fit 256 registers per lane.
 // ---------------------------------------------------------------------------
 #if AFS_PAIR
-template <int MODEL, bool HOPS, int NZ, int ROLE, bool PROF = false>
-__device__ __forceinline__ void tree_pair_run(const TreeArgs &a, WaveLdsT<TW> &lds, int grp, uint64_t *prof = nullptr) {
-  constexpr int W = TW, UPB_ = Geom<W>::UPB;
+// (W = 64: the voice kernel's pairs, one utterance per workgroup of two waves, tree_pair64_body)
+template <int MODEL, bool HOPS, int NZ, int ROLE, bool PROF = false, int W = TW>
+__device__ __forceinline__ void tree_pair_run(const TreeArgs &a, WaveLdsT<W> &lds, int grp, uint64_t *prof = nullptr) {
+  constexpr int UPB_ = Geom<W>::UPB;
+  constexpr int NT = 2 * 64 * Geom<W>::WPB;  // threads per workgroup (a pair per wave of the one-wave kernel)
   using S = Shape<W>;
   const int lane = threadIdx.x;  // 0 .. 255
   const int g = grp * Geom<W>::UPW + (lane % 64) / W, gl = lane % W;
@@ -509,7 +511,7 @@ __device__ __forceinline__ void tree_pair_run(const TreeArgs &a, WaveLdsT<TW> &l
   {
     const uint64_t *src = (const uint64_t *)&T.consts;
     uint64_t *dst = (uint64_t *)&lds.C;
-    for (int k = lane; k < (int)(sizeof(Consts) / 8); k += 256) dst[k] = src[k];
+    for (int k = lane; k < (int)(sizeof(Consts) / 8); k += NT) dst[k] = src[k];
   }
   Lane<W> R = ((const Lane<W> *)a.lane_state)[(int64_t)ue * W + gl];
   const double *ls = a.lds_state + (int64_t)ue * X_TOTAL;
@@ -614,7 +616,7 @@ __device__ __forceinline__ void tree_pair_run(const TreeArgs &a, WaveLdsT<TW> &l
     ex.acc[PH_PLACE_T0] = t_begin;
     ex.acc[PH_PLACE_T1] = __builtin_amdgcn_s_memtime();
     if (lane % 64 == 0)
-      for (int q = 0; q < PH_COUNT; ++q) prof[((int64_t)blockIdx.x * 4 + lane / 64) * PH_COUNT + q] = ex.acc[q];
+      for (int q = 0; q < PH_COUNT; ++q) prof[((int64_t)blockIdx.x * (NT / 64) + lane / 64) * PH_COUNT + q] = ex.acc[q];
   }
   if constexpr (ROLE == ROLE_DYN) {  // (the displacements of the last sample into X_RELX, the image's slot)
     if (n & 1) {
@@ -747,6 +749,35 @@ __device__ __forceinline__ void tree_pair_body(const TreeArgs &a, WaveLdsT<TW> &
   }
   if constexpr (AFS_PAIR_MAP == 3) {
     if (threadIdx.x == 0 && cu_bit) atomicAnd(cu_word, ~cu_bit);  // (after the run's last workgroup barrier)
+  }
+}
+
+// The voice kernel's pairs (64 lanes per utterance): one utterance per workgroup of two waves, wave 0
+// DYN and wave 1 STAT, for batches that leave a SIMD to each wave (afs_tree.h TREE_PAIR64_MAX): the
+// sample's chain split over two SIMDs instead of one wave's.
+template <int MODEL, bool HOPS, bool PROF = false>
+__device__ __forceinline__ void tree_pair64_body(const TreeArgs &a, WaveLdsT<64> &lds, uint64_t *prof = nullptr) {
+  if (a.skip_claims && (int64_t)*a.skip_claims > a.skip_cap) return;
+  if (a.order && a.order[blockIdx.x] >= a.B) return;
+  const bool stat = threadIdx.x >= 64;
+  if (!stat) {
+    tree_pair_run<MODEL, HOPS, NZ_FULL, ROLE_DYN, PROF, 64>(a, lds, 0, prof);
+  } else if constexpr (HOPS) {
+    const int nz = noise_variant<64>(a, 0, (int)threadIdx.x % 64);
+    if (false) {
+#if AFS_NZ_SET & 2
+    } else if (nz == NZ_GLOTTIS) {
+      tree_pair_run<MODEL, HOPS, NZ_GLOTTIS, ROLE_STAT, PROF, 64>(a, lds, 0, prof);
+#endif
+#if AFS_NZ_SET & 1
+    } else if (nz == NZ_TONGUE1) {
+      tree_pair_run<MODEL, HOPS, NZ_TONGUE1, ROLE_STAT, PROF, 64>(a, lds, 0, prof);
+#endif
+    } else {
+      tree_pair_run<MODEL, HOPS, NZ_FULL, ROLE_STAT, PROF, 64>(a, lds, 0, prof);
+    }
+  } else {
+    tree_pair_run<MODEL, HOPS, NZ_FULL, ROLE_STAT, PROF, 64>(a, lds, 0, prof);
   }
 }
 

@@ -193,7 +193,8 @@ afs_status afs_set_stream(afs_ctx *ctx, void *hip_stream);
  * one-lane solvers). */
 int32_t afs_lanes_per_utterance(const afs_ctx *ctx, int32_t batch);
 /* Name of the synthesis kernel a batch of this size runs ("tree_pair_kernel": 16 lanes per
- * utterance, two waves per SIMD; "tree_synth_kernel": the 64-lane voice kernel, or 16 lanes in a
+ * utterance, two waves per SIMD; "tree_pair64_kernel": the 64-lane voice kernel as wave pairs, small
+ * batches; "tree_synth_kernel": the 64-lane voice kernel one wave per utterance, or any batch of a
  * one-wave build; "lane_synth_kernel": the one-lane solvers) -- for matching profiler output.
  * Diagnostics; no reference counterpart. */
 const char *afs_synthesis_kernel(const afs_ctx *ctx, int32_t batch);

@@ -26,6 +26,14 @@ __global__ void __launch_bounds__(256, 2) tree_prof_kernel(TreeArgs a, uint64_t 
   __shared__ int pattern[5];
   tree_pair_body<AFS_GLOTTIS_TRIANGULAR, HOPS, true>(a, lds, pattern, prof);
 }
+#elif AFS_PAIR && PP_W == 64
+// the voice kernel's pairs (AFS_PAIR builds, -DPP_W=64): two waves per utterance
+constexpr int PWPB = 2, PUPB = 1;
+template <bool HOPS>
+__global__ void __launch_bounds__(128, AFS_PAIR64_WAVES) tree_prof_kernel(TreeArgs a, uint64_t *prof) {
+  __shared__ WaveLdsT<64> lds;
+  tree_pair64_body<AFS_GLOTTIS_TRIANGULAR, HOPS, true>(a, lds, prof);
+}
 #else
 constexpr int PWPB = Geom<PW>::WPB, PUPB = Geom<PW>::UPB;
 

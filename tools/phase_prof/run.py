@@ -69,8 +69,9 @@ def main():
         # while both run, by their roles (weighted by the overlap of their loops' spans)
         simd = (hw >> np.uint64(4)) & np.uint64(3)
         cu = ((hw >> np.uint64(32)) << np.uint64(8)) | ((hw >> np.uint64(8)) & np.uint64(255))
-        blk = np.arange(waves) // 4
-        spread = np.mean([len(set(simd[b * 4:(b + 1) * 4].tolist())) == 4 for b in range(waves // 4)])
+        wpb = lib.pp_waves_per_block()
+        blk = np.arange(waves) // wpb
+        spread = np.mean([len(set(simd[b * wpb:(b + 1) * wpb].tolist())) == wpb for b in range(waves // wpb)])
         pairs = {"DYN+DYN": 0.0, "DYN+STAT": 0.0, "STAT+STAT": 0.0}
         key = (cu << np.uint64(2)) | simd
         order = np.argsort(key, kind="stable")
@@ -87,7 +88,7 @@ def main():
                         pairs[["STAT+STAT", "DYN+STAT", "DYN+DYN"][int(dyn[i]) + int(dyn[j])]] += ov
         tot_ov = sum(pairs.values()) or 1.0
         xcc = sorted(set((hw >> np.uint64(32)).tolist()))
-        print(f"  placement: workgroups on four SIMDs {100 * spread:.1f} %; XCC ids {xcc}; SIMD sharing by roles " +
+        print(f"  placement: workgroups on {wpb} distinct SIMDs {100 * spread:.1f} %; XCC ids {xcc}; SIMD sharing by roles " +
               ", ".join(f"{k} {100 * v / tot_ov:.1f} %" for k, v in pairs.items()))
     wt = (ctypes.c_uint64 * waves)()
     lib.pp_wave_totals(wt)

@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--samples", type=int, default=44100)
     ap.add_argument("--hop", type=int, default=441)
     ap.add_argument("--digest", default=None)
-    ap.add_argument("--upw", type=int, default=4,
+    ap.add_argument("--upw", type=float, default=4,
                     help="utterances per wave (4: the one-wave 16-lane kernel; 2: the wave pairs, two waves per "
                          "four utterances; 1: the voice kernel)")
     a = ap.parse_args()

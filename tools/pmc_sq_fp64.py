@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--samples", type=int, default=44100)
     ap.add_argument("--hop", type=int, default=441)
-    ap.add_argument("--upw", type=int, default=4, help="utterances per wave (4: the 16-lane kernel, 1: the voice kernel)")
+    ap.add_argument("--upw", type=float, default=4, help="utterances per wave (4: the 16-lane kernel, 1: the voice kernel)")
     a = ap.parse_args()
     d = a.dir or os.path.join(ROOT, "gpurun_out", a.tag)
     tot = {}

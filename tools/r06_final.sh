@@ -16,7 +16,7 @@ for s in $STEPS; do
     bench|prof|pmc|sq|mix) bash tools/session.sh $TAG $s || exit $? ;;
     c2) BENCH_ARGS="--batch 1024" bash tools/session.sh ${TAG}_c2 sq || exit $? ;;
     pp) PP_HOPS=1 PP_PAIR_ROLES=1 timeout -k 10 240 python tools/phase_prof/run.py --batch 65536 --seconds 0.02 > $OUT/pp_64k.txt 2>&1 || exit 1
-        PP_LIB=libphase_prof_w64.so timeout -k 10 200 python tools/phase_prof/run.py --batch 1024 --seconds 0.05 > $OUT/pp_w64_1024.txt 2>&1 || exit 1
+        PP_PAIR_ROLES=1 PP_LIB=libphase_prof_w64.so timeout -k 10 200 python tools/phase_prof/run.py --batch 1024 --seconds 0.05 > $OUT/pp_w64_1024.txt 2>&1 || exit 1
         cat $OUT/pp_64k.txt $OUT/pp_w64_1024.txt ;;
     bal) timeout -k 10 300 python tools/shard_balance.py > $OUT/shard_balance.txt 2>&1 || exit 1; cat $OUT/shard_balance.txt ;;
   esac
