@@ -70,9 +70,9 @@ def test_adapter_realtime_latency(adapter_bin, oracle, tmp_path, parity_report):
     Bounds: the hard real-time one -- no call's wall time above the 50 ms of audio it makes (the first
     synthesis call included: afs_create loads the kernels' code objects, which HIP otherwise loads at
     their first launch) -- and, on the device time of a call (K5 + K1 + K6, HIP events: free of the
-    host's scheduling jitter on a shared box), p99 below the reference core's time for the same 1102
-    samples (7.5 ms: 147 k samples/s per core, bench.py cpu_baseline).  The wall-time p99 against
-    7.5 ms is reported, not asserted."""
+    host's scheduling jitter on a shared box), p99 below 6.0 ms -- 20 % under the reference core's
+    time for the same 1102 samples (7.5 ms: 147 k samples/s per core, bench.py cpu_baseline); the voice
+    kernel's wave pairs measured 5.2 ms.  The wall-time p99 is reported, not asserted."""
     f = oracle.af_to_frame(default_shapes()["s"])
     f["velum_opening_cm2"] = 0.2
     f["glottis"] = DEFAULT_GLOTTIS
@@ -105,7 +105,7 @@ def test_adapter_realtime_latency(adapter_bin, oracle, tmp_path, parity_report):
         f"slowest call (#{w + 1}): conversion {conv[w] * 1e3:.1f} us, K5 {k5[w]:.3f}, K1 {k1[w]:.3f}, K6 {k6[w]:.3f}, "
         f"host {rest[w]:.3f} ms")
     assert ms.max() < hop / fs * 1e3, (p50, p99, ms.max(), w, t[w])
-    assert d99 < 7.5, (np.median(dev), d99)
+    assert d99 < 6.0, (np.median(dev), d99)
 
 
 REF_BACKEND = "/root/reference/src/Backend"
