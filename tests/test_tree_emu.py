@@ -315,3 +315,64 @@ def test_arm_scan_extreme_areas_vs_oracle(emu, oracle, case):
         assert np.all(np.isfinite(x)) and np.all(np.isfinite(y)), (case, fs)
         scale = max(1.0, float(np.abs(y).max()))
         assert np.abs(x[:2048] - y[:2048]).max() <= TOL * scale, (case, fs)
+
+
+@pytest.fixture(scope="module")
+def pair_emu():
+    subprocess.check_call(["make", "-s", "-C", EMU])
+    lib = ctypes.CDLL(os.path.join(EMU, "libpair_emu.so"))
+    vp = ctypes.c_void_p
+    lib.emu_pair_utterance.restype = ctypes.c_long
+    lib.emu_pair_utterance.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_double, ctypes.c_int,
+                                       vp, ctypes.c_double, vp, vp]
+    return lib
+
+
+@pytest.mark.parametrize("W", [16, 64])
+@pytest.mark.parametrize("opt", [{}, {"glottis_model": 1}, {"glottis_loss": 2, "transvelar_coupling": 1},
+                                 {"radiation_from_skin": 0, "generate_noise_sources": 0}],
+                         ids=lambda o: "+".join(f"{k}={v}" for k, v in o.items()) or "default")
+def test_wave_pair_step_equals_one_wave(emu, pair_emu, oracle, W, opt):
+    """The wave pairs (tree_core.h sample_step_pair, the device's throughput and voice kernels): the
+    DYN and STAT roles on two threads meeting at the step's barriers (tests/emu/pair_emu.cpp) give
+    the one-wave step's audio (tone filter in K6, as on the device) and rand() count bit for bit --
+    the lean solver, the glottis committed by STAT, the rand() blocks generated on DYN included."""
+    from oracle_lib import OPTION_DEFAULTS
+
+    from areafunctionsynthesis_amd.frames import DEFAULT_GLOTTIS
+    from areafunctionsynthesis_amd.params import default_shapes
+    if W == 64 and opt:
+        pytest.skip("the one-wave emulator takes options at 16 lanes (lane-width invariance: test_lane_width_invariance)")
+    sh = default_shapes()
+    frames = []
+    for name, f0, velum in (("a:", 120.0, 0.0), ("s", 125.0, 0.3), ("i:", 130.0, 0.0), ("z", 118.0, 0.5)):
+        f = oracle.af_to_frame(sh[name])
+        f["glottis"] = DEFAULT_GLOTTIS
+        f["glottis"][0] = f0
+        f["velum_opening_cm2"] = velum
+        if opt.get("glottis_model"):
+            f["glottis"][5] = 1.2
+        frames.append(f)
+    frames = np.ascontiguousarray(np.stack(frames * 2), dtype=FRAME_DTYPE)
+    hop, fs, seed = 300, 22050.0, 11
+    o = dict(OPTION_DEFAULTS, **opt)
+    iopt = np.array([o[k] for k in ("turbulence_losses", "soft_walls", "generate_noise_sources", "radiation_from_skin",
+                                    "piriform_fossa", "inner_length_corrections", "transvelar_coupling",
+                                    "glottis_loss", "glottis_model")], dtype=np.int32)
+    y = np.zeros((frames.size - 1) * hop)
+    draws = np.zeros(1, np.uint64)
+    n = pair_emu.emu_pair_utterance(frames.ctypes.data, frames.size, hop, seed, fs, W, iopt.ctypes.data,
+                                    float(o["flow_separation_area_ratio"]), y.ctypes.data, draws.ctypes.data)
+    assert n == y.size
+    emu.lib.emu_tree_set_tone_k6.argtypes = [ctypes.c_int]
+    emu.lib.emu_tree_set_tone_k6(1)
+    try:
+        x = emu.opt(frames, hop, seed, fs, opt) if W == 16 else emu(frames, hop, seed, fs, W=W)
+    finally:
+        emu.lib.emu_tree_set_tone_k6(0)
+    assert np.isfinite(y).all()
+    assert np.array_equal(x, y), np.abs(x - y).max()
+    z = oracle.utterance(frames, hop, seed, fs, opt=opt)
+    assert np.abs(y[:2048] - z[:2048]).max() <= TOL
+    if o["generate_noise_sources"]:
+        assert int(draws[0]) > 0
