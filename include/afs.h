@@ -122,9 +122,10 @@ typedef struct afs_options {
  * returns their summed durations (measurement only: a few microseconds per launch). */
 #define AFS_PROFILE 0x2u
 /* Tree solver, lanes per utterance.  By default the library picks per call (per session: at its
- * creation) from the batch: the voice kernel (64 lanes, one utterance per wave, two tube sections
- * per lane: the shortest time per sample) while the batch is no larger than the GPU's SIMD count,
- * the throughput kernel (16 lanes, four utterances per wave, six sections per lane) above.  These
+ * creation) from the batch: the voice kernel (64 lanes, two tube sections per lane, each utterance's
+ * phases split over a pair of waves on two SIMDs: the shortest time per sample) while the batch is no
+ * larger than the GPU's SIMD count, the throughput kernel (16 lanes, six sections per lane, four
+ * utterances per pair of waves, two waves per SIMD) above.  These
  * flags force one of them (not both).  The two kernels evaluate the same operations per section but
  * are separate compilations: their audio agrees within the parity tolerances, not bit for bit. */
 #define AFS_LANES_16 0x4u
