@@ -559,6 +559,10 @@ __device__ __forceinline__ void tree_pair_run(const TreeArgs &a, WaveLdsT<W> &ld
   __syncthreads();  // (the LDS image and X_FRAME in place for both roles)
   uint64_t next = 0;
   if constexpr (ROLE == ROLE_STAT) next = hmixed ? (HOPS ? pd[i * PLAN_WORDS] : pl[0]) : 0;
+  if constexpr (ROLE == ROLE_STAT && AFS_PAIR_PRIO == 3) AFS_SETPRIO(2);
+  if constexpr (ROLE == ROLE_STAT && AFS_PAIR_PRIO == 0) {
+    if (a.stat_prio) AFS_SETPRIO(2);  // (TreeArgs::stat_prio)
+  }
   uint64_t t_begin = 0;
   if constexpr (PROF) t_begin = ex.last = __builtin_amdgcn_s_memtime();
   for (int64_t t = 0; t < n; ++t) {

@@ -184,7 +184,9 @@ int32_t afs_abi_version(void);
  *                           lightest variant each launch's noise-source plans allow (same audio);
  *                           =2 the variants for every call (default: for calls whose batch is mostly
  *                           light or holds >= 16 waves per SIMD: DESIGN.md 2.5)
- *   AFS_PLAN_OVERLAP=1      chunked path: K5 of the next launch beside K1 of this one */
+ *   AFS_PLAN_OVERLAP=1      chunked path: K5 of the next launch beside K1 of this one
+ *   AFS_STAT_PRIO=0 / 1     the throughput kernel's STAT waves never / always at the higher issue
+ *                           priority (default: for launches of 2-4 rounds of workgroups per CU) */
 afs_status afs_create(afs_ctx **ctx, const afs_config *cfg);
 void afs_destroy(afs_ctx *ctx);
 const char *afs_last_error(const afs_ctx *ctx);
