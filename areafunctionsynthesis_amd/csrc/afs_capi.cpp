@@ -196,10 +196,10 @@ afs_status run_chunks(afs_ctx *c, const afs_frame *frames, int64_t fstride, int 
       afs::TreeArgs a{c->dev_tab, frames, fstride, frame_row, hop, s0, s1, out + s0, ostride, plan, plan_stride, lanes,
                       (double *)ws, B, c->host_tab.uni, hops, hop_stride, p25_row0(s0), p25_stride, so.order,
                       so.variants ? 1 : 0, so.grid, so.variants_dev, skip, skip_cap};
-      {  // the pairs' STAT priority for launches of 2-4 rounds of workgroups per CU slot (two per CU)
+      {  // the pairs' STAT priority mode by the launch's rounds of workgroups per CU slot (two per CU)
         const int64_t blocks = so.grid > 0 ? so.grid : ((int64_t)B + afs::TREE_UPB - 1) / afs::TREE_UPB;
         const int64_t slots = std::max<int64_t>(1, c->simds / 2), rounds = (blocks + slots - 1) / slots;
-        a.stat_prio = c->stat_prio >= 0 ? c->stat_prio : (width == afs::TREE_W && rounds >= 2 && rounds <= 4);
+        a.stat_prio = c->stat_prio >= 0 ? c->stat_prio : ((width == afs::TREE_W && rounds >= 2) ? 2 : 0);
       }
       hipEvent_t e1 = prof_event(c);
       HIP_TRY(c, afs::launch_tree_synth(a, width, c->stream));

@@ -50,7 +50,7 @@ struct afs_ctx {
   // at least half of the utterances in a light class (shape_order), 2 for every call, 0 never
   int noise_variants = 1;
   int class_order = 2;                 // AFS_CLASS_ORDER: the slot order's noise-class key (af_kernels.hip; A/B)
-  int stat_prio = -1;                  // AFS_STAT_PRIO: the pairs' STAT priority, -1 by the launch's rounds (A/B: 0 / 1)
+  int stat_prio = -1;                  // AFS_STAT_PRIO: the pairs' STAT priority mode (afs_tree.h), -1 by the launch's rounds
   void *keys = nullptr;                // shape keys, sorted keys, utterance indices, the variant flag (device)
   size_t keys_bytes = 0;
   void *sort_tmp = nullptr;            // the device radix sort's scratch

@@ -52,9 +52,10 @@ struct TreeArgs {
   // then runs the call through the chunked path instead
   const uint32_t *skip_claims = nullptr;
   int64_t skip_cap = 0;
-  // wave pairs: the STAT waves run at a higher issue priority than their SIMDs' DYN waves (s_setprio;
-  // afs_capi.cpp sets it for launches of 2-4 rounds of workgroups per CU slot: +2.5-5 %, neutral or
-  // worse at 1 and >= 8 rounds, profiles/r06_pair_ab.txt r06zj)
+  // wave pairs: when the STAT waves run at a higher issue priority than their SIMDs' DYN waves
+  // (s_setprio; tree_core.h pair_prio): 0 never, 1 during the solver, 2 during the first phase group and
+  // the solver, 3 the whole launch (afs_capi.cpp picks by the launch's rounds of workgroups per CU
+  // slot; profiles/r06_pair_ab.txt r06zh-r06zm)
   int stat_prio = 0;
 };
 // K5: the noise-source plans of samples [s_begin, s_end) of `rows` frame rows.

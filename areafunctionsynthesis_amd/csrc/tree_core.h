@@ -2525,11 +2525,12 @@ AFS_HD inline void sample_step(Xc &x, double *X, const Uni &U, const Consts &C, 
 #define AFS_PAIR_LEAN 1  // the STAT wave's solver in the lean form (arm_walk_lean; 0: arm_walk, every load ahead)
 #endif
 #ifndef AFS_PAIR_PRIO
-// the STAT wave's issue priority over its SIMD's other wave (a DYN wave of another workgroup): 0 as the
-// host sets TreeArgs::stat_prio (for the whole launch), 1 during the solver, 2 during the first phase
-// group and the solver, 3 always (A/B builds)
+// the STAT wave's issue priority over its SIMD's other wave (a DYN wave of another workgroup): 1 during
+// the solver, 2 during the first phase group and the solver, 3 always; 0: the launch's mode
+// (TreeArgs::stat_prio, the executor's prio) -- nonzero values fix it at compile time (A/B builds)
 #define AFS_PAIR_PRIO 0
 #endif
+template <class Xc> AFS_HD inline int pair_prio(const Xc &x) { return AFS_PAIR_PRIO ? AFS_PAIR_PRIO : x.prio; }
 #ifndef AFS_PAIR_SPLIT1
 // the first phase group in two: the DYN wave evaluates and commits the glottis alone (the STAT wave
 // its static network meanwhile), a barrier, then DYN's network beside STAT's targets and noise (0:
@@ -2551,7 +2552,9 @@ AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Cons
 #define AFS_PM(t) AFS_SCHED_BARRIER()
 #endif
   AFS_PM(";MARK P1 begin");
-  if constexpr (ROLE == ROLE_STAT && AFS_PAIR_PRIO == 2) AFS_SETPRIO(2);
+  if constexpr (ROLE == ROLE_STAT) {
+    if (pair_prio(x) == 2) AFS_SETPRIO(2);
+  }
   const int rcur = par ? X_RELX2 : X_RELX, rnext = par ? X_RELX : X_RELX2;
   // (SPLIT1 2: DYN commits the glottis, STAT evaluates only the upper area it needs -- the
   // triangular model's split form; the two-mass model keeps both evaluations)
@@ -2646,14 +2649,18 @@ AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Cons
   }
   x.bar();
   x.mark(PH_P1WAIT);
-  if constexpr (ROLE == ROLE_STAT && AFS_PAIR_PRIO == 2) AFS_SETPRIO(0);
+  if constexpr (ROLE == ROLE_STAT) {
+    if (pair_prio(x) == 2) AFS_SETPRIO(0);
+  }
   AFS_PM(";MARK rows");
   x.par([&](int gl, Lane<W> &R) { phase_rows<W, ROLE>(gl, R, X, X, U, C); });
   x.mark(PH_ROWS);
   x.bar();
   x.mark(PH_P2WAIT);
   AFS_PM(";MARK solver");
-  if constexpr (ROLE == ROLE_STAT && (AFS_PAIR_PRIO == 1 || AFS_PAIR_PRIO == 2)) AFS_SETPRIO(2);
+  if constexpr (ROLE == ROLE_STAT) {
+    if (pair_prio(x) == 1 || pair_prio(x) == 2) AFS_SETPRIO(2);
+  }
   if constexpr (ROLE == ROLE_STAT) {
 #if !defined(AFS_PAIR_PROBE_NOSOLVE)
     // (64 lanes at one wave per SIMD: registers to spare for the full form)
@@ -2685,7 +2692,9 @@ AFS_HD inline void sample_step_pair_v(Xc &x, double *X, const Uni &U, const Cons
 #endif
   x.bar();
   x.mark(PH_P3WAIT);
-  if constexpr (ROLE == ROLE_STAT && (AFS_PAIR_PRIO == 1 || AFS_PAIR_PRIO == 2)) AFS_SETPRIO(0);
+  if constexpr (ROLE == ROLE_STAT) {
+    if (pair_prio(x) == 1 || pair_prio(x) == 2) AFS_SETPRIO(0);
+  }
   AFS_PM(";MARK update");
   if constexpr (ROLE == ROLE_DYN)
     x.par_uniform([&](int gl, Lane<W> &R) { phase_update<W, ROLE>(gl, R, X, X, U, C); },

@@ -55,6 +55,7 @@ struct GpuExec {
   Lane<W> *R;
   uint64_t last = 0;
   uint64_t acc[PROF ? PH_COUNT : 1] = {};
+  int prio = 0;  // (wave pairs: the launch's STAT priority mode, TreeArgs::stat_prio)
   template <class F> __device__ __forceinline__ void par(F f) { f(gl, *R); }
   // the lane's registers, for values that are the same on every lane of the utterance
   __device__ __forceinline__ const Lane<W> &first() const { return *R; }
@@ -520,6 +521,7 @@ __device__ __forceinline__ void tree_pair_run(const TreeArgs &a, WaveLdsT<W> &ld
   __syncthreads();
   const Consts &C = lds.C;
   GpuExec<PROF, W, AFS_PAIR_MARK_SB != 0> ex{gl, &R};
+  ex.prio = a.stat_prio;
   const int64_t row = a.frame_row ? a.frame_row[ue] : ue;
   const afs_frame *fu = a.frames + row * a.frame_stride;
   double *o = a.out + (int64_t)ue * a.out_stride;
@@ -559,9 +561,8 @@ __device__ __forceinline__ void tree_pair_run(const TreeArgs &a, WaveLdsT<W> &ld
   __syncthreads();  // (the LDS image and X_FRAME in place for both roles)
   uint64_t next = 0;
   if constexpr (ROLE == ROLE_STAT) next = hmixed ? (HOPS ? pd[i * PLAN_WORDS] : pl[0]) : 0;
-  if constexpr (ROLE == ROLE_STAT && AFS_PAIR_PRIO == 3) AFS_SETPRIO(2);
-  if constexpr (ROLE == ROLE_STAT && AFS_PAIR_PRIO == 0) {
-    if (a.stat_prio) AFS_SETPRIO(2);  // (TreeArgs::stat_prio)
+  if constexpr (ROLE == ROLE_STAT) {
+    if (pair_prio(ex) == 3) AFS_SETPRIO(2);  // (the whole launch; modes 1, 2: sample_step_pair)
   }
   uint64_t t_begin = 0;
   if constexpr (PROF) t_begin = ex.last = __builtin_amdgcn_s_memtime();

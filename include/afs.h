@@ -185,8 +185,9 @@ int32_t afs_abi_version(void);
  *                           =2 the variants for every call (default: for calls whose batch is mostly
  *                           light or holds >= 16 waves per SIMD: DESIGN.md 2.5)
  *   AFS_PLAN_OVERLAP=1      chunked path: K5 of the next launch beside K1 of this one
- *   AFS_STAT_PRIO=0 / 1     the throughput kernel's STAT waves never / always at the higher issue
- *                           priority (default: for launches of 2-4 rounds of workgroups per CU) */
+ *   AFS_STAT_PRIO=0..3      when the throughput kernel's STAT waves run at the higher issue priority:
+ *                           never / the solver / the first phase group and the solver / always
+ *                           (default: 2 for launches of two or more rounds of workgroups per CU) */
 afs_status afs_create(afs_ctx **ctx, const afs_config *cfg);
 void afs_destroy(afs_ctx *ctx);
 const char *afs_last_error(const afs_ctx *ctx);

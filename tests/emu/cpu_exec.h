@@ -33,6 +33,7 @@ struct CpuExec {
   static constexpr bool kToneOut = TONE;        // the device's tone filter in K6 (emu_tree_set_tone_k6)
   Lane<W> *R;
   Barrier2 *barrier = nullptr;  // (wave pairs, pair_emu.cpp: the two roles' threads meet here)
+  int prio = 0;                 // (the device's issue-priority mode: no effect on the host)
   void bar() {
     if (barrier) barrier->wait();
   }
