@@ -618,10 +618,9 @@ def main() -> None:
                 "ratio_to_value": ds["value"] / d["value"],
                 "roofline": ds["roofline"], "fp64": ds["fp64"],
                 "rows_bitwise_equal_to_the_batch": shard.same_as_batch, "rows_compared": shard.same_rows,
-                "why_slower": "8192 utterances fill the GPU's 1024 SIMDs (one wave of 4 utterances each) exactly "
-                              "twice: each SIMD runs two waves back to back, so lighter noise-phase variants "
-                              "(DESIGN.md 2.5) shorten a SIMD's time only when both of its waves are light; at "
-                              "65536 utterances each SIMD runs 16 waves and the light ones balance",
+                "why_slower": "8192 utterances are two rounds of workgroups per CU slot (65536: sixteen); K1 takes "
+                              "~159 ms per round of 0.5 s utterances plus a fixed ~21-29 ms per launch, present with "
+                              "uniform blocks too -- 8 % of an 8192 launch, 1 % of a 65536 one (DESIGN.md 2.5)",
             }
         print(json.dumps(result), flush=True)
     if comm is not None:
